@@ -1,0 +1,80 @@
+"""Oracle restatement of the vision encoders.
+
+TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+Parameters are plain dicts keyed by the reference state-dict names with the
+wrapper prefix stripped (``embeddings.cls_token``, ``layers.3.mlp.fc1.weight``,
+...), i.e. exactly ``ViTModel.state_dict()`` of transformers 5.15.0, which the
+reference's ``ViTEncoder`` wraps as ``self.model`` (src/models/encoders.py:103-104).
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+
+def vit_embeddings(p, images, patch_size):
+    """ViTPatchEmbeddings + ViTEmbeddings.forward
+    (transformers/models/vit/modeling_vit.py:60-69, 129-161):
+    Conv2d(k=s=patch) -> flatten(2).transpose(1,2) -> cat(CLS) -> + pos-emb.
+    Dropout is p=0 (ViTConfig.hidden_dropout_prob)."""
+    x = F.conv2d(images, p["embeddings.patch_embeddings.projection.weight"],
+                 p["embeddings.patch_embeddings.projection.bias"], stride=patch_size)
+    x = x.flatten(2).transpose(1, 2)
+    cls = p["embeddings.cls_token"].expand(x.shape[0], -1, -1)
+    x = torch.cat([cls, x], dim=1)
+    return x + p["embeddings.position_embeddings"]
+
+
+def mha_self(x, wq, bq, wk, bk, wv, bv, wo, bo, num_heads, causal=False, key_pad=None):
+    """Scaled-dot-product self attention with separate q/k/v projections
+    (ViTAttention, modeling_vit.py:207-238 + eager/sdpa 164-189): scale 1/sqrt(hd),
+    non-causal, no mask for ViT."""
+    B, N, D = x.shape
+    hd = D // num_heads
+    q = F.linear(x, wq, bq).view(B, N, num_heads, hd).transpose(1, 2)
+    k = F.linear(x, wk, bk).view(B, N, num_heads, hd).transpose(1, 2)
+    v = F.linear(x, wv, bv).view(B, N, num_heads, hd).transpose(1, 2)
+    s = torch.matmul(q, k.transpose(-1, -2)) / math.sqrt(hd)
+    if causal:
+        s = s.masked_fill(torch.ones(N, N, dtype=torch.bool).triu(1), float("-inf"))
+    if key_pad is not None:
+        s = s.masked_fill(key_pad[:, None, None, :], float("-inf"))
+    a = torch.softmax(s, dim=-1)
+    o = torch.matmul(a, v).transpose(1, 2).reshape(B, N, D)
+    return F.linear(o, wo, bo)
+
+
+def vit_layer(p, i, x, num_heads, eps):
+    """ViTLayer.forward (modeling_vit.py:266-286), pre-LN:
+    x += o_proj(SDPA(LN_before(x))); x += fc2(GELU_erf(fc1(LN_after(x))))."""
+    pre = f"layers.{i}."
+    D = x.shape[-1]
+    h = F.layer_norm(x, (D,), p[pre + "layernorm_before.weight"], p[pre + "layernorm_before.bias"], eps)
+    a = pre + "attention."
+    x = x + mha_self(h, p[a + "q_proj.weight"], p[a + "q_proj.bias"], p[a + "k_proj.weight"],
+                     p[a + "k_proj.bias"], p[a + "v_proj.weight"], p[a + "v_proj.bias"],
+                     p[a + "o_proj.weight"], p[a + "o_proj.bias"], num_heads)
+    h = F.layer_norm(x, (D,), p[pre + "layernorm_after.weight"], p[pre + "layernorm_after.bias"], eps)
+    h = F.gelu(F.linear(h, p[pre + "mlp.fc1.weight"], p[pre + "mlp.fc1.bias"]))
+    return x + F.linear(h, p[pre + "mlp.fc2.weight"], p[pre + "mlp.fc2.bias"])
+
+
+def vit_model(p, images, num_layers, num_heads, patch_size, eps=1e-12):
+    """ViTModel.forward (modeling_vit.py:336-381): embeddings -> layers -> final
+    layernorm (348) -> ViTPooler tanh(dense(h[:,0])) (289-301)."""
+    x = vit_embeddings(p, images, patch_size)
+    for i in range(num_layers):
+        x = vit_layer(p, i, x, num_heads, eps)
+    D = x.shape[-1]
+    seq = F.layer_norm(x, (D,), p["layernorm.weight"], p["layernorm.bias"], eps)
+    pooled = torch.tanh(F.linear(seq[:, 0], p["pooler.dense.weight"], p["pooler.dense.bias"]))
+    return seq, pooled
+
+
+def vit_encoder(p, images, num_layers, num_heads, patch_size, eps=1e-12):
+    """ViTEncoder.forward (src/models/encoders.py:118-137): features drop CLS
+    (122), proj = Identity when hidden == feature_dim (109-113), all-ones mask
+    (130-131; restated as None = no key padding)."""
+    seq, pooled = vit_model(p, images, num_layers, num_heads, patch_size, eps)
+    return {"features": seq[:, 1:], "pooled_features": pooled, "attention_mask": None}
