@@ -1,0 +1,162 @@
+#!/usr/bin/env python3
+"""Headline benchmark: config 3 of BASELINE.json — ViT-B/16 + Transformer decoder
+(6 layers, 8 heads) + multi-head attention, CE train step at bs=256 per GPU, bf16
+storage / fp32 accumulation, synthetic 224x224x3 images + 20-token captions.
+
+One step = forward + shifted CE + backward + (DP: gradient all-reduce over RCCL)
++ AdamW update + LR-schedule step, exactly the reference's
+CaptioningTrainer._train_epoch body (src/train/trainer.py:218-289).
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+N>1:    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "image-captioning-ml-project_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
+FLOP_PER_IMAGE = 120.7e9  # config-3 fwd+bwd algorithmic FLOPs per image
+
+
+def build(batch, device):
+    import capk
+    from capk import config as C
+    from capk.models import captioning_model as cm
+    from capk.train import CapkAdamW, CombinedLoss
+    torch.manual_seed(42)  # Config.seed (src/config.py:152)
+    cfg = C.Config()
+    cfg.model.encoder = C.EncoderConfig(encoder_type="vit", pretrained_model_name="google/vit-base-patch16-224")
+    cfg.model.decoder = C.DecoderConfig(decoder_type="transformer", hidden_dim=768, num_layers=6, num_heads=8)
+    cfg.model.attention = C.AttentionConfig(attention_type="multi_head")
+    cfg.model.vocab_size, cfg.model.pad_token_id = 50257, 50256  # GPT-2 tokenizer (src/main.py:160-168)
+    cfg.model.bos_token_id = cfg.model.eos_token_id = 50256
+    model = cm.ImageCaptioningModel(cfg)
+    cpu_sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    store = capk.prepare(model, device, "bf16")
+    opt = CapkAdamW(store, lr=cfg.training.learning_rate, weight_decay=cfg.training.weight_decay)
+    loss_fn = CombinedLoss(cfg.model.pad_token_id)
+    return cfg, model, store, opt, loss_fn, cpu_sd
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=4)
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    from capk import ops
+    from capk.train.dp import allreduce_grads
+    from capk.train.optim import cosine_schedule_with_warmup
+    cfg, model, store, opt, loss_fn, cpu_sd = build(args.batch, device)
+    B = args.batch
+    g = torch.Generator(device=device).manual_seed(0 + 1000 * rank)
+    images = torch.randn(B, 3, 224, 224, device=device, generator=g)
+    g1 = torch.Generator(device=device).manual_seed(1 + 1000 * rank)
+    captions = torch.randint(0, 50256, (B, 20), device=device, generator=g1)
+    total_steps = 10_000
+    step_no = [0]
+
+    def step():
+        out = model(images=images, captions=captions, caption_lengths=None)
+        loss = loss_fn(logits=out["logits"], targets=captions)["total_loss"]
+        loss.backward()
+        if world > 1:
+            allreduce_grads(store)
+        lr = cosine_schedule_with_warmup(step_no[0], cfg.training.learning_rate, cfg.training.warmup_steps,
+                                         total_steps)
+        opt.step(lr=lr)
+        step_no[0] += 1
+        return loss
+
+    for _ in range(args.warmup):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ops.GEMM_TIMER.start()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ops.GEMM_TIMER.stop()
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    gem = ops.GEMM_TIMER.summary()
+    final_loss = float(loss)
+
+    if rank == 0:
+        ms = elapsed / args.steps * 1e3
+        value = B * world * args.steps / elapsed
+        achieved = gem["avg_flops"] / (gem["avg_ms"] * 1e-3) / 1e12 if gem["launches"] else 0.0
+        rec = {
+            "metric": "images/sec train (ViT+Transformer bs=256) at 1/2/4/8 GPUs; beam-5 captions/sec",
+            "value": round(value, 2),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (randn 224x224x3 images, randint 20-token captions), random-init weights",
+            "config": {"workload": "config 3: ViT-B/16 + Transformer(6L,8H) + multi_head, CE train step",
+                       "global_batch": B * world, "per_gpu_batch": B, "seq_len": 20, "image_tokens": 197,
+                       "vocab": 50257, "parallelism": f"dp{world}"},
+            "roofline": {"bound": "mfma", "kernel": "gemm_bf16_kernel (all bf16 GEMM launches in the timed steps)",
+                         "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                         "launches": gem["launches"], "avg_launch_ms": round(gem["avg_ms"], 4),
+                         "gemm_share_of_step": round(gem["total_ms"] / (elapsed * 1e3), 3)},
+            "model_flops": {"per_image": FLOP_PER_IMAGE,
+                            "tflops": round(FLOP_PER_IMAGE * value / world / 1e12, 1),
+                            "frac_of_peak": round(FLOP_PER_IMAGE * value / world / 1e12 / PEAK_BF16_TFLOPS, 4)},
+            "final_loss": round(final_loss, 4),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            from oracle.step import time_cpu_baseline
+            threads = min(16, os.cpu_count() or 1)
+            ips, dt = time_cpu_baseline(cpu_sd, batch=args.cpu_batch, steps=args.cpu_steps, threads=threads)
+            rec["cpu_baseline"] = {"value": round(ips, 3), "unit": "images/s", "cores": threads, "kind": "port",
+                                   "sample": f"oracle fp32 CPU train step (torch CPU), batch {args.cpu_batch}, "
+                                             f"{args.cpu_steps} timed steps after 1 warm-up ({dt:.1f} s)"}
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

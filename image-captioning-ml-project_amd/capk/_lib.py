@@ -1,0 +1,89 @@
+"""ctypes binding of libcapk.so (the C ABI declared in include/capk.h).
+
+The product path has NO fallback: if the library is missing or was built for
+another architecture, every compute call raises.  Build with
+``make -C image-captioning-ml-project_amd/csrc`` (or ``__graft_entry__.build()``).
+"""
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcapk.so")
+
+F32 = 0
+BF16 = 1
+
+ACT_NONE, ACT_GELU_ERF, ACT_GELU_TANH, ACT_QUICK_GELU, ACT_TANH, ACT_RELU = 0, 1, 2, 3, 4, 5
+ACT_BWD = 16
+
+_c_p = ctypes.c_void_p
+_i = ctypes.c_int
+_i64 = ctypes.c_int64
+_f = ctypes.c_float
+_sz = ctypes.c_size_t
+
+# name -> (restype, [argtypes])  — must mirror include/capk.h exactly
+SIGNATURES = {
+    "capk_last_error": (ctypes.c_char_p, []),
+    "capk_version": (_i, []),
+    "capk_device_arch": (_i, [ctypes.c_char_p, _i]),
+    "capk_gemm_workspace": (_sz, [_i, _i, _i, _i, _i]),
+    "capk_gemm": (_i, [_i, _i, _i, _i, _i, _c_p, _i64, _i, _c_p, _i64, _i, _c_p, _i64, _f, _f,
+                       _c_p, _c_p, _i64, _i, _c_p, _c_p, _i64, _c_p, _sz, _c_p]),
+    "capk_layernorm_fwd": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _c_p, _f, _c_p, _i64, _c_p, _c_p, _c_p]),
+    "capk_layernorm_bwd_workspace": (_sz, [_i, _i]),
+    "capk_layernorm_bwd": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p, _c_p, _c_p, _c_p, _i64, _c_p, _i64,
+                                _c_p, _c_p, _i, _c_p, _sz, _c_p]),
+    "capk_attention_fwd": (_i, [_i, _i, _i, _i, _i, _i, _f, _i, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _i64,
+                                _i64, _c_p, _c_p, _i64, _i64, _c_p, _c_p]),
+    "capk_attention_bwd": (_i, [_i, _i, _i, _i, _i, _i, _f, _i, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _i64,
+                                _i64, _c_p, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _c_p, _i64, _i64, _c_p,
+                                _i64, _i64, _c_p, _i64, _i64, _c_p]),
+    "capk_patchify": (_i, [_i, _i, _i, _i, _i, _i, _c_p, _c_p, _c_p]),
+    "capk_vit_assemble": (_i, [_i, _i, _i, _i, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "capk_vit_assemble_bwd_workspace": (_sz, [_i, _i, _i]),
+    "capk_vit_assemble_bwd": (_i, [_i, _i, _i, _i, _c_p, _c_p, _c_p, _c_p, _c_p, _sz, _c_p]),
+    "capk_embedding_fwd": (_i, [_i, _i, _i, _i, _c_p, _c_p, _c_p, _i, _c_p, _c_p]),
+    "capk_embedding_bwd": (_i, [_i, _i, _i, _i, _c_p, _c_p, _i, _c_p, _c_p, _i, _c_p]),
+    "capk_shifted_ce_workspace": (_sz, [_i, _i]),
+    "capk_shifted_ce": (_i, [_i, _i, _i, _i, _i64, _c_p, _c_p, _i, _c_p, _c_p, _c_p, _c_p, _sz, _c_p]),
+    "capk_zero": (_i, [_c_p, _sz, _c_p]),
+    "capk_colsum_workspace": (_sz, [_i, _i]),
+    "capk_colsum": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i, _c_p, _sz, _c_p]),
+    "capk_cast": (_i, [_i, _i, _i64, _c_p, _c_p, _c_p]),
+    "capk_copy_rows": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p]),
+    "capk_act_bwd": (_i, [_i, _i64, _i, _c_p, _c_p, _c_p, _c_p]),
+    "capk_adamw": (_i, [_i64, _c_p, _c_p, _c_p, _c_p, _c_p, _f, _f, _f, _f, _f, _f, _f, _c_p]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class CapkError(RuntimeError):
+    pass
+
+
+def load(path=LIB_PATH):
+    """Load libcapk.so and bind every symbol of include/capk.h (raises if absent)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise CapkError(f"libcapk.so not found at {path}: build it with "
+                            f"`make -C image-captioning-ml-project_amd/csrc` (no CPU fallback exists)")
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = load().capk_last_error().decode(errors="replace")
+        raise CapkError(f"{what} failed (rc={rc}): {msg}")

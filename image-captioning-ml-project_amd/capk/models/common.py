@@ -1,0 +1,83 @@
+"""Shared pieces of the capk model modules: precision, parameter access, and the
+fused transformer building blocks (pre-/post-LN attention + MLP) expressed as
+sequences of libcapk kernel launches with explicit backward passes.
+
+Each block is a ``torch.autograd.Function`` whose backward writes parameter
+gradients straight into the flat fp32 gradient buffer of the ParamStore
+(``p._capk_grad``) and returns only the activation gradient; one parameter per
+block is passed as an "anchor" input so autograd schedules the backward.
+"""
+import torch
+import torch.nn as nn
+
+from .. import ops
+from ..ops import HeadView
+
+
+def compute_dtype(m):
+    return getattr(m, "_capk_dtype", torch.bfloat16)
+
+
+def W(p, dtype):
+    """Weight as the kernels consume it: bf16 shadow in bf16 mode, fp32 master otherwise."""
+    if dtype == torch.bfloat16:
+        return p._capk_bf16
+    return p.detach()
+
+
+def G(p):
+    return p._capk_grad
+
+
+def mark(p):
+    st = getattr(p, "_capk_store_ref", None)
+    if st is not None:
+        st.mark_written(p)
+
+
+def set_precision(model, dtype):
+    """'bf16' (throughput path) or 'fp32' (parity path) for every capk module."""
+    if isinstance(dtype, str):
+        dtype = {"bf16": torch.bfloat16, "fp32": torch.float32, "float32": torch.float32,
+                 "bfloat16": torch.bfloat16}[dtype]
+    for m in model.modules():
+        m._capk_dtype = dtype
+    return model
+
+
+class CapkModule(nn.Module):
+    """Base class: modules whose forward runs on libcapk kernels."""
+
+    @property
+    def cdtype(self):
+        return compute_dtype(self)
+
+    def _check_ready(self, p):
+        if not hasattr(p, "_capk_grad"):
+            raise RuntimeError("capk: parameters are not attached to a ParamStore; call "
+                               "capk.prepare(model, device) before running the model")
+
+
+def linear_bwd(dy, x, w_param, b_param, dtype, *, fused=None, need_dx=True, act_bwd=0, aux=None,
+               dw_accumulate=False):
+    """Backward of y = x W^T + b: dW, db into the grad buffer; returns dX (or None)."""
+    if fused is not None:
+        wmat, gw = fused[0].w(dtype), fused[0].grad
+        gb = fused[1].grad if fused[1] is not None else None
+    else:
+        wmat, gw = W(w_param, dtype), G(w_param)
+        gb = G(b_param) if b_param is not None else None
+    ops.linear_dw(dy, x, gw, accumulate=dw_accumulate)
+    if gb is not None:
+        ops.colsum(dy, gb, accumulate=dw_accumulate)
+    if not need_dx:
+        return None
+    return ops.linear_dx(dy, wmat, act_bwd=act_bwd, aux=aux)
+
+
+def heads(buf, col_off, B, N, row_stride_rows=None):
+    """HeadView over a [B*N, C] buffer for columns starting at col_off."""
+    C = buf.shape[1]
+    rs = C
+    bs = (row_stride_rows if row_stride_rows is not None else N) * C
+    return HeadView(buf, col_off, bs, rs)

@@ -1,0 +1,74 @@
+"""Caption-decoder plugin surface — mirrors src/models/decoders.py.
+
+``build_decoder(DecoderConfig, AttentionConfig, vocab_size, pad, bos, eos)`` and
+``CaptionDecoder.forward(encoder_features, captions, caption_lengths, **kw) ->
+{"logits": [B,T,V], ...}`` / ``.generate(encoder_features, max_length, **kw) ->
+(ids, info)`` keep the reference contract (decoders.py:20-69, 659-692).
+"""
+from abc import ABC, abstractmethod
+
+import torch
+import torch.nn as nn
+
+from ..config import AttentionConfig, DecoderConfig, DecoderType
+from .transformer import TransformerDecoderCore
+
+
+class CaptionDecoder(nn.Module, ABC):
+    """decoders.py:20-69."""
+
+    @abstractmethod
+    def forward(self, encoder_features, captions=None, caption_lengths=None, **kwargs):
+        ...
+
+    @abstractmethod
+    def generate(self, encoder_features, max_length, **kwargs):
+        ...
+
+
+class TransformerDecoder(TransformerDecoderCore, CaptionDecoder):
+    """decoders.py:317-493 on libcapk kernels."""
+
+    def __init__(self, config: DecoderConfig, vocab_size: int, pad_token_id: int, bos_token_id: int,
+                 eos_token_id: int):
+        TransformerDecoderCore.__init__(self, config.hidden_dim, config.num_layers, config.num_heads,
+                                        config.dropout, config.max_length, vocab_size, pad_token_id)
+        self.num_layers = config.num_layers
+        self.dropout_p = config.dropout
+        self.bos_token_id = bos_token_id
+        self.eos_token_id = eos_token_id
+
+    def forward(self, encoder_features, captions=None, caption_lengths=None, **kwargs):
+        if captions is None:
+            return self.generate(encoder_features, 50)  # decoders.py:378-380
+        # D4/D5: the encoder mask is all-ones (no padded image tokens) -> memory_key_padding_mask=None
+        logits, hidden = self.forward_logits(encoder_features["features"], captions)
+        return {"logits": logits, "hidden_states": hidden}
+
+    @torch.no_grad()
+    def generate(self, encoder_features, max_length, **kwargs):
+        """Greedy decoding (decoders.py:439-493): start from bos, append argmax of the
+        last position, stop when every sequence emitted eos.  Same arithmetic as the
+        reference's full re-decode per step (pad mask off: no pad in a generated prefix)."""
+        feats = encoder_features["features"]
+        B = feats.shape[0]
+        ids = torch.full((B, 1), self.bos_token_id, dtype=torch.long, device=feats.device)
+        for _ in range(max_length - 1):
+            logits, _ = self.forward_logits(feats, ids, use_pad_mask=False)
+            nxt = logits[:, -1, :].argmax(dim=-1, keepdim=True)
+            ids = torch.cat([ids, nxt], dim=1)
+            if bool((nxt == self.eos_token_id).all()):
+                break
+        return ids, {}
+
+
+def build_decoder(config: DecoderConfig, attention_config: AttentionConfig, vocab_size: int, pad_token_id: int,
+                  bos_token_id: int, eos_token_id: int) -> CaptionDecoder:
+    """decoders.py:659-692 (with D2: string types accepted; D3: attention hidden_dim filled)."""
+    dt = config.decoder_type if isinstance(config.decoder_type, DecoderType) else DecoderType(config.decoder_type)
+    attention_config.hidden_dim = config.hidden_dim
+    if dt == DecoderType.TRANSFORMER:
+        return TransformerDecoder(config, vocab_size, pad_token_id, bos_token_id, eos_token_id)
+    if dt in (DecoderType.LSTM, DecoderType.GPT2):
+        raise NotImplementedError(f"capk: decoder '{dt.value}' is scheduled after the Transformer hot path")
+    raise ValueError(f"Unsupported decoder type: {config.decoder_type}")

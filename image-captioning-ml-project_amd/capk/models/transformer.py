@@ -1,0 +1,261 @@
+"""Transformer caption decoder on libcapk kernels.
+
+Restates src/models/decoders.py:317-493 (TransformerDecoder) whose layers are
+torch ``nn.TransformerDecoderLayer`` (post-LN, GELU, batch_first;
+torch/nn/modules/transformer.py:985-1200).  Parameter names are identical to
+the reference state dict (``embedding``, ``position_encoding``,
+``transformer_decoder.layers.{i}.self_attn.in_proj_weight`` ..., ``output_layer``,
+``visual_projection``).
+
+The whole teacher-forced pass — token+position embedding, N post-LN layers,
+LM head — is ONE autograd Function, so the memory gradient shared by all
+cross-attention K/V projections is accumulated in place by beta=1 GEMM
+epilogues instead of by autograd adds.  The vocabulary dimension of the LM
+head is zero-padded to a multiple of 64 (``Vp``) inside the flat parameter
+store, so every LM-head GEMM runs on full tiles; the returned logits are a
+[B, T, V] view of the padded [B*T, Vp] buffer.
+
+Memory features may come with a row gap per batch element (the ViT sequence
+output minus its CLS row is a strided view): the K/V projection runs on the
+underlying rows and attention addresses batch b at row b*(S+gap) — no copy.
+"""
+import copy
+import math
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .._lib import ACT_GELU_ERF
+from .common import G, CapkModule, W, heads, linear_bwd
+from ..ops import HeadView
+
+
+def _pad64(v):
+    return (v + 63) // 64 * 64
+
+
+class _DecoderLayerParams(nn.Module):
+    """Parameter holder with nn.TransformerDecoderLayer's names (and its init)."""
+
+    def __init__(self, d, nhead, dff, dropout):
+        super().__init__()
+        ref = nn.TransformerDecoderLayer(d, nhead, dff, dropout, activation="gelu", batch_first=True)
+        self.self_attn = ref.self_attn
+        self.multihead_attn = ref.multihead_attn
+        self.linear1 = ref.linear1
+        self.linear2 = ref.linear2
+        self.norm1 = ref.norm1
+        self.norm2 = ref.norm2
+        self.norm3 = ref.norm3
+        self.nhead = nhead
+        self.dropout_p = dropout
+
+
+class _TransformerDecoderStack(nn.Module):
+    def __init__(self, layer, num_layers):
+        super().__init__()
+        # nn.TransformerDecoder deep-copies one layer: every layer starts from identical weights
+        self.layers = nn.ModuleList([copy.deepcopy(layer) for _ in range(num_layers)])
+        self.num_layers = num_layers
+
+
+class TransformerDecoderCore(CapkModule):
+    """Compute core used by capk.models.decoders.TransformerDecoder."""
+
+    def __init__(self, hidden_dim, num_layers, num_heads, dropout, max_length, vocab_size, pad_token_id):
+        super().__init__()
+        self.hidden_dim = hidden_dim
+        self.num_heads = num_heads
+        self.vocab_size = vocab_size
+        self.vocab_pad = _pad64(vocab_size)
+        self.pad_token_id = pad_token_id
+        self.embedding = nn.Embedding(vocab_size, hidden_dim, padding_idx=pad_token_id)
+        self.position_encoding = nn.Embedding(max_length, hidden_dim)
+        layer = _DecoderLayerParams(hidden_dim, num_heads, hidden_dim * 4, dropout)
+        self.transformer_decoder = _TransformerDecoderStack(layer, num_layers)
+        self.output_layer = nn.Linear(hidden_dim, vocab_size)
+        self.visual_projection = nn.Linear(hidden_dim, hidden_dim)
+        self.output_layer.weight._capk_pad_rows = self.vocab_pad
+        self.output_layer.bias._capk_pad_rows = self.vocab_pad
+
+    # -------------------------------------------------------------- forward
+    def forward_logits(self, features, captions, use_pad_mask=True):
+        """features [B,S,D] (row stride may include a gap), captions [B,T] int64 ->
+        (logits [B,T,V] view, hidden [B,T,D]).  use_pad_mask: tgt_key_padding_mask =
+        captions == pad (decoders.py:405); generate() passes none (decoders.py:473-477)."""
+        return _DecoderFn.apply(features, captions, self.visual_projection.weight, self, use_pad_mask)
+
+
+def _mem_geometry(features):
+    """Rows of the memory as a [M_ext, D] matrix over the features' own storage."""
+    B, S, D = features.shape
+    assert features.stride(2) == 1 and features.stride(1) == D, "features rows must be contiguous"
+    rows_per_b = features.stride(0) // D
+    assert features.stride(0) % D == 0 and rows_per_b >= S
+    M_ext = (B - 1) * rows_per_b + S
+    mem = features.as_strided((M_ext, D), (D, 1))
+    return mem, rows_per_b, M_ext
+
+
+class _DecoderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, features, captions, anchor, m, use_pad_mask):
+        ctx.set_materialize_grads(False)
+        dt = m.cdtype
+        B, S, D = features.shape
+        T = captions.shape[1]
+        H = m.num_heads
+        hd = D // H
+        scale = 1.0 / math.sqrt(hd)
+        V, Vp = m.vocab_size, m.vocab_pad
+        captions = captions.contiguous()
+        if features.dtype != dt:
+            raise TypeError(f"capk TransformerDecoder: features dtype {features.dtype} != compute dtype {dt}")
+        feat_mem, rpb, M_ext = _mem_geometry(features)
+        vp = m.visual_projection
+        mem = ops.linear(feat_mem, W(vp.weight, dt), vp.bias.detach())  # [M_ext, D]
+        tgt_pad = (captions == m.pad_token_id) if use_pad_mask else None  # bool [B,T] mask bookkeeping
+        x = ops.embedding_fwd(captions, m.embedding.weight.detach(), m.position_encoding.weight.detach(), 0, dt)
+        BT = B * T
+        saved_layers = []
+        for L in m.transformer_decoder.layers:
+            sa, ca = L.self_attn, L.multihead_attn
+            x_in = x
+            qkv = ops.linear(x, W(sa.in_proj_weight, dt), sa.in_proj_bias.detach())
+            a = torch.empty(BT, D, dtype=dt, device=x.device)
+            lse1, kp = ops.attention_fwd(heads(qkv, 0, B, T), heads(qkv, D, B, T), heads(qkv, 2 * D, B, T),
+                                         heads(a, 0, B, T), B, H, T, T, hd, scale, causal=True, key_pad=tgt_pad)
+            s1 = ops.linear(a, W(sa.out_proj.weight, dt), sa.out_proj.bias.detach(), residual=x)
+            x1, mu1, rs1 = ops.layernorm_fwd(s1, L.norm1.weight.detach(), L.norm1.bias.detach(), L.norm1.eps)
+            wca = W(ca.in_proj_weight, dt)
+            bca = ca.in_proj_bias.detach()
+            qc = ops.linear(x1, wca[:D], bca[:D])
+            kv = ops.linear(mem, wca[D:], bca[D:])  # [M_ext, 2D]
+            c = torch.empty(BT, D, dtype=dt, device=x.device)
+            kvh_k = HeadView(kv, 0, rpb * 2 * D, 2 * D)
+            kvh_v = HeadView(kv, D, rpb * 2 * D, 2 * D)
+            lse2, _ = ops.attention_fwd(heads(qc, 0, B, T), kvh_k, kvh_v, heads(c, 0, B, T), B, H, T, S, hd, scale)
+            s2 = ops.linear(c, W(ca.out_proj.weight, dt), ca.out_proj.bias.detach(), residual=x1)
+            x2, mu2, rs2 = ops.layernorm_fwd(s2, L.norm2.weight.detach(), L.norm2.bias.detach(), L.norm2.eps)
+            I = L.linear1.weight.shape[0]
+            f_pre = torch.empty(BT, I, dtype=dt, device=x.device)
+            f = ops.linear(x2, W(L.linear1.weight, dt), L.linear1.bias.detach(), act=ACT_GELU_ERF, preact=f_pre)
+            s3 = ops.linear(f, W(L.linear2.weight, dt), L.linear2.bias.detach(), residual=x2)
+            x, mu3, rs3 = ops.layernorm_fwd(s3, L.norm3.weight.detach(), L.norm3.bias.detach(), L.norm3.eps)
+            saved_layers.append((x_in, qkv, a, lse1, kp, s1, mu1, rs1, x1, qc, kv, c, lse2, s2, mu2, rs2, x2, f_pre,
+                                 f, s3, mu3, rs3))
+        ol = m.output_layer
+        wout = ol._capk_pad_bf16 if dt == torch.bfloat16 else ol._capk_pad_master
+        logits_pad = ops.linear(x, wout, _pad_bias(ol))
+        ctx.m = m
+        ctx.dims = (B, S, T, D, H, hd, scale, V, Vp, rpb, M_ext)
+        ctx.saved = (feat_mem, mem, captions, saved_layers, x)
+        ctx.features_meta = (features.shape, features.stride())
+        logits = logits_pad[:, :V].view(B, T, V)
+        hidden = x.view(B, T, D)
+        ctx.logits_pad = logits_pad
+        return logits, hidden
+
+    @staticmethod
+    def backward(ctx, dlogits, dhidden):
+        m = ctx.m
+        dt = m.cdtype
+        B, S, T, D, H, hd, scale, V, Vp, rpb, M_ext = ctx.dims
+        feat_mem, mem, captions, saved_layers, xT = ctx.saved
+        ctx.saved = None
+        BT = B * T
+        dev = xT.device
+        ol = m.output_layer
+        # ---- LM head
+        if dlogits is not None:
+            dl = _padded_grad(dlogits, ctx.logits_pad, BT, V, Vp)
+            ops.linear_dw(dl, xT, ol._capk_pad_grad)
+            ops.colsum(dl, _pad_bias_grad(ol))
+            wout = ol._capk_pad_bf16 if dt == torch.bfloat16 else ol._capk_pad_master
+            dx = ops.linear_dx(dl, wout)
+        else:
+            dx = torch.zeros(BT, D, dtype=dt, device=dev)
+            ops.zero_(ol._capk_pad_grad)
+            ops.zero_(_pad_bias_grad(ol))
+        if dhidden is not None:
+            dx = dx + dhidden.reshape(BT, D)
+        ctx.logits_pad = None
+        dmem = torch.empty(M_ext, D, dtype=dt, device=dev)
+        first = True
+        for li in range(len(saved_layers) - 1, -1, -1):
+            L = m.transformer_decoder.layers[li]
+            sa, ca = L.self_attn, L.multihead_attn
+            (x_in, qkv, a, lse1, kp, s1, mu1, rs1, x1, qc, kv, c, lse2, s2, mu2, rs2, x2, f_pre, f, s3, mu3,
+             rs3) = saved_layers[li]
+            saved_layers[li] = None
+            # norm3(x2 + FFN(x2))
+            ds3 = ops.layernorm_bwd(dx, s3, L.norm3.weight.detach(), mu3, rs3, G(L.norm3.weight), G(L.norm3.bias))
+            dfp = linear_bwd(ds3, f, L.linear2.weight, L.linear2.bias, dt, act_bwd=ACT_GELU_ERF, aux=f_pre)
+            ops.linear_dw(dfp, x2, G(L.linear1.weight))
+            ops.colsum(dfp, G(L.linear1.bias))
+            ops.linear_dx(dfp, W(L.linear1.weight, dt), out=ds3, beta=1.0)  # dx2 = ds3 + dfp W1
+            # norm2(x1 + MHA(x1, mem))
+            ds2 = ops.layernorm_bwd(ds3, s2, L.norm2.weight.detach(), mu2, rs2, G(L.norm2.weight), G(L.norm2.bias))
+            dc = linear_bwd(ds2, c, ca.out_proj.weight, ca.out_proj.bias, dt)
+            dqc = torch.empty(BT, D, dtype=dt, device=dev)
+            dkv = torch.empty(M_ext, 2 * D, dtype=dt, device=dev)
+            if rpb != S:
+                ops.zero_(dkv)  # gap rows (e.g. ViT CLS rows) get no K/V gradient
+            ops.attention_bwd(heads(qc, 0, B, T), HeadView(kv, 0, rpb * 2 * D, 2 * D),
+                              HeadView(kv, D, rpb * 2 * D, 2 * D), heads(c, 0, B, T), heads(dc, 0, B, T), lse2,
+                              heads(dqc, 0, B, T), HeadView(dkv, 0, rpb * 2 * D, 2 * D),
+                              HeadView(dkv, D, rpb * 2 * D, 2 * D), B, H, T, S, hd, scale)
+            gW, gB = G(ca.in_proj_weight), G(ca.in_proj_bias)
+            wca = W(ca.in_proj_weight, dt)
+            ops.linear_dw(dkv, mem, gW[D:])
+            ops.colsum(dkv, gB[D:])
+            ops.linear_dx(dkv, wca[D:], out=dmem, beta=0.0 if first else 1.0)
+            first = False
+            ops.linear_dw(dqc, x1, gW[:D])
+            ops.colsum(dqc, gB[:D])
+            ops.linear_dx(dqc, wca[:D], out=ds2, beta=1.0)  # dx1 = ds2 + dqc Wq
+            # norm1(x + SA(x))
+            ds1 = ops.layernorm_bwd(ds2, s1, L.norm1.weight.detach(), mu1, rs1, G(L.norm1.weight), G(L.norm1.bias))
+            da = linear_bwd(ds1, a, sa.out_proj.weight, sa.out_proj.bias, dt)
+            dqkv = torch.empty_like(qkv)
+            ops.attention_bwd(heads(qkv, 0, B, T), heads(qkv, D, B, T), heads(qkv, 2 * D, B, T), heads(a, 0, B, T),
+                              heads(da, 0, B, T), lse1, heads(dqkv, 0, B, T), heads(dqkv, D, B, T),
+                              heads(dqkv, 2 * D, B, T), B, H, T, T, hd, scale, causal=True, key_pad_u8=kp)
+            ops.linear_dw(dqkv, x_in, G(sa.in_proj_weight))
+            ops.colsum(dqkv, G(sa.in_proj_bias))
+            ops.linear_dx(dqkv, W(sa.in_proj_weight, dt), out=ds1, beta=1.0)  # dx = ds1 + dqkv Win
+            dx = ds1
+        # embeddings (scatter-add into zeroed grads; padding_idx rows skipped)
+        ops.zero_(G(m.embedding.weight))
+        ops.zero_(G(m.position_encoding.weight))
+        ops.embedding_bwd(captions, dx, m.pad_token_id, G(m.embedding.weight), G(m.position_encoding.weight), 0)
+        # visual projection
+        vp = m.visual_projection
+        # gap rows of dmem are exactly zero: every dkv gap row is zero (see above)
+        ops.linear_dw(dmem, feat_mem, G(vp.weight))
+        ops.colsum(dmem, G(vp.bias))
+        dfeat_mem = ops.linear_dx(dmem, W(vp.weight, dt))
+        shape, stride = ctx.features_meta
+        dfeatures = dfeat_mem.as_strided(shape, stride, 0)
+        return dfeatures, None, None, None, None
+
+
+def _pad_bias(ol):
+    return ol.bias._capk_pad_master
+
+
+def _pad_bias_grad(ol):
+    return ol.bias._capk_pad_grad
+
+
+def _padded_grad(dlogits, logits_pad, BT, V, Vp):
+    """The CE kernel writes its gradient into a padded [BT, Vp] buffer and hands back a
+    [B,T,V] view of it; recover that buffer (or pad a foreign gradient)."""
+    base = dlogits._base
+    if (base is not None and tuple(base.shape) == (BT, Vp) and base.data_ptr() == dlogits.data_ptr()
+            and base.is_contiguous()):
+        return base
+    out = torch.zeros(BT, Vp, dtype=logits_pad.dtype, device=logits_pad.device)
+    out[:, :V].copy_(dlogits.reshape(BT, V))
+    return out

@@ -1,0 +1,270 @@
+"""ViT / ViT-B-16 image encoder on libcapk kernels.
+
+Module tree and parameter names mirror transformers 5.15 ``ViTModel``
+(``embeddings.cls_token``, ``embeddings.position_embeddings``,
+``embeddings.patch_embeddings.projection``, ``layers.{i}.attention.{q,k,v,o}_proj``,
+``layers.{i}.layernorm_before/after``, ``layers.{i}.mlp.fc1/fc2``, ``layernorm``,
+``pooler.dense``) so reference checkpoints load unchanged.  The arithmetic is
+re-expressed as launches of hand-written gfx950 kernels:
+
+  patchify (im2col, HBM-bound) -> patch GEMM (MFMA) -> CLS/pos assembly
+  per layer: LN -> fused QKV GEMM (+bias) -> fused attention -> O GEMM (+bias+residual)
+             -> LN -> FC1 GEMM (+bias+GELU, pre-activation kept) -> FC2 GEMM (+bias+residual)
+  final LN -> pooler GEMM (+bias+tanh) on the CLS rows
+
+Activations live as [B*(N+1), D] row-major buffers; heads are addressed by
+stride, so there are no transposes anywhere.
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .._lib import ACT_GELU_ERF, ACT_TANH
+from ..params import Fused
+from .common import G, CapkModule, W, heads, linear_bwd, mark
+
+VIT_ARCHS = {
+    # pretrained_model_name -> architecture (weights are random-init offline or loaded from a checkpoint)
+    "google/vit-base-patch16-224": dict(hidden_size=768, num_hidden_layers=12, num_attention_heads=12,
+                                        intermediate_size=3072, image_size=224, patch_size=16, num_channels=3,
+                                        layer_norm_eps=1e-12),
+    "google/vit-base-patch16-224-in21k": dict(hidden_size=768, num_hidden_layers=12, num_attention_heads=12,
+                                              intermediate_size=3072, image_size=224, patch_size=16,
+                                              num_channels=3, layer_norm_eps=1e-12),
+    "google/vit-large-patch16-224": dict(hidden_size=1024, num_hidden_layers=24, num_attention_heads=16,
+                                         intermediate_size=4096, image_size=224, patch_size=16, num_channels=3,
+                                         layer_norm_eps=1e-12),
+}
+
+
+def _trunc(t, std=0.02):
+    nn.init.trunc_normal_(t, mean=0.0, std=std)
+
+
+class _PatchEmbeddings(nn.Module):
+    def __init__(self, a):
+        super().__init__()
+        self.projection = nn.Conv2d(a["num_channels"], a["hidden_size"], a["patch_size"], a["patch_size"])
+
+
+class _Embeddings(nn.Module):
+    def __init__(self, a):
+        super().__init__()
+        n = (a["image_size"] // a["patch_size"]) ** 2
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, a["hidden_size"]))
+        self.position_embeddings = nn.Parameter(torch.zeros(1, n + 1, a["hidden_size"]))
+        self.patch_embeddings = _PatchEmbeddings(a)
+
+
+class _Attention(nn.Module):
+    def __init__(self, d):
+        super().__init__()
+        self.q_proj = nn.Linear(d, d)
+        self.k_proj = nn.Linear(d, d)
+        self.v_proj = nn.Linear(d, d)
+        self.o_proj = nn.Linear(d, d)
+        self.qkv_w = Fused([self.q_proj.weight, self.k_proj.weight, self.v_proj.weight])
+        self.qkv_b = Fused([self.q_proj.bias, self.k_proj.bias, self.v_proj.bias])
+
+    def _capk_fused_groups(self):
+        return [self.qkv_w, self.qkv_b]
+
+
+class _MLP(nn.Module):
+    def __init__(self, d, i):
+        super().__init__()
+        self.fc1 = nn.Linear(d, i)
+        self.fc2 = nn.Linear(i, d)
+
+
+class ViTLayer(CapkModule):
+    def __init__(self, a):
+        super().__init__()
+        d = a["hidden_size"]
+        self.num_heads = a["num_attention_heads"]
+        self.eps = a["layer_norm_eps"]
+        self.attention = _Attention(d)
+        self.layernorm_before = nn.LayerNorm(d, eps=self.eps)
+        self.layernorm_after = nn.LayerNorm(d, eps=self.eps)
+        self.mlp = _MLP(d, a["intermediate_size"])
+
+    def forward(self, x, B, N):
+        return _ViTLayerFn.apply(x, self.attention.o_proj.weight, self, B, N)
+
+
+class _Pooler(nn.Module):
+    def __init__(self, d):
+        super().__init__()
+        self.dense = nn.Linear(d, d)
+
+
+class CapkViTModel(CapkModule):
+    """ViTModel (modeling_vit.py:336-381) with add_pooling_layer=True."""
+
+    def __init__(self, arch):
+        super().__init__()
+        self.arch = dict(arch)
+        self.config = type("ViTArch", (), dict(arch))()
+        self.embeddings = _Embeddings(arch)
+        self.layers = nn.ModuleList([ViTLayer(arch) for _ in range(arch["num_hidden_layers"])])
+        self.layernorm = nn.LayerNorm(arch["hidden_size"], eps=arch["layer_norm_eps"])
+        self.pooler = _Pooler(arch["hidden_size"])
+        self._init_weights()
+
+    def _init_weights(self):
+        # ViTPreTrainedModel._init_weights: trunc-normal(0.02) weights, zero bias, LN 1/0
+        for m in self.modules():
+            if isinstance(m, (nn.Linear, nn.Conv2d)):
+                _trunc(m.weight.data)
+                nn.init.zeros_(m.bias)
+            elif isinstance(m, nn.LayerNorm):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+        _trunc(self.embeddings.cls_token.data)
+        _trunc(self.embeddings.position_embeddings.data)
+
+    def _capk_optional_params(self):
+        # the pooler receives no gradient when the decoder ignores pooled_features
+        return [self.pooler.dense.weight, self.pooler.dense.bias]
+
+    def forward(self, images):
+        """images [B,C,H,W] -> (sequence_output [B*(N+1), D] flat, pooled [B, D])."""
+        a = self.arch
+        B = images.shape[0]
+        P = a["patch_size"]
+        Np = (images.shape[2] // P) * (images.shape[3] // P)
+        N = Np + 1
+        x = _ViTEmbedFn.apply(images, self.embeddings.patch_embeddings.projection.weight, self, B, Np)
+        for layer in self.layers:
+            x = layer(x, B, N)
+        seq, pooled = _ViTHeadFn.apply(x, self.layernorm.weight, self, B, N)
+        return seq, pooled
+
+
+# --------------------------------------------------------------- functions --
+class _ViTEmbedFn(torch.autograd.Function):
+    """Patch conv as im2col + GEMM, then CLS + position embeddings (modeling_vit.py:60-69,129-161)."""
+
+    @staticmethod
+    def forward(ctx, images, anchor, m, B, Np):
+        dt = m.cdtype
+        P = m.arch["patch_size"]
+        D = m.arch["hidden_size"]
+        proj = m.embeddings.patch_embeddings.projection
+        patches = ops.patchify(images, P, dt)
+        pe = ops.linear(patches, W(proj.weight, dt).view(D, -1), proj.bias.detach())
+        x = ops.vit_assemble(pe, m.embeddings.cls_token.detach(), m.embeddings.position_embeddings.detach(), B, Np,
+                             D)
+        ctx.m, ctx.B, ctx.Np = m, B, Np
+        ctx.patches = patches
+        return x
+
+    @staticmethod
+    def backward(ctx, dx):
+        m, B, Np = ctx.m, ctx.B, ctx.Np
+        D = m.arch["hidden_size"]
+        dx = dx.contiguous()
+        emb = m.embeddings
+        dpatch = ops.vit_assemble_bwd(dx, B, Np, D, G(emb.cls_token).view(-1), G(emb.position_embeddings).view(-1))
+        proj = emb.patch_embeddings.projection
+        ops.linear_dw(dpatch, ctx.patches, G(proj.weight).view(D, -1))
+        ops.colsum(dpatch, G(proj.bias))
+        ctx.patches = None
+        return None, None, None, None, None
+
+
+class _ViTLayerFn(torch.autograd.Function):
+    """ViTLayer.forward (modeling_vit.py:266-286), pre-LN."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, L, B, N):
+        dt = L.cdtype
+        D = x.shape[1]
+        H = L.num_heads
+        hd = D // H
+        at, mlp = L.attention, L.mlp
+        ln1, ln2 = L.layernorm_before, L.layernorm_after
+        h1, mu1, rs1 = ops.layernorm_fwd(x, ln1.weight.detach(), ln1.bias.detach(), L.eps)
+        qkv = ops.linear(h1, at.qkv_w.w(dt), at.qkv_b.master)
+        o = torch.empty(x.shape[0], D, dtype=x.dtype, device=x.device)
+        lse, _ = ops.attention_fwd(heads(qkv, 0, B, N), heads(qkv, D, B, N), heads(qkv, 2 * D, B, N),
+                                   heads(o, 0, B, N), B, H, N, N, hd, 1.0 / math.sqrt(hd))
+        x1 = ops.linear(o, W(at.o_proj.weight, dt), at.o_proj.bias.detach(), residual=x)
+        h2, mu2, rs2 = ops.layernorm_fwd(x1, ln2.weight.detach(), ln2.bias.detach(), L.eps)
+        I = mlp.fc1.weight.shape[0]
+        f_pre = torch.empty(x.shape[0], I, dtype=x.dtype, device=x.device)
+        f = ops.linear(h2, W(mlp.fc1.weight, dt), mlp.fc1.bias.detach(), act=ACT_GELU_ERF, preact=f_pre)
+        y = ops.linear(f, W(mlp.fc2.weight, dt), mlp.fc2.bias.detach(), residual=x1)
+        ctx.L, ctx.B, ctx.N = L, B, N
+        ctx.saved = (x, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, f_pre, f)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        L, B, N = ctx.L, ctx.B, ctx.N
+        dt = L.cdtype
+        x, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, f_pre, f = ctx.saved
+        ctx.saved = None
+        dy = dy.contiguous()
+        D = x.shape[1]
+        H = L.num_heads
+        hd = D // H
+        at, mlp = L.attention, L.mlp
+        ln1, ln2 = L.layernorm_before, L.layernorm_after
+        dfp = linear_bwd(dy, f, mlp.fc2.weight, mlp.fc2.bias, dt, act_bwd=ACT_GELU_ERF, aux=f_pre)
+        dh2 = linear_bwd(dfp, h2, mlp.fc1.weight, mlp.fc1.bias, dt)
+        dx1 = ops.layernorm_bwd(dh2, x1, ln2.weight.detach(), mu2, rs2, G(ln2.weight), G(ln2.bias), dres=dy)
+        do = linear_bwd(dx1, o, at.o_proj.weight, at.o_proj.bias, dt)
+        dqkv = torch.empty_like(qkv)
+        ops.attention_bwd(heads(qkv, 0, B, N), heads(qkv, D, B, N), heads(qkv, 2 * D, B, N), heads(o, 0, B, N),
+                          heads(do, 0, B, N), lse, heads(dqkv, 0, B, N), heads(dqkv, D, B, N),
+                          heads(dqkv, 2 * D, B, N), B, H, N, N, hd, 1.0 / math.sqrt(hd))
+        dh1 = linear_bwd(dqkv, h1, None, None, dt, fused=(at.qkv_w, at.qkv_b))
+        dx = ops.layernorm_bwd(dh1, x, ln1.weight.detach(), mu1, rs1, G(ln1.weight), G(ln1.bias), dres=dx1)
+        return dx, None, None, None, None
+
+
+class _ViTHeadFn(torch.autograd.Function):
+    """Final layernorm (modeling_vit.py:348) + ViTPooler tanh(dense(h[:,0])) (289-301)."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, m, B, N):
+        ctx.set_materialize_grads(False)
+        dt = m.cdtype
+        D = x.shape[1]
+        ln = m.layernorm
+        seq, mu, rs = ops.layernorm_fwd(x, ln.weight.detach(), ln.bias.detach(), ln.eps)
+        cls_rows = seq.view(B, N, D)[:, 0]
+        pre = torch.empty(B, D, dtype=seq.dtype, device=seq.device)
+        dense = m.pooler.dense
+        pooled = ops.linear(cls_rows, W(dense.weight, dt), dense.bias.detach(), act=ACT_TANH, preact=pre)
+        ctx.m, ctx.B, ctx.N = m, B, N
+        ctx.saved = (x, mu, rs, seq, pre)
+        return seq, pooled
+
+    @staticmethod
+    def backward(ctx, dseq, dpooled):
+        m, B, N = ctx.m, ctx.B, ctx.N
+        dt = m.cdtype
+        x, mu, rs, seq, pre = ctx.saved
+        ctx.saved = None
+        D = x.shape[1]
+        if dseq is None:
+            dseq = torch.zeros_like(seq)
+        else:
+            dseq = dseq.contiguous().clone() if dpooled is not None else dseq.contiguous()
+        if dpooled is not None:
+            dense = m.pooler.dense
+            dpre = ops.act_bwd(dpooled.contiguous(), pre, ACT_TANH)
+            cls_rows = seq.view(B, N, D)[:, 0]
+            ops.linear_dw(dpre, cls_rows, G(dense.weight))
+            ops.colsum(dpre, G(dense.bias))
+            mark(dense.weight)
+            mark(dense.bias)
+            dcls = dseq.view(B, N, D)[:, 0]
+            ops.linear_dx(dpre, W(dense.weight, dt), out=dcls, beta=1.0)
+        ln = m.layernorm
+        dx = ops.layernorm_bwd(dseq, x, ln.weight.detach(), mu, rs, G(ln.weight), G(ln.bias))
+        return dx, None, None, None, None

@@ -1,0 +1,287 @@
+"""Tensor-level wrappers over the C ABI (device pointers + current HIP stream).
+
+Every function here launches hand-written HIP kernels from libcapk.so on
+``torch.cuda.current_stream()``; torch is used only for memory (caching
+allocator), streams and autograd bookkeeping.  There is deliberately no CPU or
+eager-PyTorch fallback: a missing library or a non-GPU tensor raises.
+"""
+import torch
+
+from . import _lib
+from ._lib import ACT_BWD, BF16, F32, check  # noqa: F401
+
+_DT = {torch.float32: F32, torch.bfloat16: BF16}
+
+
+def dtype_code(t):
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise _lib.CapkError(f"capk: unsupported dtype {t.dtype}")
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _need_gpu(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise _lib.CapkError("capk ops need device (HIP) tensors; there is no CPU path")
+
+
+def _ws(nbytes, device):
+    if nbytes == 0:
+        return None
+    return torch.empty(int(nbytes), dtype=torch.uint8, device=device)
+
+
+def lib():
+    return _lib.load()
+
+
+# ------------------------------------------------------------------- GEMM ---
+class KernelTimer:
+    """Optional HIP-event bracketing of every GEMM launch on the current stream
+    (bench.py's live roofline measurement).  Off by default: zero overhead."""
+
+    def __init__(self):
+        self.enabled = False
+        self.records = []  # (start_event, end_event, flops, in_dtype)
+
+    def start(self):
+        self.records = []
+        self.enabled = True
+
+    def stop(self):
+        self.enabled = False
+
+    def summary(self):
+        torch.cuda.synchronize()
+        tot_ms, tot_flops, n = 0.0, 0.0, 0
+        for s, e, fl, _ in self.records:
+            tot_ms += s.elapsed_time(e)
+            tot_flops += fl
+            n += 1
+        return {"launches": n, "total_ms": tot_ms, "flops": tot_flops,
+                "avg_ms": tot_ms / max(n, 1), "avg_flops": tot_flops / max(n, 1)}
+
+
+GEMM_TIMER = KernelTimer()
+
+
+def gemm(A, a_kmajor, B, b_kmajor, M, N, K, C, *, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=None,
+         residual=None, ldr=0, act=0, preact=None, aux=None, ldx=0):
+    """C[m,n] = alpha*sum_k A(m,k)B(n,k) + beta*C + bias + residual -> act (see capk.h)."""
+    _need_gpu(A, B, C)
+    L = lib()
+    it, ot = dtype_code(A), dtype_code(C)
+    wsb = L.capk_gemm_workspace(it, ot, M, N, K)
+    ws = _ws(wsb, A.device)
+    timed = GEMM_TIMER.enabled
+    if timed:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    rc = L.capk_gemm(it, ot, M, N, K, _p(A), lda, int(a_kmajor), _p(B), ldb, int(b_kmajor), _p(C), ldc,
+                     float(alpha), float(beta), _p(bias), _p(residual), ldr, int(act), _p(preact), _p(aux), ldx,
+                     _p(ws), wsb if ws is not None else 0, _stream())
+    check(rc, "capk_gemm")
+    if timed:
+        ev1.record()
+        GEMM_TIMER.records.append((ev0, ev1, 2.0 * M * N * K, it))
+    return C
+
+
+def linear(x, w, b=None, *, out=None, residual=None, act=0, preact=None, out_dtype=None):
+    """y = x @ w^T + b (+ residual) (act); x [M,K] (row stride may exceed K), w [N,K] contiguous."""
+    M, K = x.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=out_dtype or x.dtype, device=x.device)
+    gemm(x, True, w, True, M, N, K, out, lda=x.stride(0), ldb=w.stride(0), ldc=out.stride(0), bias=b,
+         residual=residual, ldr=residual.stride(0) if residual is not None else 0, act=act, preact=preact,
+         ldx=preact.stride(0) if preact is not None else 0)
+    return out
+
+
+def linear_dx(dy, w, *, out=None, act_bwd=0, aux=None, beta=0.0):
+    """dX[M,K] = dY[M,N] @ W[N,K]  (optionally * act'(aux) for a fused activation backward)."""
+    M, N = dy.shape
+    K = w.shape[1]
+    if out is None:
+        out = torch.empty(M, K, dtype=dy.dtype, device=dy.device)
+    gemm(dy, True, w, False, M, K, N, out, lda=dy.stride(0), ldb=w.stride(0), ldc=out.stride(0), beta=beta,
+         act=(ACT_BWD | act_bwd) if act_bwd else 0, aux=aux, ldx=aux.stride(0) if aux is not None else 0)
+    return out
+
+
+def linear_dw(dy, x, dw, *, accumulate=False):
+    """dW[N,K] (fp32) (+)= dY[M,N]^T @ X[M,K]."""
+    M, N = dy.shape
+    K = x.shape[1]
+    gemm(dy, False, x, False, N, K, M, dw, lda=dy.stride(0), ldb=x.stride(0), ldc=dw.stride(0),
+         beta=1.0 if accumulate else 0.0)
+    return dw
+
+
+def colsum(dy, out, accumulate=False):
+    """out[n] (+)= sum_m dy[m, n] (bias gradient, fp32)."""
+    _need_gpu(dy, out)
+    L = lib()
+    M, N = dy.shape
+    wsb = L.capk_colsum_workspace(M, N)
+    ws = _ws(wsb, dy.device)
+    check(L.capk_colsum(dtype_code(dy), M, N, _p(dy), dy.stride(0), _p(out), int(accumulate), _p(ws), wsb,
+                        _stream()), "capk_colsum")
+    return out
+
+
+# -------------------------------------------------------------- LayerNorm ---
+def layernorm_fwd(x, w, b, eps, out=None):
+    _need_gpu(x)
+    rows, cols = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+    check(lib().capk_layernorm_fwd(dtype_code(x), rows, cols, _p(x), x.stride(0), _p(w), _p(b), float(eps),
+                                   _p(out), out.stride(0), _p(mean), _p(rstd), _stream()), "capk_layernorm_fwd")
+    return out, mean, rstd
+
+
+def layernorm_bwd(dy, x, w, mean, rstd, dw, db, *, dres=None, out=None, accumulate=False):
+    L = lib()
+    rows, cols = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    wsb = L.capk_layernorm_bwd_workspace(rows, cols)
+    ws = _ws(wsb, x.device)
+    check(L.capk_layernorm_bwd(dtype_code(x), rows, cols, _p(dy), dy.stride(0), _p(x), x.stride(0), _p(w),
+                               _p(mean), _p(rstd), _p(out), out.stride(0), _p(dres),
+                               dres.stride(0) if dres is not None else 0, _p(dw), _p(db), int(accumulate),
+                               _p(ws), wsb, _stream()), "capk_layernorm_bwd")
+    return out
+
+
+# -------------------------------------------------------------- attention ---
+class HeadView:
+    """A [B, N, H*hd] token view inside a larger buffer: base tensor + offsets (elements)."""
+
+    __slots__ = ("t", "off", "bs", "rs")
+
+    def __init__(self, t, off, bs, rs):
+        self.t, self.off, self.bs, self.rs = t, off, bs, rs
+
+    def ptr(self):
+        return self.t.data_ptr() + self.off * self.t.element_size()
+
+
+def attention_fwd(q, k, v, o, B, H, Nq, Nk, hd, scale, causal=False, key_pad=None):
+    """q/k/v/o: HeadView.  Returns lse [B,H,Nq] fp32."""
+    lse = torch.empty(B, H, Nq, dtype=torch.float32, device=q.t.device)
+    kp = None if key_pad is None else key_pad.to(torch.uint8).contiguous()
+    check(lib().capk_attention_fwd(dtype_code(q.t), B, H, Nq, Nk, hd, float(scale), int(causal),
+                                   q.ptr(), q.bs, q.rs, k.ptr(), k.bs, k.rs, v.ptr(), v.bs, v.rs, _p(kp),
+                                   o.ptr(), o.bs, o.rs, _p(lse), _stream()), "capk_attention_fwd")
+    return lse, kp
+
+
+def attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Nq, Nk, hd, scale, causal=False, key_pad_u8=None):
+    check(lib().capk_attention_bwd(dtype_code(q.t), B, H, Nq, Nk, hd, float(scale), int(causal),
+                                   q.ptr(), q.bs, q.rs, k.ptr(), k.bs, k.rs, v.ptr(), v.bs, v.rs,
+                                   _p(key_pad_u8), o.ptr(), o.bs, o.rs, do.ptr(), do.bs, do.rs, _p(lse),
+                                   dq.ptr(), dq.bs, dq.rs, dk.ptr(), dk.bs, dk.rs, dv.ptr(), dv.bs, dv.rs,
+                                   _stream()), "capk_attention_bwd")
+
+
+# ------------------------------------------------------ embeddings / misc ---
+def patchify(images, P, out_dtype):
+    B, C, H, W = images.shape
+    _need_gpu(images)
+    out = torch.empty(B * (H // P) * (W // P), C * P * P, dtype=out_dtype, device=images.device)
+    img = images.contiguous().float()
+    check(lib().capk_patchify(_DT[out_dtype], B, C, H, W, P, _p(img), _p(out), _stream()), "capk_patchify")
+    return out
+
+
+def vit_assemble(patch_out, cls, pos, B, Np, D):
+    x = torch.empty(B * (Np + 1), D, dtype=patch_out.dtype, device=patch_out.device)
+    check(lib().capk_vit_assemble(dtype_code(patch_out), B, Np, D, _p(patch_out), _p(cls), _p(pos), _p(x),
+                                  _stream()), "capk_vit_assemble")
+    return x
+
+
+def vit_assemble_bwd(dx, B, Np, D, dcls, dpos):
+    L = lib()
+    dpatch = torch.empty(B * Np, D, dtype=dx.dtype, device=dx.device)
+    wsb = L.capk_vit_assemble_bwd_workspace(B, Np, D)
+    ws = _ws(wsb, dx.device)
+    check(L.capk_vit_assemble_bwd(dtype_code(dx), B, Np, D, _p(dx), _p(dpatch), _p(dcls), _p(dpos), _p(ws), wsb,
+                                  _stream()), "capk_vit_assemble_bwd")
+    return dpatch
+
+
+def embedding_fwd(ids, table, pos, pos_offset, out_dtype):
+    B, T = ids.shape
+    D = table.shape[1]
+    out = torch.empty(B * T, D, dtype=out_dtype, device=table.device)
+    check(lib().capk_embedding_fwd(_DT[out_dtype], B, T, D, _p(ids), _p(table), _p(pos), int(pos_offset), _p(out),
+                                   _stream()), "capk_embedding_fwd")
+    return out
+
+
+def embedding_bwd(ids, dout, padding_idx, dtable, dpos, pos_offset=0):
+    B, T = ids.shape
+    D = dout.shape[1]
+    check(lib().capk_embedding_bwd(dtype_code(dout), B, T, D, _p(ids), _p(dout),
+                                   -1 if padding_idx is None else int(padding_idx), _p(dtable), _p(dpos),
+                                   int(pos_offset), _stream()), "capk_embedding_bwd")
+
+
+def shifted_ce(logits2d, targets, B, T, V, ignore_index, *, want_loss=True, dlogits=None, grad_scale=None):
+    """loss fp32 [2] = (mean, count) if want_loss; fills dlogits (times *grad_scale, a device scalar)."""
+    L = lib()
+    loss = torch.empty(2, dtype=torch.float32, device=logits2d.device) if want_loss else None
+    wsb = L.capk_shifted_ce_workspace(B, T)
+    ws = _ws(wsb, logits2d.device)
+    check(L.capk_shifted_ce(dtype_code(logits2d), B, T, V, logits2d.stride(0), _p(logits2d), _p(targets),
+                            int(ignore_index), _p(grad_scale), _p(loss), _p(dlogits), _p(ws), wsb, _stream()),
+          "capk_shifted_ce")
+    return loss
+
+
+def zero_(t):
+    check(lib().capk_zero(_p(t), t.numel() * t.element_size(), _stream()), "capk_zero")
+    return t
+
+
+def cast(x, out):
+    check(lib().capk_cast(dtype_code(x), dtype_code(out), x.numel(), _p(x), _p(out), _stream()), "capk_cast")
+    return out
+
+
+def copy_rows(x, out):
+    rows, cols = x.shape
+    check(lib().capk_copy_rows(dtype_code(x), rows, cols, _p(x), x.stride(0), _p(out), out.stride(0), _stream()),
+          "capk_copy_rows")
+    return out
+
+
+def act_bwd(dy, aux, act, out=None):
+    if out is None:
+        out = torch.empty_like(dy)
+    check(lib().capk_act_bwd(dtype_code(dy), dy.numel(), int(act), _p(dy), _p(aux), _p(out), _stream()),
+          "capk_act_bwd")
+    return out
+
+
+def adamw(param, grad, m, v, param_bf16, lr, wd, beta1, beta2, eps, step):
+    bc1 = 1.0 - beta1 ** step
+    bc2 = 1.0 - beta2 ** step
+    check(lib().capk_adamw(param.numel(), _p(param), _p(grad), _p(m), _p(v), _p(param_bf16), float(lr), float(wd),
+                           float(beta1), float(beta2), float(eps), float(bc1), float(bc2), _stream()), "capk_adamw")

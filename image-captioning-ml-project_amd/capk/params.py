@@ -1,0 +1,189 @@
+"""Flat parameter storage for the capk hot path.
+
+Every parameter of a model is re-homed into one of two flat fp32 *master*
+buffers — weight-decay and no-weight-decay, following the reference's AdamW
+group rule (src/train/trainer.py:114-128) — with a parallel flat fp32 gradient
+buffer and a flat bf16 *shadow* used by the bf16 kernels.  ``p.data``,
+``p.grad``, ``p._capk_grad`` and ``p._capk_bf16`` are views into those buffers,
+so:
+
+* the fused AdamW kernel updates a whole group in one launch and refreshes the
+  bf16 shadow in the same pass (no separate cast kernel per step);
+* parameters that are consumed together (q/k/v projections) are laid out
+  adjacently and exposed as one fused [3D, D] matrix (``Fused``), so the QKV
+  projection is a single GEMM;
+* data-parallel gradient all-reduce works on large contiguous buckets.
+
+Parameters that the reference leaves without a gradient in some
+configurations (the ViT pooler when the decoder ignores ``pooled_features``:
+torch AdamW then skips them) are placed at the tail of their buffer and marked
+optional; the optimizer only updates them in steps where a backward wrote them.
+"""
+import torch
+
+ALIGN = 16  # elements: keeps every view 64-B (fp32) / 32-B (bf16) aligned
+
+
+def no_decay(name):
+    """trainer.py:114-128: names containing 'bias' or 'LayerNorm.weight' skip weight decay."""
+    return any(nd in name for nd in ("bias", "LayerNorm.weight"))
+
+
+def _round(n):
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+def _alloc_numel(p):
+    pr = getattr(p, "_capk_pad_rows", None)
+    if pr:
+        assert pr >= p.shape[0]
+        return pr * (p.numel() // p.shape[0])
+    return p.numel()
+
+
+class Fused:
+    """Adjacent parameters exposed as one matrix: master / bf16 / grad views."""
+
+    def __init__(self, params):
+        self.params = list(params)
+        self.master = self.bf16 = self.grad = None
+
+    def w(self, dtype):
+        return self.bf16 if dtype == torch.bfloat16 else self.master
+
+
+class ParamStore:
+    def __init__(self, model, device, bf16_shadow=True):
+        self.device = torch.device(device)
+        named = list(model.named_parameters())
+        names = {id(p): n for n, p in named}
+        fused = []
+        for m in model.modules():
+            fn = getattr(m, "_capk_fused_groups", None)
+            if fn is not None:
+                fused.extend(fn())
+        in_fused = {}
+        for f in fused:
+            for p in f.params:
+                in_fused[id(p)] = f
+        self.groups = {"decay": [], "no_decay": []}
+        self.optional = set()
+        for m in model.modules():
+            for p in getattr(m, "_capk_optional_params", lambda: [])():
+                self.optional.add(id(p))
+        # order: fused groups first (kept adjacent), then the rest in registration order;
+        # optional-grad parameters last within each buffer
+        seen = set()
+        order = []
+        for f in fused:
+            for p in f.params:
+                if id(p) not in seen:
+                    seen.add(id(p))
+                    order.append(p)
+        for _, p in named:
+            if id(p) not in seen:
+                seen.add(id(p))
+                order.append(p)
+        for p in order:
+            g = "no_decay" if no_decay(names[id(p)]) else "decay"
+            self.groups[g].append(p)
+        for g in self.groups:
+            self.groups[g].sort(key=lambda p: id(p) in self.optional)  # stable: optional to the tail
+        self.master, self.grad, self.bf16, self.offsets = {}, {}, {}, {}
+        self.required_numel = {}
+        self.params = []
+        self.names = {}
+        for g, plist in self.groups.items():
+            total = sum(_round(_alloc_numel(p)) for p in plist)
+            master = torch.zeros(max(total, ALIGN), dtype=torch.float32, device=self.device)
+            grad = torch.zeros_like(master)
+            shadow = torch.zeros(master.numel(), dtype=torch.bfloat16, device=self.device) if bf16_shadow else None
+            off = 0
+            req = 0
+            for p in plist:
+                n = p.numel()
+                with torch.no_grad():
+                    master[off:off + n].copy_(p.detach().reshape(-1).to(self.device, torch.float32))
+                p.data = master[off:off + n].view(p.shape)
+                p._capk_grad = grad[off:off + n].view(p.shape)
+                p.grad = p._capk_grad
+                if shadow is not None:
+                    p._capk_bf16 = shadow[off:off + n].view(p.shape)
+                pr = getattr(p, "_capk_pad_rows", None)
+                if pr:
+                    # zero-padded row extension (e.g. vocab rounded up for the GEMM tiles)
+                    pshape = (pr,) + tuple(p.shape[1:])
+                    npad = _alloc_numel(p)
+                    p._capk_pad_master = master[off:off + npad].view(pshape)
+                    p._capk_pad_grad = grad[off:off + npad].view(pshape)
+                    p._capk_pad_bf16 = None if shadow is None else shadow[off:off + npad].view(pshape)
+                p._capk_store_ref = self
+                p._capk_group = g
+                p._capk_offset = off
+                self.offsets[id(p)] = (g, off)
+                self.names[id(p)] = names[id(p)]
+                off += _round(_alloc_numel(p))
+                if id(p) not in self.optional:
+                    req = off
+                self.params.append(p)
+            self.master[g], self.grad[g], self.bf16[g] = master, grad, shadow
+            self.required_numel[g] = req
+        for f in fused:
+            self._bind_fused(f)
+        self.written_optional = set()
+        self.refresh_shadow()
+
+    def _bind_fused(self, f):
+        g, off0 = self.offsets[id(f.params[0])]
+        off = off0
+        for p in f.params:
+            assert self.offsets[id(p)] == (g, off), "fused parameters must be adjacent in one group"
+            off += _round(p.numel())
+            assert _round(p.numel()) == p.numel(), "fused parameters must have ALIGN-multiple sizes"
+        rows = sum(p.shape[0] for p in f.params)
+        shape = (rows,) + tuple(f.params[0].shape[1:])
+        n = off - off0
+        f.master = self.master[g][off0:off0 + n].view(shape)
+        f.grad = self.grad[g][off0:off0 + n].view(shape)
+        f.bf16 = None if self.bf16[g] is None else self.bf16[g][off0:off0 + n].view(shape)
+
+    def refresh_shadow(self):
+        """Re-derive the bf16 shadow after the master weights changed outside the optimizer."""
+        from . import ops
+        for g in self.groups:
+            if self.bf16[g] is not None and self.master[g].is_cuda:
+                ops.cast(self.master[g], self.bf16[g])
+            elif self.bf16[g] is not None:
+                self.bf16[g].copy_(self.master[g])
+
+    def mark_written(self, p):
+        if id(p) in self.optional:
+            self.written_optional.add(id(p))
+
+    def relink_grads(self):
+        for p in self.params:
+            if p.grad is None or p.grad.data_ptr() != p._capk_grad.data_ptr():
+                p.grad = p._capk_grad
+
+    def segments(self, group):
+        """[(key, start, end)] ranges of `group` to update this step.  Keys are stable so the
+        optimizer can keep per-range step counts (torch AdamW keeps a step count per
+        parameter; optional parameters advance only in steps that produced a gradient)."""
+        segs = [((group, "required"), 0, self.required_numel[group])] if self.required_numel[group] else []
+        for p in self.groups[group]:
+            if id(p) in self.optional and id(p) in self.written_optional:
+                off = p._capk_offset
+                segs.append(((group, off), off, off + _round(_alloc_numel(p))))
+        return segs
+
+
+def store_of(module):
+    return getattr(module, "_capk_store", None)
+
+
+def attach(model, device, bf16_shadow=True):
+    """Build the ParamStore for `model` and remember it on every submodule."""
+    st = ParamStore(model, device, bf16_shadow)
+    for m in model.modules():
+        m._capk_store = st
+    return st

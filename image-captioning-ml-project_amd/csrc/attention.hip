@@ -1,0 +1,550 @@
+// Fused multi-head attention forward/backward for short sequences
+// (ViT N=197, CLIP N=50, decoder T=20 self / T x 196 cross).  One workgroup per
+// (batch, head); the whole K/V (fwd) or Q/K/V/dO (bwd) of that head is staged
+// in LDS once, so S = QK^T never reaches HBM.
+//
+// bf16 path (v_mfma_f32_16x16x32_bf16):
+//  fwd: each wave owns 16-query tiles and computes S^T = K Q^T so that every
+//       lane holds one query's scores (column = lane&15); row max / sum need
+//       only two xor-shuffles (16, 32).  P^T stays in registers and is the B
+//       operand of O^T = V^T P^T with the k (=key) order permuted to match the
+//       accumulator layout; V is staged transposed (Vt[d][key]) so the A operand
+//       is two ds_read_b64.  LSE is saved for backward.
+//  bwd: phase A (waves own 16-key blocks): S, dP, dS recomputed with the key on
+//       the lane; dV^T += dO^T P and dK^T += Q^T dS take dO^T / Q^T from the
+//       row-major LDS images via ds_read_b64_tr_b16.  Phase B (waves own 16-query
+//       blocks): S^T, dP^T recomputed; dQ^T += K^T dS^T (K^T by tr reads).  No
+//       atomics: every output element has one owner.
+// f32 path (parity): straightforward per-query / per-key loops, exact fp32.
+#include "common.h"
+
+namespace capk {
+
+struct AttnArgs {
+  int B, H, Nq, Nk, hd, causal;
+  float scale;
+  const void *q, *k, *v, *o, *dout;
+  int64_t q_bs, q_rs, k_bs, k_rs, v_bs, v_rs, o_bs, o_rs, do_bs, do_rs;
+  const uint8_t* key_pad;
+  void* out;
+  int64_t out_bs, out_rs;
+  float* lse;
+  const float* lse_in;
+  void *dq, *dk, *dv;
+  int64_t dq_bs, dq_rs, dk_bs, dk_rs, dv_bs, dv_rs;
+};
+
+__device__ __forceinline__ bool key_ok(const AttnArgs& a, int b, int key, int q) {
+  if (key >= a.Nk) return false;
+  if (a.causal && key > q) return false;
+  if (a.key_pad && a.key_pad[(int64_t)b * a.Nk + key]) return false;
+  return true;
+}
+
+__device__ __forceinline__ bf16x8 ld8(const bf16* p) { return *(const bf16x8*)p; }
+__device__ __forceinline__ bf16x8 zero8() {
+  bf16x8 z;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) z[i] = (bf16)0.f;
+  return z;
+}
+__device__ __forceinline__ bf16x8 pack8(const f32x4& a, const f32x4& b) {
+  bf16x8 r;
+  r[0] = (bf16)a[0]; r[1] = (bf16)a[1]; r[2] = (bf16)a[2]; r[3] = (bf16)a[3];
+  r[4] = (bf16)b[0]; r[5] = (bf16)b[1]; r[6] = (bf16)b[2]; r[7] = (bf16)b[3];
+  return r;
+}
+__device__ __forceinline__ void store4(bf16* p, const f32x4& v, float s) {
+  bf16x4 r;
+  r[0] = (bf16)(v[0] * s); r[1] = (bf16)(v[1] * s); r[2] = (bf16)(v[2] * s); r[3] = (bf16)(v[3] * s);
+  *(bf16x4*)p = r;
+}
+// transposed 4x16 block read: rows r0..r0+3 (lane-group local), columns c0..c0+15
+__device__ __forceinline__ bf16x4 tr_read(const bf16* img, int st, int r0, int c0, int lane) {
+  const int i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+  const bf16* a = img + (r0 + q) * st + c0 + 4 * p;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, a));
+}
+__device__ __forceinline__ bf16x8 tr_read8(const bf16* img, int st, int r0, int c0, int lane) {
+  // logical k = 8g + j  <->  rows r0 + 4g + j (j<4), r0 + 16 + 4g + (j-4) (j>=4)
+  const int g = lane >> 4;
+  bf16x4 x0 = tr_read(img, st, r0 + 4 * g, c0, lane);
+  bf16x4 x1 = tr_read(img, st, r0 + 16 + 4 * g, c0, lane);
+  bf16x8 r;
+  r[0] = x0[0]; r[1] = x0[1]; r[2] = x0[2]; r[3] = x0[3];
+  r[4] = x1[0]; r[5] = x1[1]; r[6] = x1[2]; r[7] = x1[3];
+  return r;
+}
+
+// stage rows [0, NP) x [0, HDP) of one head into a row-major LDS image (stride st)
+template <int HDP>
+__device__ __forceinline__ void stage_rows(bf16* img, int st, const bf16* src, int64_t bs_off, int64_t rs, int n,
+                                           int NP, int hoff, int hd) {
+  constexpr int NCH = HDP / 8;
+  for (int c = threadIdx.x; c < NP * NCH; c += blockDim.x) {
+    const int r = c / NCH, dc = c % NCH;
+    bf16x8 v = zero8();
+    if (r < n && dc * 8 < hd) v = ld8(src + bs_off + (int64_t)r * rs + hoff + dc * 8);
+    *(bf16x8*)(img + r * st + dc * 8) = v;
+  }
+}
+
+template <int HDP>
+__global__ __launch_bounds__(256) void attn_fwd_bf16(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int NKP = (a.Nk + 31) & ~31;
+  const int KST = HDP + 8, VST = NKP + 8;
+  bf16* Ks = (bf16*)smem;
+  bf16* Vt = Ks + NKP * KST;
+  const int hoff = h * a.hd;
+  stage_rows<HDP>(Ks, KST, (const bf16*)a.k, (int64_t)b * a.k_bs, a.k_rs, a.Nk, NKP, hoff, a.hd);
+  {
+    constexpr int NCH = HDP / 8;
+    const bf16* vsrc = (const bf16*)a.v + (int64_t)b * a.v_bs + hoff;
+    for (int c = threadIdx.x; c < NKP * NCH; c += blockDim.x) {
+      const int r = c / NCH, dc = c % NCH;
+      bf16x8 v = zero8();
+      if (r < a.Nk && dc * 8 < a.hd) v = ld8(vsrc + (int64_t)r * a.v_rs + dc * 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) Vt[(dc * 8 + i) * VST + r] = v[i];
+    }
+  }
+  __syncthreads();
+
+  const int NKB = NKP / 16;
+  const bf16* qsrc = (const bf16*)a.q + (int64_t)b * a.q_bs + hoff;
+  for (int qt = wave; qt * 16 < a.Nq; qt += 4) {
+    const int qi = qt * 16 + (lane & 15);
+    bf16x8 qf[HDP / 32];
+#pragma unroll
+    for (int s = 0; s < HDP / 32; ++s) {
+      const int d = s * 32 + 8 * (lane >> 4);
+      qf[s] = (qi < a.Nq && d < a.hd) ? ld8(qsrc + (int64_t)qi * a.q_rs + d) : zero8();
+    }
+    f32x4 sc[16];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 16; ++kb) {
+      if (kb < NKB) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < HDP / 32; ++s) {
+          bf16x8 kf = *(const bf16x8*)(Ks + (kb * 16 + (lane & 15)) * KST + s * 32 + 8 * (lane >> 4));
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kb * 16 + (lane >> 4) * 4 + r;
+          acc[r] = key_ok(a, b, key, qi) ? acc[r] * a.scale : -INFINITY;
+          mx = fmaxf(mx, acc[r]);
+        }
+        sc[kb] = acc;
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float l = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 16; ++kb) {
+      if (kb < NKB) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = __expf(sc[kb][r] - mx);
+          sc[kb][r] = p;
+          l += p;
+        }
+      }
+    }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    f32x4 o[HDP / 16];
+#pragma unroll
+    for (int db = 0; db < HDP / 16; ++db) o[db] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      if (2 * t < NKB) {
+        const bf16x8 pb = pack8(sc[2 * t], sc[2 * t + 1]);
+#pragma unroll
+        for (int db = 0; db < HDP / 16; ++db) {
+          const bf16* vr = Vt + (db * 16 + (lane & 15)) * VST + 32 * t + 4 * (lane >> 4);
+          bf16x4 v0 = *(const bf16x4*)vr, v1 = *(const bf16x4*)(vr + 16);
+          bf16x8 va;
+          va[0] = v0[0]; va[1] = v0[1]; va[2] = v0[2]; va[3] = v0[3];
+          va[4] = v1[0]; va[5] = v1[1]; va[6] = v1[2]; va[7] = v1[3];
+          o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, o[db], 0, 0, 0);
+        }
+      }
+    }
+    if (qi < a.Nq) {
+      const float inv = 1.f / l;
+      bf16* orow = (bf16*)a.out + (int64_t)b * a.out_bs + (int64_t)qi * a.out_rs + hoff;
+#pragma unroll
+      for (int db = 0; db < HDP / 16; ++db) {
+        const int d0 = db * 16 + (lane >> 4) * 4;
+        if (d0 < a.hd) store4(orow + d0, o[db], inv);
+      }
+      if ((lane >> 4) == 0) a.lse[((int64_t)b * a.H + h) * a.Nq + qi] = mx + __logf(l);
+    }
+  }
+}
+
+template <int HDP>
+__global__ __launch_bounds__(256) void attn_bwd_bf16(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int NQP = (a.Nq + 31) & ~31, NKP = (a.Nk + 31) & ~31;
+  constexpr int ST = HDP + 8;
+  bf16* Qs = (bf16*)smem;
+  bf16* dOs = Qs + NQP * ST;
+  bf16* Ks = dOs + NQP * ST;
+  bf16* Vs = Ks + NKP * ST;
+  float* lse_s = (float*)(Vs + NKP * ST);
+  float* del_s = lse_s + NQP;
+  const int hoff = h * a.hd;
+  stage_rows<HDP>(Qs, ST, (const bf16*)a.q, (int64_t)b * a.q_bs, a.q_rs, a.Nq, NQP, hoff, a.hd);
+  stage_rows<HDP>(dOs, ST, (const bf16*)a.dout, (int64_t)b * a.do_bs, a.do_rs, a.Nq, NQP, hoff, a.hd);
+  stage_rows<HDP>(Ks, ST, (const bf16*)a.k, (int64_t)b * a.k_bs, a.k_rs, a.Nk, NKP, hoff, a.hd);
+  stage_rows<HDP>(Vs, ST, (const bf16*)a.v, (int64_t)b * a.v_bs, a.v_rs, a.Nk, NKP, hoff, a.hd);
+  // delta_q = sum_d dO*O (fp32), one wave per query row
+  for (int q = wave; q < NQP; q += 4) {
+    float s = 0.f;
+    if (q < a.Nq) {
+      const bf16* orow = (const bf16*)a.o + (int64_t)b * a.o_bs + (int64_t)q * a.o_rs + hoff;
+      const bf16* drow = (const bf16*)a.dout + (int64_t)b * a.do_bs + (int64_t)q * a.do_rs + hoff;
+      for (int d = lane; d < a.hd; d += 64) s += (float)orow[d] * (float)drow[d];
+    }
+    s = wave_sum(s);
+    if (lane == 0) {
+      del_s[q] = s;
+      lse_s[q] = q < a.Nq ? a.lse_in[((int64_t)b * a.H + h) * a.Nq + q] : 0.f;
+    }
+  }
+  __syncthreads();
+
+  // ---- phase A: dK, dV (waves own 16-key blocks)
+  for (int kb = wave; kb < NKP / 16; kb += 4) {
+    const int keyl = kb * 16 + (lane & 15);
+    f32x4 dvt[HDP / 16], dkt[HDP / 16];
+#pragma unroll
+    for (int db = 0; db < HDP / 16; ++db) dvt[db] = dkt[db] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < NQP / 32; ++t) {
+      f32x4 p[2], ds[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int qa = t * 32 + c * 16 + (lane & 15);
+        f32x4 s_acc = {0.f, 0.f, 0.f, 0.f}, dp_acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < HDP / 32; ++s) {
+          const int d = s * 32 + 8 * (lane >> 4);
+          s_acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(Qs + qa * ST + d),
+                                                          *(const bf16x8*)(Ks + keyl * ST + d), s_acc, 0, 0, 0);
+          dp_acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(dOs + qa * ST + d),
+                                                           *(const bf16x8*)(Vs + keyl * ST + d), dp_acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = t * 32 + c * 16 + (lane >> 4) * 4 + r;
+          const bool ok = q < a.Nq && key_ok(a, b, keyl, q);
+          const float pv = ok ? __expf(s_acc[r] * a.scale - lse_s[q]) : 0.f;
+          p[c][r] = pv;
+          ds[c][r] = pv * (dp_acc[r] - del_s[q]);
+        }
+      }
+      const bf16x8 pb = pack8(p[0], p[1]), dsb = pack8(ds[0], ds[1]);
+#pragma unroll
+      for (int db = 0; db < HDP / 16; ++db) {
+        dvt[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_read8(dOs, ST, t * 32, db * 16, lane), pb, dvt[db], 0, 0, 0);
+        dkt[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_read8(Qs, ST, t * 32, db * 16, lane), dsb, dkt[db], 0, 0, 0);
+      }
+    }
+    if (keyl < a.Nk) {
+      bf16* dkrow = (bf16*)a.dk + (int64_t)b * a.dk_bs + (int64_t)keyl * a.dk_rs + hoff;
+      bf16* dvrow = (bf16*)a.dv + (int64_t)b * a.dv_bs + (int64_t)keyl * a.dv_rs + hoff;
+#pragma unroll
+      for (int db = 0; db < HDP / 16; ++db) {
+        const int d0 = db * 16 + (lane >> 4) * 4;
+        if (d0 < a.hd) {
+          store4(dkrow + d0, dkt[db], a.scale);
+          store4(dvrow + d0, dvt[db], 1.f);
+        }
+      }
+    }
+  }
+
+  // ---- phase B: dQ (waves own 16-query blocks)
+  for (int qb = wave; qb < NQP / 16; qb += 4) {
+    const int ql = qb * 16 + (lane & 15);
+    const float lq = lse_s[ql], dq_del = del_s[ql];
+    f32x4 dqt[HDP / 16];
+#pragma unroll
+    for (int db = 0; db < HDP / 16; ++db) dqt[db] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < NKP / 32; ++t) {
+      f32x4 ds[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int ka = t * 32 + c * 16 + (lane & 15);
+        f32x4 s_acc = {0.f, 0.f, 0.f, 0.f}, dp_acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < HDP / 32; ++s) {
+          const int d = s * 32 + 8 * (lane >> 4);
+          s_acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(Ks + ka * ST + d),
+                                                          *(const bf16x8*)(Qs + ql * ST + d), s_acc, 0, 0, 0);
+          dp_acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(Vs + ka * ST + d),
+                                                           *(const bf16x8*)(dOs + ql * ST + d), dp_acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = t * 32 + c * 16 + (lane >> 4) * 4 + r;
+          const bool ok = ql < a.Nq && key_ok(a, b, key, ql);
+          const float pv = ok ? __expf(s_acc[r] * a.scale - lq) : 0.f;
+          ds[c][r] = pv * (dp_acc[r] - dq_del);
+        }
+      }
+      const bf16x8 dsb = pack8(ds[0], ds[1]);
+#pragma unroll
+      for (int db = 0; db < HDP / 16; ++db)
+        dqt[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_read8(Ks, ST, t * 32, db * 16, lane), dsb, dqt[db], 0, 0, 0);
+    }
+    if (ql < a.Nq) {
+      bf16* dqrow = (bf16*)a.dq + (int64_t)b * a.dq_bs + (int64_t)ql * a.dq_rs + hoff;
+#pragma unroll
+      for (int db = 0; db < HDP / 16; ++db) {
+        const int d0 = db * 16 + (lane >> 4) * 4;
+        if (d0 < a.hd) store4(dqrow + d0, dqt[db], a.scale);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------ f32 parity path
+template <int HD>
+__global__ __launch_bounds__(64) void attn_fwd_f32(AttnArgs a) {
+  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
+  const int q = blockIdx.y * 64 + threadIdx.x;
+  if (q >= a.Nq) return;
+  const int hoff = h * HD;
+  const float* qr = (const float*)a.q + (int64_t)b * a.q_bs + (int64_t)q * a.q_rs + hoff;
+  const float* kb = (const float*)a.k + (int64_t)b * a.k_bs + hoff;
+  const float* vb = (const float*)a.v + (int64_t)b * a.v_bs + hoff;
+  float qv[HD], o[HD];
+#pragma unroll
+  for (int d = 0; d < HD; ++d) { qv[d] = qr[d]; o[d] = 0.f; }
+  float mx = -INFINITY;
+  for (int j = 0; j < a.Nk; ++j) {
+    if (!key_ok(a, b, j, q)) continue;
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < HD; ++d) s += qv[d] * kb[(int64_t)j * a.k_rs + d];
+    mx = fmaxf(mx, s * a.scale);
+  }
+  float l = 0.f;
+  for (int j = 0; j < a.Nk; ++j) {
+    if (!key_ok(a, b, j, q)) continue;
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < HD; ++d) s += qv[d] * kb[(int64_t)j * a.k_rs + d];
+    const float p = expf(s * a.scale - mx);
+    l += p;
+#pragma unroll
+    for (int d = 0; d < HD; ++d) o[d] += p * vb[(int64_t)j * a.v_rs + d];
+  }
+  float* orow = (float*)a.out + (int64_t)b * a.out_bs + (int64_t)q * a.out_rs + hoff;
+#pragma unroll
+  for (int d = 0; d < HD; ++d) orow[d] = o[d] / l;
+  a.lse[((int64_t)b * a.H + h) * a.Nq + q] = mx + logf(l);
+}
+
+template <int HD>
+__global__ __launch_bounds__(64) void attn_bwd_dq_f32(AttnArgs a) {
+  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
+  const int q = blockIdx.y * 64 + threadIdx.x;
+  if (q >= a.Nq) return;
+  const int hoff = h * HD;
+  const float* qr = (const float*)a.q + (int64_t)b * a.q_bs + (int64_t)q * a.q_rs + hoff;
+  const float* orow = (const float*)a.o + (int64_t)b * a.o_bs + (int64_t)q * a.o_rs + hoff;
+  const float* dorow = (const float*)a.dout + (int64_t)b * a.do_bs + (int64_t)q * a.do_rs + hoff;
+  const float* kb = (const float*)a.k + (int64_t)b * a.k_bs + hoff;
+  const float* vb = (const float*)a.v + (int64_t)b * a.v_bs + hoff;
+  float qv[HD], dov[HD], dq[HD];
+  float del = 0.f;
+#pragma unroll
+  for (int d = 0; d < HD; ++d) { qv[d] = qr[d]; dov[d] = dorow[d]; dq[d] = 0.f; del += dov[d] * orow[d]; }
+  const float lse = a.lse_in[((int64_t)b * a.H + h) * a.Nq + q];
+  for (int j = 0; j < a.Nk; ++j) {
+    if (!key_ok(a, b, j, q)) continue;
+    float s = 0.f, dp = 0.f;
+#pragma unroll
+    for (int d = 0; d < HD; ++d) {
+      s += qv[d] * kb[(int64_t)j * a.k_rs + d];
+      dp += dov[d] * vb[(int64_t)j * a.v_rs + d];
+    }
+    const float p = expf(s * a.scale - lse);
+    const float ds = p * (dp - del);
+#pragma unroll
+    for (int d = 0; d < HD; ++d) dq[d] += ds * kb[(int64_t)j * a.k_rs + d];
+  }
+  float* dqrow = (float*)a.dq + (int64_t)b * a.dq_bs + (int64_t)q * a.dq_rs + hoff;
+#pragma unroll
+  for (int d = 0; d < HD; ++d) dqrow[d] = dq[d] * a.scale;
+}
+
+template <int HD>
+__global__ __launch_bounds__(64) void attn_bwd_dkv_f32(AttnArgs a) {
+  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
+  const int j = blockIdx.y * 64 + threadIdx.x;
+  if (j >= a.Nk) return;
+  const int hoff = h * HD;
+  const float* krow = (const float*)a.k + (int64_t)b * a.k_bs + (int64_t)j * a.k_rs + hoff;
+  const float* vrow = (const float*)a.v + (int64_t)b * a.v_bs + (int64_t)j * a.v_rs + hoff;
+  float kv[HD], vv[HD], dk[HD], dv[HD];
+#pragma unroll
+  for (int d = 0; d < HD; ++d) { kv[d] = krow[d]; vv[d] = vrow[d]; dk[d] = 0.f; dv[d] = 0.f; }
+  for (int q = 0; q < a.Nq; ++q) {
+    if (!key_ok(a, b, j, q)) continue;
+    const float* qr = (const float*)a.q + (int64_t)b * a.q_bs + (int64_t)q * a.q_rs + hoff;
+    const float* orow = (const float*)a.o + (int64_t)b * a.o_bs + (int64_t)q * a.o_rs + hoff;
+    const float* dorow = (const float*)a.dout + (int64_t)b * a.do_bs + (int64_t)q * a.do_rs + hoff;
+    float s = 0.f, dp = 0.f, del = 0.f;
+#pragma unroll
+    for (int d = 0; d < HD; ++d) {
+      s += qr[d] * kv[d];
+      dp += dorow[d] * vv[d];
+      del += dorow[d] * orow[d];
+    }
+    const float p = expf(s * a.scale - a.lse_in[((int64_t)b * a.H + h) * a.Nq + q]);
+    const float ds = p * (dp - del);
+#pragma unroll
+    for (int d = 0; d < HD; ++d) {
+      dv[d] += p * dorow[d];
+      dk[d] += ds * qr[d];
+    }
+  }
+  float* dkrow = (float*)a.dk + (int64_t)b * a.dk_bs + (int64_t)j * a.dk_rs + hoff;
+  float* dvrow = (float*)a.dv + (int64_t)b * a.dv_bs + (int64_t)j * a.dv_rs + hoff;
+#pragma unroll
+  for (int d = 0; d < HD; ++d) { dkrow[d] = dk[d] * a.scale; dvrow[d] = dv[d]; }
+}
+
+static size_t fwd_smem(int Nk, int hdp) {
+  const int NKP = (Nk + 31) & ~31;
+  return (size_t)NKP * (hdp + 8) * 2 + (size_t)hdp * (NKP + 8) * 2;
+}
+static size_t bwd_smem(int Nq, int Nk, int hdp) {
+  const int NQP = (Nq + 31) & ~31, NKP = (Nk + 31) & ~31;
+  return (size_t)(2 * NQP + 2 * NKP) * (hdp + 8) * 2 + (size_t)2 * NQP * 4;
+}
+
+template <typename K>
+static int launch_dyn(K kernel, dim3 grid, dim3 block, size_t shm, hipStream_t st, const AttnArgs& a,
+                      const char* name) {
+  if (shm > 65536) {
+    hipError_t e = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    if (e != hipSuccess) return hip_status(e, name);
+  }
+  hipLaunchKernelGGL(kernel, grid, block, shm, st, a);
+  CAPK_LAUNCH_CHECK(name);
+  return CAPK_OK;
+}
+
+static int hdp_of(int hd) { return hd <= 32 ? 32 : hd <= 64 ? 64 : hd <= 96 ? 96 : 128; }
+
+static int check_common(int dtype, int B, int H, int Nq, int Nk, int hd) {
+  CAPK_CHECK_ARG(B > 0 && H > 0 && Nq > 0 && Nk > 0, "capk_attention: bad sizes");
+  CAPK_CHECK_ARG(Nq <= 256 && Nk <= 256, "capk_attention: Nq, Nk <= 256 (got %d, %d)", Nq, Nk);
+  CAPK_CHECK_ARG(hd % 8 == 0 && hd <= 128, "capk_attention: hd=%d must be a multiple of 8, <= 128", hd);
+  CAPK_CHECK_ARG(dtype == CAPK_BF16 || dtype == CAPK_F32, "capk_attention: dtype");
+  return CAPK_OK;
+}
+
+#define F32_HD_DISPATCH(KERNEL, grid, ...)                                                           \
+  switch (a.hd) {                                                                                   \
+    case 8: hipLaunchKernelGGL(KERNEL<8>, grid, dim3(64), 0, st, a); break;                         \
+    case 16: hipLaunchKernelGGL(KERNEL<16>, grid, dim3(64), 0, st, a); break;                       \
+    case 32: hipLaunchKernelGGL(KERNEL<32>, grid, dim3(64), 0, st, a); break;                       \
+    case 64: hipLaunchKernelGGL(KERNEL<64>, grid, dim3(64), 0, st, a); break;                       \
+    case 96: hipLaunchKernelGGL(KERNEL<96>, grid, dim3(64), 0, st, a); break;                       \
+    case 128: hipLaunchKernelGGL(KERNEL<128>, grid, dim3(64), 0, st, a); break;                     \
+    default: set_error("capk_attention(f32): hd=%d unsupported", a.hd); return CAPK_EUNSUPPORTED;   \
+  }
+
+}  // namespace capk
+
+using namespace capk;
+
+extern "C" int capk_attention_fwd(int dtype, int B, int H, int Nq, int Nk, int hd, float scale, int causal,
+                                  const void* q, int64_t q_bs, int64_t q_rs, const void* k, int64_t k_bs,
+                                  int64_t k_rs, const void* v, int64_t v_bs, int64_t v_rs, const uint8_t* key_pad,
+                                  void* o, int64_t o_bs, int64_t o_rs, float* lse, void* stream) {
+  int rc = check_common(dtype, B, H, Nq, Nk, hd);
+  if (rc) return rc;
+  AttnArgs a{};
+  a.B = B; a.H = H; a.Nq = Nq; a.Nk = Nk; a.hd = hd; a.causal = causal; a.scale = scale;
+  a.q = q; a.k = k; a.v = v; a.q_bs = q_bs; a.q_rs = q_rs; a.k_bs = k_bs; a.k_rs = k_rs; a.v_bs = v_bs; a.v_rs = v_rs;
+  a.key_pad = key_pad; a.out = o; a.out_bs = o_bs; a.out_rs = o_rs; a.lse = lse;
+  hipStream_t st = S(stream);
+  if (dtype == CAPK_F32) {
+    dim3 grid(B * H, cdiv(Nq, 64));
+    F32_HD_DISPATCH(attn_fwd_f32, grid);
+    CAPK_LAUNCH_CHECK("attn_fwd_f32");
+    return CAPK_OK;
+  }
+  CAPK_CHECK_ARG(q_rs % 8 == 0 && k_rs % 8 == 0 && v_rs % 8 == 0 && o_rs % 4 == 0 && q_bs % 8 == 0 &&
+                     k_bs % 8 == 0 && v_bs % 8 == 0,
+                 "capk_attention_fwd(bf16): strides must allow 16-B vector access");
+  const int hdp = hdp_of(hd);
+  const size_t shm = fwd_smem(Nk, hdp);
+  const dim3 grid(B * H), block(256);
+  switch (hdp) {
+    case 32: return launch_dyn(attn_fwd_bf16<32>, grid, block, shm, st, a, "attn_fwd_bf16");
+    case 64: return launch_dyn(attn_fwd_bf16<64>, grid, block, shm, st, a, "attn_fwd_bf16");
+    case 96: return launch_dyn(attn_fwd_bf16<96>, grid, block, shm, st, a, "attn_fwd_bf16");
+    default: return launch_dyn(attn_fwd_bf16<128>, grid, block, shm, st, a, "attn_fwd_bf16");
+  }
+}
+
+extern "C" int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int hd, float scale, int causal,
+                                  const void* q, int64_t q_bs, int64_t q_rs, const void* k, int64_t k_bs,
+                                  int64_t k_rs, const void* v, int64_t v_bs, int64_t v_rs, const uint8_t* key_pad,
+                                  const void* o, int64_t o_bs, int64_t o_rs, const void* dout, int64_t do_bs,
+                                  int64_t do_rs, const float* lse, void* dq, int64_t dq_bs, int64_t dq_rs, void* dk,
+                                  int64_t dk_bs, int64_t dk_rs, void* dv, int64_t dv_bs, int64_t dv_rs,
+                                  void* stream) {
+  int rc = check_common(dtype, B, H, Nq, Nk, hd);
+  if (rc) return rc;
+  AttnArgs a{};
+  a.B = B; a.H = H; a.Nq = Nq; a.Nk = Nk; a.hd = hd; a.causal = causal; a.scale = scale;
+  a.q = q; a.k = k; a.v = v; a.q_bs = q_bs; a.q_rs = q_rs; a.k_bs = k_bs; a.k_rs = k_rs; a.v_bs = v_bs; a.v_rs = v_rs;
+  a.key_pad = key_pad; a.o = o; a.o_bs = o_bs; a.o_rs = o_rs; a.dout = dout; a.do_bs = do_bs; a.do_rs = do_rs;
+  a.lse_in = lse; a.dq = dq; a.dq_bs = dq_bs; a.dq_rs = dq_rs; a.dk = dk; a.dk_bs = dk_bs; a.dk_rs = dk_rs;
+  a.dv = dv; a.dv_bs = dv_bs; a.dv_rs = dv_rs;
+  hipStream_t st = S(stream);
+  if (dtype == CAPK_F32) {
+    {
+      dim3 grid(B * H, cdiv(Nq, 64));
+      F32_HD_DISPATCH(attn_bwd_dq_f32, grid);
+      CAPK_LAUNCH_CHECK("attn_bwd_dq_f32");
+    }
+    {
+      dim3 grid(B * H, cdiv(Nk, 64));
+      F32_HD_DISPATCH(attn_bwd_dkv_f32, grid);
+      CAPK_LAUNCH_CHECK("attn_bwd_dkv_f32");
+    }
+    return CAPK_OK;
+  }
+  CAPK_CHECK_ARG(q_rs % 8 == 0 && k_rs % 8 == 0 && v_rs % 8 == 0 && do_rs % 8 == 0 && dq_rs % 4 == 0 &&
+                     dk_rs % 4 == 0 && dv_rs % 4 == 0,
+                 "capk_attention_bwd(bf16): strides must allow vector access");
+  const int hdp = hdp_of(hd);
+  const size_t shm = bwd_smem(Nq, Nk, hdp);
+  CAPK_CHECK_ARG(shm <= 160 * 1024, "capk_attention_bwd: LDS %zu > 160 KiB", shm);
+  const dim3 grid(B * H), block(256);
+  switch (hdp) {
+    case 32: return launch_dyn(attn_bwd_bf16<32>, grid, block, shm, st, a, "attn_bwd_bf16");
+    case 64: return launch_dyn(attn_bwd_bf16<64>, grid, block, shm, st, a, "attn_bwd_bf16");
+    case 96: return launch_dyn(attn_bwd_bf16<96>, grid, block, shm, st, a, "attn_bwd_bf16");
+    default: return launch_dyn(attn_bwd_bf16<128>, grid, block, shm, st, a, "attn_bwd_bf16");
+  }
+}

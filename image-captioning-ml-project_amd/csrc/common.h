@@ -1,0 +1,128 @@
+// Shared device/host helpers for libcapk (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string>
+
+#include "../../include/capk.h"
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned short u16;
+
+#define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
+
+namespace capk {
+
+// ---------------------------------------------------------------- errors ----
+void set_error(const char* fmt, ...);
+int hip_status(hipError_t e, const char* what);
+
+#define CAPK_CHECK_ARG(cond, ...)            \
+  do {                                       \
+    if (!(cond)) {                           \
+      ::capk::set_error(__VA_ARGS__);        \
+      return CAPK_EINVAL;                    \
+    }                                        \
+  } while (0)
+
+#define CAPK_LAUNCH_CHECK(what)                                      \
+  do {                                                               \
+    hipError_t _e = hipGetLastError();                               \
+    if (_e != hipSuccess) return ::capk::hip_status(_e, what);       \
+  } while (0)
+
+// ------------------------------------------------------------ conversions ---
+__device__ __forceinline__ float to_f32(float x) { return x; }
+__device__ __forceinline__ float to_f32(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f32(float x);
+template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
+
+// vector of 8 elements of T <-> 8 floats
+template <typename T> struct Vec8;
+template <> struct Vec8<float> {
+  __device__ __forceinline__ static void load(const float* p, float (&v)[8]) {
+    f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+    v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+    v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+  }
+  __device__ __forceinline__ static void store(float* p, const float (&v)[8]) {
+    f32x4 a = {v[0], v[1], v[2], v[3]}, b = {v[4], v[5], v[6], v[7]};
+    *(f32x4*)p = a; *(f32x4*)(p + 4) = b;
+  }
+};
+template <> struct Vec8<bf16> {
+  __device__ __forceinline__ static void load(const bf16* p, float (&v)[8]) {
+    bf16x8 a = *(const bf16x8*)p;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)a[i];
+  }
+  __device__ __forceinline__ static void store(bf16* p, const float (&v)[8]) {
+    bf16x8 a;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = (bf16)v[i];
+    *(bf16x8*)p = a;
+  }
+};
+
+// ------------------------------------------------------------ activations ---
+__device__ __forceinline__ float act_fwd(int act, float x) {
+  switch (act) {
+    case CAPK_ACT_GELU_ERF: return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+    case CAPK_ACT_GELU_TANH: {
+      const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+      return 0.5f * x * (1.0f + tanhf(k0 * (x + k1 * x * x * x)));
+    }
+    case CAPK_ACT_QUICK_GELU: return x / (1.0f + __expf(-1.702f * x));
+    case CAPK_ACT_TANH: return tanhf(x);
+    case CAPK_ACT_RELU: return x > 0.f ? x : 0.f;
+    default: return x;
+  }
+}
+// derivative d act(x) / dx
+__device__ __forceinline__ float act_grad(int act, float x) {
+  switch (act) {
+    case CAPK_ACT_GELU_ERF: {
+      float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+      float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+      return cdf + x * pdf;
+    }
+    case CAPK_ACT_GELU_TANH: {
+      const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+      float u = k0 * (x + k1 * x * x * x);
+      float t = tanhf(u);
+      return 0.5f * (1.0f + t) + 0.5f * x * (1.0f - t * t) * k0 * (1.0f + 3.0f * k1 * x * x);
+    }
+    case CAPK_ACT_QUICK_GELU: {
+      float s = 1.0f / (1.0f + __expf(-1.702f * x));
+      return s + 1.702f * x * s * (1.0f - s);
+    }
+    case CAPK_ACT_TANH: { float t = tanhf(x); return 1.0f - t * t; }
+    case CAPK_ACT_RELU: return x > 0.f ? 1.f : 0.f;
+    default: return 1.0f;
+  }
+}
+
+// ------------------------------------------------------- wave reductions ----
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+inline hipStream_t S(void* s) { return (hipStream_t)s; }
+
+}  // namespace capk

@@ -1,0 +1,494 @@
+// HBM-bound kernels of the hot path: ViT patchify + token assembly, token and
+// position embeddings, shifted cross entropy (fwd+bwd fused), bias-gradient
+// column sums, casts/copies and the AdamW update.  All use 16-B vector
+// accesses per lane (cdna guide G13).
+#include "common.h"
+
+namespace capk {
+
+// ------------------------------------------------------------ patchify -----
+template <typename T>
+__global__ __launch_bounds__(256) void patchify_kernel(int B, int C, int H, int W, int P,
+                                                       const float* __restrict__ img, T* __restrict__ out) {
+  const int nw = W / P, np = (H / P) * nw, kcols = C * P * P;
+  const int64_t total = (int64_t)B * np * (kcols / 8);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int chunk = (int)(i % (kcols / 8));
+    const int64_t row = i / (kcols / 8);
+    const int b = (int)(row / np), p = (int)(row % np);
+    const int col = chunk * 8;
+    const int c = col / (P * P), kh = (col / P) % P, kw = col % P;
+    const int y = (p / nw) * P + kh, x = (p % nw) * P + kw;
+    float v[8];
+    Vec8<float>::load(img + (((int64_t)b * C + c) * H + y) * W + x, v);
+    Vec8<T>::store(out + row * kcols + col, v);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void vit_assemble_kernel(int B, int Np, int D, const T* __restrict__ patch,
+                                                           const float* __restrict__ cls, const float* __restrict__ pos,
+                                                           T* __restrict__ x) {
+  const int dch = D / 8;
+  const int64_t total = (int64_t)B * (Np + 1) * dch;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % dch);
+    const int64_t row = i / dch;
+    const int b = (int)(row / (Np + 1)), n = (int)(row % (Np + 1));
+    float v[8], pv[8];
+    if (n == 0) Vec8<float>::load(cls + c * 8, v);
+    else Vec8<T>::load(patch + ((int64_t)b * Np + n - 1) * D + c * 8, v);
+    Vec8<float>::load(pos + (int64_t)n * D + c * 8, pv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += pv[k];
+    Vec8<T>::store(x + row * D + c * 8, v);
+  }
+}
+
+// ------------------------------------------------------------ embeddings ---
+template <typename T>
+__global__ __launch_bounds__(256) void embedding_fwd_kernel(int B, int T_, int D, const int64_t* __restrict__ ids,
+                                                            const float* __restrict__ table,
+                                                            const float* __restrict__ pos, int pos_offset,
+                                                            T* __restrict__ out) {
+  const int dch = D / 8;
+  const int64_t total = (int64_t)B * T_ * dch;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % dch);
+    const int64_t row = i / dch;
+    const int t = (int)(row % T_);
+    float v[8];
+    Vec8<float>::load(table + ids[row] * D + c * 8, v);
+    if (pos) {
+      float pv[8];
+      Vec8<float>::load(pos + (int64_t)(pos_offset + t) * D + c * 8, pv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += pv[k];
+    }
+    Vec8<T>::store(out + row * D + c * 8, v);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void embedding_bwd_kernel(int B, int T_, int D, const int64_t* __restrict__ ids,
+                                                            const T* __restrict__ dout, int padding_idx,
+                                                            float* __restrict__ dtable, float* __restrict__ dpos,
+                                                            int pos_offset) {
+  const int64_t total = (int64_t)B * T_ * D;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int d = (int)(i % D);
+    const int64_t row = i / D;
+    const float g = to_f32(dout[i]);
+    const int64_t id = ids[row];
+    if (dtable && id != padding_idx) atomicAdd(dtable + id * D + d, g);
+    if (dpos) atomicAdd(dpos + (int64_t)(pos_offset + (int)(row % T_)) * D + d, g);
+  }
+}
+
+// ------------------------------------------------------- shifted CE --------
+__global__ void ce_count_kernel(int B, int T_, const int64_t* __restrict__ targets, int ignore_index,
+                                float* __restrict__ cnt) {
+  float c = 0.f;
+  for (int i = threadIdx.x; i < B * (T_ - 1); i += blockDim.x) {
+    const int b = i / (T_ - 1), t = i % (T_ - 1);
+    c += targets[(int64_t)b * T_ + t + 1] != ignore_index ? 1.f : 0.f;
+  }
+  __shared__ float red[16];
+  c = wave_sum(c);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
+    cnt[0] = s;
+  }
+}
+
+constexpr int CE_THREADS = 1024;
+constexpr int CE_MAXCH = 8;  // up to 8*8*1024 = 65536 columns per row
+
+__device__ __forceinline__ float block_reduce(float v, float* red, bool is_max) {
+  v = is_max ? wave_max(v) : wave_sum(v);
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float r = red[0];
+  for (int i = 1; i < nw; ++i) r = is_max ? fmaxf(r, red[i]) : r + red[i];
+  return r;
+}
+
+template <typename T>
+__global__ __launch_bounds__(CE_THREADS) void ce_rows_kernel(int B, int T_, int V, int64_t ld,
+                                                             const T* __restrict__ logits,
+                                                             const int64_t* __restrict__ targets, int ignore_index,
+                                                             const float* __restrict__ grad_scale, const float* __restrict__ cnt,
+                                                             float* __restrict__ row_loss, T* __restrict__ dlogits) {
+  __shared__ float red[16];
+  const int row = blockIdx.x;
+  const int b = row / T_, t = row % T_;
+  const int64_t tgt = (t < T_ - 1) ? targets[(int64_t)b * T_ + t + 1] : (int64_t)ignore_index;
+  const bool counted = tgt != ignore_index;
+  const T* lr = logits + (int64_t)row * ld;
+  const int nch = (int)(ld / 8);
+  if (!counted) {
+    if (threadIdx.x == 0 && row_loss) row_loss[row] = 0.f;
+    if (dlogits) {
+      const float z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int c = threadIdx.x; c < nch; c += CE_THREADS) Vec8<T>::store(dlogits + (int64_t)row * ld + c * 8, z);
+    }
+    return;
+  }
+  const float tgt_logit = to_f32(lr[tgt]);  // read before any in-place gradient write
+  float v[CE_MAXCH][8];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < CE_MAXCH; ++k) {
+    const int c = threadIdx.x + k * CE_THREADS;
+    if (c < nch) {
+      Vec8<T>::load(lr + c * 8, v[k]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (c * 8 + i >= V) v[k][i] = -INFINITY;
+        mx = fmaxf(mx, v[k][i]);
+      }
+    }
+  }
+  mx = block_reduce(mx, red, true);
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < CE_MAXCH; ++k) {
+    const int c = threadIdx.x + k * CE_THREADS;
+    if (c < nch) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        v[k][i] = __expf(v[k][i] - mx);
+        s += v[k][i];
+      }
+    }
+  }
+  s = block_reduce(s, red, false);
+  const float lse = mx + __logf(s);
+  if (threadIdx.x == 0 && row_loss) row_loss[row] = lse - tgt_logit;
+  if (dlogits) {
+    const float scale = (grad_scale ? grad_scale[0] : 1.f) / cnt[0];
+    const float inv = 1.f / s;
+#pragma unroll
+    for (int k = 0; k < CE_MAXCH; ++k) {
+      const int c = threadIdx.x + k * CE_THREADS;
+      if (c < nch) {
+        float g[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int col = c * 8 + i;
+          g[i] = col < V ? (v[k][i] * inv - (col == tgt ? 1.f : 0.f)) * scale : 0.f;
+        }
+        Vec8<T>::store(dlogits + (int64_t)row * ld + c * 8, g);
+      }
+    }
+  }
+}
+
+__global__ void ce_finish_kernel(int rows, const float* __restrict__ row_loss, const float* __restrict__ cnt,
+                                 float* __restrict__ out) {
+  __shared__ float red[16];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < rows; i += blockDim.x) s += row_loss[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+    out[0] = t / cnt[0];
+    out[1] = cnt[0];
+  }
+}
+
+// ------------------------------------------------------------ colsum --------
+constexpr int CS_ROWS_PER_SPLIT = 512;
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_kernel(int M, int N, const T* __restrict__ dy, int64_t ldy,
+                                                     float* __restrict__ part) {
+  __shared__ float red[4][64 * 8 + 4];
+  const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int m0 = blockIdx.y * CS_ROWS_PER_SPLIT, m1 = min(M, m0 + CS_ROWS_PER_SPLIT);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c * 8 < N) {
+    for (int m = m0 + ph; m < m1; m += 4) {
+      float v[8];
+      Vec8<T>::load(dy + (int64_t)m * ldy + c * 8, v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += v[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[ph][lane * 8 + i] = acc[i];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 512; i += 256) {
+    const int col = blockIdx.x * 512 + i;
+    if (col < N) part[(int64_t)blockIdx.y * N + col] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+  }
+}
+
+__global__ void colsum_finish_kernel(int splits, int N, const float* __restrict__ part, float* __restrict__ out,
+                                     int accumulate) {
+  for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < N; n += gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += part[(int64_t)k * N + n];
+    out[n] = accumulate ? out[n] + s : s;
+  }
+}
+
+// ------------------------------------------------------------ copies -------
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void cast_kernel(int64_t n, const TI* __restrict__ x, TO* __restrict__ y) {
+  const int64_t n8 = n / 8;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    float v[8];
+    Vec8<TI>::load(x + i * 8, v);
+    Vec8<TO>::store(y + i * 8, v);
+  }
+  for (int64_t i = n8 * 8 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = from_f32<TO>(to_f32(x[i]));
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void copy_rows_kernel(int rows, int cols, const T* __restrict__ x, int64_t ldx,
+                                                        T* __restrict__ y, int64_t ldy) {
+  const int ch = cols / 8;
+  const int64_t total = (int64_t)rows * ch;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / ch;
+    const int c = (int)(i % ch);
+    float v[8];
+    Vec8<T>::load(x + r * ldx + c * 8, v);
+    Vec8<T>::store(y + r * ldy + c * 8, v);
+  }
+}
+
+// ------------------------------------------------------------ AdamW --------
+__global__ __launch_bounds__(256) void adamw_kernel(int64_t n, float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    bf16* __restrict__ pb, float lr, float wd, float b1, float b2,
+                                                    float eps, float bc1, float bc2) {
+  const float step_size = lr / bc1;
+  const float bc2s = sqrtf(bc2);
+  const float decay = 1.f - lr * wd;
+  const int64_t n4 = n / 4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    f32x4 pv = ((f32x4*)p)[i], gv = ((const f32x4*)g)[i], mv = ((f32x4*)m)[i], vv = ((f32x4*)v)[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      pv[k] *= decay;
+      mv[k] = mv[k] + (gv[k] - mv[k]) * (1.f - b1);
+      vv[k] = vv[k] * b2 + (1.f - b2) * gv[k] * gv[k];
+      const float denom = sqrtf(vv[k]) / bc2s + eps;
+      pv[k] = pv[k] - step_size * (mv[k] / denom);
+    }
+    ((f32x4*)p)[i] = pv;
+    ((f32x4*)m)[i] = mv;
+    ((f32x4*)v)[i] = vv;
+    if (pb) {
+      bf16x4 o;
+      o[0] = (bf16)pv[0]; o[1] = (bf16)pv[1]; o[2] = (bf16)pv[2]; o[3] = (bf16)pv[3];
+      ((bf16x4*)pb)[i] = o;
+    }
+  }
+  for (int64_t i = n4 * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float pv = p[i] * decay, gv = g[i];
+    float mv = m[i] + (gv - m[i]) * (1.f - b1);
+    float vv = v[i] * b2 + (1.f - b2) * gv * gv;
+    pv = pv - step_size * (mv / (sqrtf(vv) / bc2s + eps));
+    p[i] = pv; m[i] = mv; v[i] = vv;
+    if (pb) pb[i] = (bf16)pv;
+  }
+}
+
+// ------------------------------------------------------- activation bwd ----
+template <typename T>
+__global__ __launch_bounds__(256) void act_bwd_kernel(int64_t n, int act, const T* __restrict__ dy,
+                                                      const T* __restrict__ aux, T* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = from_f32<T>(to_f32(dy[i]) * act_grad(act, to_f32(aux[i])));
+}
+
+static int grid_for(int64_t work, int per_block = 256) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>(8192, (work + per_block - 1) / per_block));
+}
+
+}  // namespace capk
+
+using namespace capk;
+
+#define DT_DISPATCH(dtype, NAME, ...)                                        \
+  if ((dtype) == CAPK_BF16) { NAME(bf16, __VA_ARGS__); }                     \
+  else if ((dtype) == CAPK_F32) { NAME(float, __VA_ARGS__); }                \
+  else { set_error("%s: bad dtype %d", __func__, (int)(dtype)); return CAPK_EINVAL; }
+
+extern "C" int capk_patchify(int out_dtype, int B, int C, int H, int W, int P, const float* images, void* out,
+                             void* stream) {
+  CAPK_CHECK_ARG(B > 0 && C > 0 && P > 0 && H % P == 0 && W % P == 0 && P % 8 == 0, "capk_patchify: bad shape");
+  const int64_t work = (int64_t)B * (H / P) * (W / P) * C * P * P / 8;
+#define L(T, _) hipLaunchKernelGGL(patchify_kernel<T>, dim3(grid_for(work)), dim3(256), 0, S(stream), B, C, H, W, P, images, (T*)out)
+  DT_DISPATCH(out_dtype, L, 0)
+#undef L
+  CAPK_LAUNCH_CHECK("patchify_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_vit_assemble(int dtype, int B, int Np, int D, const void* patch_out, const float* cls,
+                                 const float* pos, void* x, void* stream) {
+  CAPK_CHECK_ARG(B > 0 && Np > 0 && D % 8 == 0, "capk_vit_assemble: bad shape");
+  const int64_t work = (int64_t)B * (Np + 1) * D / 8;
+#define L(T, _) hipLaunchKernelGGL(vit_assemble_kernel<T>, dim3(grid_for(work)), dim3(256), 0, S(stream), B, Np, D, (const T*)patch_out, cls, pos, (T*)x)
+  DT_DISPATCH(dtype, L, 0)
+#undef L
+  CAPK_LAUNCH_CHECK("vit_assemble_kernel");
+  return CAPK_OK;
+}
+
+extern "C" size_t capk_colsum_workspace(int M, int N) {
+  return (size_t)cdiv(M, CS_ROWS_PER_SPLIT) * N * sizeof(float);
+}
+
+extern "C" int capk_colsum(int dtype, int M, int N, const void* dy, int64_t ldy, float* db, int accumulate, void* ws,
+                           size_t ws_bytes, void* stream) {
+  CAPK_CHECK_ARG(M > 0 && N > 0 && N % 8 == 0 && ldy % 8 == 0, "capk_colsum: N and ldy must be multiples of 8");
+  const int splits = cdiv(M, CS_ROWS_PER_SPLIT);
+  CAPK_CHECK_ARG(ws && ws_bytes >= (size_t)splits * N * sizeof(float), "capk_colsum: workspace too small");
+  dim3 grid(cdiv(N, 512), splits);
+#define L(T, _) hipLaunchKernelGGL(colsum_kernel<T>, grid, dim3(256), 0, S(stream), M, N, (const T*)dy, ldy, (float*)ws)
+  DT_DISPATCH(dtype, L, 0)
+#undef L
+  CAPK_LAUNCH_CHECK("colsum_kernel");
+  hipLaunchKernelGGL(colsum_finish_kernel, dim3(grid_for(N)), dim3(256), 0, S(stream), splits, N, (const float*)ws, db,
+                     accumulate);
+  CAPK_LAUNCH_CHECK("colsum_finish_kernel");
+  return CAPK_OK;
+}
+
+extern "C" size_t capk_vit_assemble_bwd_workspace(int B, int Np, int D) {
+  return capk_colsum_workspace(B, (Np + 1) * D);
+}
+
+extern "C" int capk_vit_assemble_bwd(int dtype, int B, int Np, int D, const void* dx, void* dpatch, float* dcls,
+                                     float* dpos, void* ws, size_t ws_bytes, void* stream) {
+  CAPK_CHECK_ARG(B > 0 && Np > 0 && D % 8 == 0, "capk_vit_assemble_bwd: bad shape");
+  const int64_t esz = dtype == CAPK_BF16 ? 2 : 4;
+  {
+    // one 2D copy: B "rows" of Np*D elements with source pitch (Np+1)*D
+    hipError_t e = hipMemcpy2DAsync(dpatch, (size_t)Np * D * esz, (const char*)dx + D * esz, (size_t)(Np + 1) * D * esz,
+                                    (size_t)Np * D * esz, B, hipMemcpyDeviceToDevice, S(stream));
+    if (e != hipSuccess) return hip_status(e, "capk_vit_assemble_bwd memcpy2d");
+  }
+  int rc = capk_colsum(dtype, B, (Np + 1) * D, dx, (int64_t)(Np + 1) * D, dpos, 0, ws, ws_bytes, stream);
+  if (rc) return rc;
+  hipError_t e = hipMemcpyAsync(dcls, dpos, D * sizeof(float), hipMemcpyDeviceToDevice, S(stream));
+  if (e != hipSuccess) return hip_status(e, "capk_vit_assemble_bwd dcls");
+  return CAPK_OK;
+}
+
+extern "C" int capk_embedding_fwd(int dtype, int B, int T, int D, const int64_t* ids, const float* table,
+                                  const float* pos, int pos_offset, void* out, void* stream) {
+  CAPK_CHECK_ARG(B > 0 && T > 0 && D % 8 == 0, "capk_embedding_fwd: bad shape");
+  const int64_t work = (int64_t)B * T * D / 8;
+#define L(T_, _) hipLaunchKernelGGL(embedding_fwd_kernel<T_>, dim3(grid_for(work)), dim3(256), 0, S(stream), B, T, D, ids, table, pos, pos_offset, (T_*)out)
+  DT_DISPATCH(dtype, L, 0)
+#undef L
+  CAPK_LAUNCH_CHECK("embedding_fwd_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_embedding_bwd(int dtype, int B, int T, int D, const int64_t* ids, const void* dout,
+                                  int padding_idx, float* dtable, float* dpos, int pos_offset, void* stream) {
+  CAPK_CHECK_ARG(B > 0 && T > 0 && D > 0, "capk_embedding_bwd: bad shape");
+  const int64_t work = (int64_t)B * T * D;
+#define L(T_, _) hipLaunchKernelGGL(embedding_bwd_kernel<T_>, dim3(grid_for(work)), dim3(256), 0, S(stream), B, T, D, ids, (const T_*)dout, padding_idx, dtable, dpos, pos_offset)
+  DT_DISPATCH(dtype, L, 0)
+#undef L
+  CAPK_LAUNCH_CHECK("embedding_bwd_kernel");
+  return CAPK_OK;
+}
+
+extern "C" size_t capk_shifted_ce_workspace(int B, int T) { return (size_t)(B * T + 4) * sizeof(float); }
+
+extern "C" int capk_shifted_ce(int dtype, int B, int T, int V, int64_t ld, const void* logits,
+                               const int64_t* targets, int ignore_index, const float* grad_scale, float* loss_out,
+                               void* dlogits, void* ws, size_t ws_bytes, void* stream) {
+  CAPK_CHECK_ARG(B > 0 && T > 1 && V > 0 && ld >= V && ld % 8 == 0, "capk_shifted_ce: bad shape (ld %% 8)");
+  CAPK_CHECK_ARG(ld <= (int64_t)CE_MAXCH * 8 * CE_THREADS, "capk_shifted_ce: row too long");
+  CAPK_CHECK_ARG(ws && ws_bytes >= capk_shifted_ce_workspace(B, T), "capk_shifted_ce: workspace too small");
+  float* cnt = (float*)ws;
+  float* row_loss = loss_out ? cnt + 4 : nullptr;
+  hipStream_t st = S(stream);
+  hipLaunchKernelGGL(ce_count_kernel, dim3(1), dim3(1024), 0, st, B, T, targets, ignore_index, cnt);
+  CAPK_LAUNCH_CHECK("ce_count_kernel");
+#define L(T_, _) hipLaunchKernelGGL(ce_rows_kernel<T_>, dim3(B * T), dim3(CE_THREADS), 0, st, B, T, V, ld, (const T_*)logits, targets, ignore_index, grad_scale, cnt, row_loss, (T_*)dlogits)
+  DT_DISPATCH(dtype, L, 0)
+#undef L
+  CAPK_LAUNCH_CHECK("ce_rows_kernel");
+  if (loss_out) {
+    hipLaunchKernelGGL(ce_finish_kernel, dim3(1), dim3(1024), 0, st, B * T, row_loss, cnt, loss_out);
+    CAPK_LAUNCH_CHECK("ce_finish_kernel");
+  }
+  return CAPK_OK;
+}
+
+extern "C" int capk_cast(int in_dtype, int out_dtype, int64_t n, const void* x, void* y, void* stream) {
+  CAPK_CHECK_ARG(n >= 0, "capk_cast: n");
+  if (n == 0) return CAPK_OK;
+  const dim3 g(grid_for(n / 8 + 1)), b(256);
+  hipStream_t st = S(stream);
+  if (in_dtype == CAPK_F32 && out_dtype == CAPK_BF16) hipLaunchKernelGGL((cast_kernel<float, bf16>), g, b, 0, st, n, (const float*)x, (bf16*)y);
+  else if (in_dtype == CAPK_BF16 && out_dtype == CAPK_F32) hipLaunchKernelGGL((cast_kernel<bf16, float>), g, b, 0, st, n, (const bf16*)x, (float*)y);
+  else if (in_dtype == CAPK_F32 && out_dtype == CAPK_F32) hipLaunchKernelGGL((cast_kernel<float, float>), g, b, 0, st, n, (const float*)x, (float*)y);
+  else if (in_dtype == CAPK_BF16 && out_dtype == CAPK_BF16) hipLaunchKernelGGL((cast_kernel<bf16, bf16>), g, b, 0, st, n, (const bf16*)x, (bf16*)y);
+  else { set_error("capk_cast: dtype"); return CAPK_EINVAL; }
+  CAPK_LAUNCH_CHECK("cast_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_copy_rows(int dtype, int rows, int cols, const void* x, int64_t ldx, void* y, int64_t ldy,
+                              void* stream) {
+  CAPK_CHECK_ARG(rows > 0 && cols % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0, "capk_copy_rows: need multiples of 8");
+  const int64_t work = (int64_t)rows * cols / 8;
+#define L(T, _) hipLaunchKernelGGL(copy_rows_kernel<T>, dim3(grid_for(work)), dim3(256), 0, S(stream), rows, cols, (const T*)x, ldx, (T*)y, ldy)
+  DT_DISPATCH(dtype, L, 0)
+#undef L
+  CAPK_LAUNCH_CHECK("copy_rows_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_adamw(int64_t n, float* param, const float* grad, float* m, float* v, void* param_bf16, float lr,
+                          float weight_decay, float beta1, float beta2, float eps, float bc1, float bc2,
+                          void* stream) {
+  CAPK_CHECK_ARG(n >= 0 && param && grad && m && v, "capk_adamw: null");
+  CAPK_CHECK_ARG((uintptr_t)param % 16 == 0 && (uintptr_t)grad % 16 == 0 && (uintptr_t)m % 16 == 0 &&
+                     (uintptr_t)v % 16 == 0 && (uintptr_t)param_bf16 % 8 == 0,
+                 "capk_adamw: buffers must be 16-B aligned");
+  if (n == 0) return CAPK_OK;
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, S(stream), n, param, grad, m, v,
+                     (bf16*)param_bf16, lr, weight_decay, beta1, beta2, eps, bc1, bc2);
+  CAPK_LAUNCH_CHECK("adamw_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_act_bwd(int dtype, int64_t n, int act, const void* dy, const void* aux, void* out, void* stream) {
+  CAPK_CHECK_ARG(n >= 0 && dy && aux && out, "capk_act_bwd: null");
+  if (n == 0) return CAPK_OK;
+#define L(T, _) hipLaunchKernelGGL(act_bwd_kernel<T>, dim3(grid_for(n)), dim3(256), 0, S(stream), n, act, (const T*)dy, (const T*)aux, (T*)out)
+  DT_DISPATCH(dtype, L, 0)
+#undef L
+  CAPK_LAUNCH_CHECK("act_bwd_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_zero(void* ptr, size_t bytes, void* stream) {
+  if (bytes == 0) return CAPK_OK;
+  CAPK_CHECK_ARG(ptr, "capk_zero: null");
+  hipError_t e = hipMemsetAsync(ptr, 0, bytes, S(stream));
+  if (e != hipSuccess) return hip_status(e, "capk_zero");
+  return CAPK_OK;
+}

@@ -1,0 +1,178 @@
+/* capk — MI355X (gfx950) compute backend for the image-captioning hot path.
+ *
+ * C ABI of libcapk.so.  Plain pointers, sizes and strides; no torch types.
+ * The reference (thromel/Image-Captioning-ML-Project) is pure Python whose
+ * arithmetic runs inside torch / HF transformers modules; each entry point
+ * below names the reference call site it replaces (file:line).
+ *
+ * Conventions
+ *  - Return 0 on success, a negative CAPK_E* code on failure; the message of the
+ *    last failure on this thread is capk_last_error().
+ *  - dtype codes: CAPK_F32 (fp32 storage, fp32 arithmetic: the parity path) and
+ *    CAPK_BF16 (bf16 storage, fp32 accumulation: the throughput path).
+ *  - Strides are in ELEMENTS.  `stream` is a hipStream_t passed as void*.
+ *  - The caller owns every buffer (inputs, outputs, workspaces).  No entry point
+ *    allocates or frees device memory, synchronises the device or the stream,
+ *    so every call is hipGraph-capturable.
+ */
+#ifndef CAPK_H
+#define CAPK_H
+#include <stdint.h>
+#include <stddef.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CAPK_OK 0
+#define CAPK_EINVAL (-1)      /* bad shape / stride / dtype / alignment          */
+#define CAPK_EHIP (-2)        /* a HIP runtime call failed (message has details) */
+#define CAPK_EUNSUPPORTED (-3)/* combination not implemented                     */
+
+#define CAPK_F32 0
+#define CAPK_BF16 1
+
+/* epilogue activations (act argument of capk_gemm) */
+#define CAPK_ACT_NONE 0
+#define CAPK_ACT_GELU_ERF 1   /* HF "gelu" / torch F.gelu (ViT, nn.TransformerDecoderLayer) */
+#define CAPK_ACT_GELU_TANH 2  /* HF "gelu_new" (GPT-2)                                      */
+#define CAPK_ACT_QUICK_GELU 3 /* CLIP quick_gelu x*sigmoid(1.702x)                          */
+#define CAPK_ACT_TANH 4       /* ViT pooler                                                 */
+#define CAPK_ACT_RELU 5
+/* backward forms: out = acc * act'(aux) where aux is the saved pre-activation */
+#define CAPK_ACT_BWD 16
+
+const char* capk_last_error(void);
+int capk_version(void);
+int capk_device_arch(char* buf, int len); /* writes gcnArchName of the current device */
+
+/* ---------------------------------------------------------------- GEMM -----
+ * C[m,n] = alpha * sum_k A(m,k) * B(n,k)  + beta * C[m,n]
+ *          + bias[n] + residual[m,n]        (each optional; bias fp32)
+ * then  act:  CAPK_ACT_x            -> preact (optional) = pre, C = act(pre)
+ *             CAPK_ACT_BWD|CAPK_ACT_x -> C = pre * act'(aux[m,n])
+ * A(m,k) = a_kmajor ? A[m*lda + k] : A[k*lda + m]
+ * B(n,k) = b_kmajor ? B[n*ldb + k] : B[k*ldb + n]
+ * Replaces every nn.Linear / Conv1D / patch-conv GEMM (and its two backward
+ * GEMMs) on the hot path: modeling_vit.py:60-69,216-218,236,249-254;
+ * torch/nn/modules/transformer.py (in_proj/out_proj/linear1/linear2);
+ * src/models/decoders.py:390,431 (visual_projection, output_layer).
+ * in_dtype applies to A and B; out_dtype to C, residual, preact, aux.
+ * Workspace (split-K partial slabs, fp32) — query with capk_gemm_workspace();
+ * pass ws=NULL/ws_bytes=0 to disable split-K. */
+size_t capk_gemm_workspace(int in_dtype, int out_dtype, int M, int N, int K);
+int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K,
+              const void* A, int64_t lda, int a_kmajor,
+              const void* B, int64_t ldb, int b_kmajor,
+              void* C, int64_t ldc, float alpha, float beta,
+              const float* bias, const void* residual, int64_t ldr,
+              int act, void* preact, const void* aux, int64_t ldx,
+              void* ws, size_t ws_bytes, void* stream);
+
+/* -------------------------------------------------------- LayerNorm -------
+ * y = (x - mean) * rstd * w + b over the last `cols` elements of each row;
+ * mean/rstd (fp32, [rows]) saved for backward.  LN eps 1e-12 (ViT), 1e-5
+ * (nn.TransformerDecoderLayer, CLIP, GPT-2).  Replaces F.layer_norm at
+ * modeling_vit.py:270,278,348 and transformer.py:1148-1153. */
+int capk_layernorm_fwd(int dtype, int rows, int cols, const void* x, int64_t ldx,
+                       const float* w, const float* b, float eps,
+                       void* y, int64_t ldy, float* mean, float* rstd, void* stream);
+/* dx = LN'(dy) (+ dres if non-NULL); dw/db (fp32 [cols]) = sum over rows
+ * (accumulate into existing dw/db when accumulate != 0).  ws: capk_layernorm_bwd_workspace. */
+size_t capk_layernorm_bwd_workspace(int rows, int cols);
+int capk_layernorm_bwd(int dtype, int rows, int cols, const void* dy, int64_t lddy,
+                       const void* x, int64_t ldx, const float* w,
+                       const float* mean, const float* rstd,
+                       void* dx, int64_t lddx, const void* dres, int64_t ldres,
+                       float* dw, float* db, int accumulate,
+                       void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------- Attention --------
+ * Fused multi-head scaled-dot-product attention, one (batch, head) per
+ * workgroup, Q/K/V/dO staged in LDS, softmax by wavefront shuffles.
+ * Token t of batch b, head h lives at  X + b*x_bs + t*x_rs + h*hd.
+ * key_pad (optional, [B, Nk] uint8, 1 = padded key) and causal masks follow
+ * nn.MultiheadAttention (-inf).  lse (fp32 [B,H,Nq]) is saved for backward.
+ * Nk <= 256, Nq <= 256, hd in {16, 32, 64, 96, 128} (hd % 16 == 0).
+ * Replaces ViT SDPA (modeling_vit.py:164-189,219-235) and the self/cross
+ * attention of nn.TransformerDecoderLayer (transformer.py _sa_block/_mha_block). */
+int capk_attention_fwd(int dtype, int B, int H, int Nq, int Nk, int hd, float scale, int causal,
+                       const void* q, int64_t q_bs, int64_t q_rs,
+                       const void* k, int64_t k_bs, int64_t k_rs,
+                       const void* v, int64_t v_bs, int64_t v_rs,
+                       const uint8_t* key_pad,
+                       void* o, int64_t o_bs, int64_t o_rs, float* lse, void* stream);
+int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int hd, float scale, int causal,
+                       const void* q, int64_t q_bs, int64_t q_rs,
+                       const void* k, int64_t k_bs, int64_t k_rs,
+                       const void* v, int64_t v_bs, int64_t v_rs,
+                       const uint8_t* key_pad,
+                       const void* o, int64_t o_bs, int64_t o_rs,
+                       const void* dout, int64_t do_bs, int64_t do_rs, const float* lse,
+                       void* dq, int64_t dq_bs, int64_t dq_rs,
+                       void* dk, int64_t dk_bs, int64_t dk_rs,
+                       void* dv, int64_t dv_bs, int64_t dv_rs, void* stream);
+
+/* ------------------------------------------------- Embedding / patches ----
+ * ViT patchify (im2col of Conv2d k=s=P, modeling_vit.py:60-69): images fp32
+ * [B,C,H,W] -> out [B*(H/P)*(W/P), C*P*P] in out_dtype, column = c*P*P+kh*P+kw. */
+int capk_patchify(int out_dtype, int B, int C, int H, int W, int P,
+                  const float* images, void* out, void* stream);
+/* x[b,0,:] = cls + pos[0];  x[b,1+p,:] = patch_out[b*Np+p,:] + pos[1+p]
+ * (ViTEmbeddings.forward modeling_vit.py:146-157). cls/pos fp32. */
+int capk_vit_assemble(int dtype, int B, int Np, int D, const void* patch_out,
+                      const float* cls, const float* pos, void* x, void* stream);
+/* backward: dpatch[b*Np+p] = dx[b,1+p];  dcls = sum_b dx[b,0];  dpos = sum_b dx[b]
+ * (fp32, overwrite).  ws >= capk_vit_assemble_bwd_workspace(). */
+size_t capk_vit_assemble_bwd_workspace(int B, int Np, int D);
+int capk_vit_assemble_bwd(int dtype, int B, int Np, int D, const void* dx, void* dpatch,
+                          float* dcls, float* dpos, void* ws, size_t ws_bytes, void* stream);
+/* token + position embedding:  out[b*T+t] = table[ids[b*T+t]] + pos[pos_offset+t]
+ * (decoders.py:409-414; GPT-2 wte+wpe).  pos may be NULL. */
+int capk_embedding_fwd(int dtype, int B, int T, int D, const int64_t* ids, const float* table,
+                       const float* pos, int pos_offset, void* out, void* stream);
+/* dtable[ids] += dout (rows whose id == padding_idx skipped, nn.Embedding
+ * padding_idx semantics, decoders.py:337-339); dpos[pos_offset+t] += sum_b dout.
+ * dtable/dpos fp32, accumulated (caller zeroes). */
+int capk_embedding_bwd(int dtype, int B, int T, int D, const int64_t* ids, const void* dout,
+                       int padding_idx, float* dtable, float* dpos, int pos_offset, void* stream);
+
+/* --------------------------------------------------- Loss ------------------
+ * Shifted cross entropy (CombinedLoss, src/train/losses.py:236-247):
+ * logits [B*T, ld] (row b*T+t, first V columns valid) vs targets[b, t+1] for
+ * t < T-1, ignore_index = pad.  If loss_out != NULL: loss_out[0] = mean over
+ * counted tokens (fp32), loss_out[1] = count.  If dlogits != NULL it receives
+ * d(loss)/d(logits) * (*grad_scale) (grad_scale: DEVICE pointer to the upstream
+ * gradient, NULL = 1; rows t = T-1, ignored rows and columns >= V are zeroed);
+ * dlogits may alias logits. */
+size_t capk_shifted_ce_workspace(int B, int T);
+int capk_shifted_ce(int dtype, int B, int T, int V, int64_t ld, const void* logits,
+                    const int64_t* targets, int ignore_index, const float* grad_scale,
+                    float* loss_out, void* dlogits, void* ws, size_t ws_bytes, void* stream);
+/* hipMemsetAsync(ptr, 0, bytes) on the stream (gradient buffers that are scatter-added). */
+int capk_zero(void* ptr, size_t bytes, void* stream);
+
+/* --------------------------------------------------- Reductions ------------
+ * db[n] (+)= sum_m dy[m, n]   (bias gradients; fp32 out). */
+size_t capk_colsum_workspace(int M, int N);
+int capk_colsum(int dtype, int M, int N, const void* dy, int64_t ldy, float* db, int accumulate,
+                void* ws, size_t ws_bytes, void* stream);
+/* elementwise casts / copies */
+int capk_cast(int in_dtype, int out_dtype, int64_t n, const void* x, void* y, void* stream);
+int capk_copy_rows(int dtype, int rows, int cols, const void* x, int64_t ldx, void* y, int64_t ldy, void* stream);
+
+/* out = dy * act'(aux) elementwise (activation backward outside a GEMM, e.g. the
+ * ViT pooler tanh, modeling_vit.py:295-301). */
+int capk_act_bwd(int dtype, int64_t n, int act, const void* dy, const void* aux, void* out, void* stream);
+
+/* --------------------------------------------------- Optimizer -------------
+ * torch.optim.AdamW step (decoupled weight decay; trainer.py:131-134) over a
+ * flat fp32 segment; optional bf16 shadow copy of the updated parameters for
+ * the throughput path.  bc1 = 1-beta1^t, bc2 = 1-beta2^t computed by the host. */
+int capk_adamw(int64_t n, float* param, const float* grad, float* m, float* v,
+               void* param_bf16, float lr, float weight_decay, float beta1, float beta2,
+               float eps, float bc1, float bc2, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CAPK_H */

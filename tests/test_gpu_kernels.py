@@ -1,0 +1,279 @@
+"""Kernel-level parity: every libcapk kernel vs a plain PyTorch fp32 reference of the
+same op (computed on the bf16-rounded inputs for the bf16 path).  GPU only."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+cuda = pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from capk import ops as _ops
+    return _ops
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-30))
+
+
+# ------------------------------------------------------------------ GEMM ----
+@cuda
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(300, 256, 192), (128, 128, 64), (517, 384, 768)])
+def test_linear_fwd_epilogues(ops, dtype, M, N, K):
+    from capk._lib import ACT_GELU_ERF
+    g = torch.Generator(device="cuda").manual_seed(0)
+    x = torch.randn(M, K, device="cuda", generator=g).to(dtype)
+    w = (torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)).to(dtype)
+    b = torch.randn(N, device="cuda", generator=g)
+    r = torch.randn(M, N, device="cuda", generator=g).to(dtype)
+    pre = torch.empty(M, N, device="cuda", dtype=dtype)
+    y = ops.linear(x, w, b, residual=r, act=ACT_GELU_ERF, preact=pre)
+    ref_pre = x.float() @ w.float().t() + b + r.float()
+    ref = F.gelu(ref_pre)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert _rel(pre, ref_pre) < tol
+    assert _rel(y, ref) < tol
+
+
+@cuda
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_linear_backward_layouts(ops, dtype):
+    from capk._lib import ACT_GELU_ERF
+    g = torch.Generator(device="cuda").manual_seed(1)
+    M, N, K = 777, 384, 256
+    dy = torch.randn(M, N, device="cuda", generator=g).to(dtype)
+    w = (torch.randn(N, K, device="cuda", generator=g) / math.sqrt(N)).to(dtype)
+    x = torch.randn(M, K, device="cuda", generator=g).to(dtype)
+    aux = torch.randn(M, K, device="cuda", generator=g).to(dtype)
+    dx = ops.linear_dx(dy, w)
+    assert _rel(dx, dy.float() @ w.float()) < (1e-5 if dtype == torch.float32 else 1e-2)
+    # fused activation backward: dX * gelu'(aux)
+    dxa = ops.linear_dx(dy, w, act_bwd=ACT_GELU_ERF, aux=aux)
+    a = aux.float().requires_grad_(True)
+    F.gelu(a).backward(dy.float() @ w.float())
+    assert _rel(dxa, a.grad) < (1e-5 if dtype == torch.float32 else 1e-2)
+    dw = torch.empty(N, K, device="cuda", dtype=torch.float32)
+    ops.linear_dw(dy, x, dw)
+    assert _rel(dw, dy.float().t() @ x.float()) < (1e-5 if dtype == torch.float32 else 5e-3)
+
+
+@cuda
+def test_gemm_bf16_splitk_and_beta(ops):
+    """dW-shaped GEMM with a long reduction (split-K slabs + reduce) and accumulate."""
+    g = torch.Generator(device="cuda").manual_seed(2)
+    M, N, K = 8192, 256, 384  # dy [M,N], x [M,K]: dW [N,K] reduces over M
+    dy = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    dw = torch.randn(N, K, device="cuda", generator=g)
+    dw0 = dw.clone()
+    ops.linear_dw(dy, x, dw, accumulate=True)
+    ref = dw0 + dy.float().t() @ x.float()
+    assert _rel(dw, ref) < 5e-3
+
+
+@cuda
+def test_gemm_bf16_strided_rows_and_beta_output(ops):
+    """A with row stride > K (CLS rows of a [B,N,D] buffer) and C written with ldc, beta=1."""
+    g = torch.Generator(device="cuda").manual_seed(3)
+    B, Ntok, D = 40, 5, 128
+    seq = torch.randn(B * Ntok, D, device="cuda", generator=g).bfloat16()
+    cls = seq.view(B, Ntok, D)[:, 0]
+    w = (torch.randn(D, D, device="cuda", generator=g) / math.sqrt(D)).bfloat16()
+    y = ops.linear(cls, w)
+    assert _rel(y, cls.float() @ w.float().t()) < 1e-2
+    out = torch.randn(B * Ntok, D, device="cuda", generator=g).bfloat16()
+    o0 = out.clone()
+    tgt = out.view(B, Ntok, D)[:, 0]
+    ops.linear_dx(y, w, out=tgt, beta=1.0)
+    ref = o0.view(B, Ntok, D)[:, 0].float() + y.float() @ w.float()
+    assert _rel(out.view(B, Ntok, D)[:, 0], ref) < 1e-2
+    assert torch.equal(out.view(B, Ntok, D)[:, 1:], o0.view(B, Ntok, D)[:, 1:])
+
+
+# ------------------------------------------------------------- LayerNorm ----
+@cuda
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cols,eps", [(768, 1e-12), (1536, 1e-5), (32, 1e-5)])
+def test_layernorm(ops, dtype, cols, eps):
+    g = torch.Generator(device="cuda").manual_seed(4)
+    rows = 1000
+    x = (torch.randn(rows, cols, device="cuda", generator=g) * 3 + 1).to(dtype)
+    w = torch.randn(cols, device="cuda", generator=g)
+    b = torch.randn(cols, device="cuda", generator=g)
+    dy = torch.randn(rows, cols, device="cuda", generator=g).to(dtype)
+    dres = torch.randn(rows, cols, device="cuda", generator=g).to(dtype)
+    y, mu, rs = ops.layernorm_fwd(x, w, b, eps)
+    xr = x.float().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    yr = F.layer_norm(xr, (cols,), wr, br, eps)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert _rel(y, yr) < tol
+    yr.backward(dy.float())
+    dw = torch.empty(cols, device="cuda")
+    db = torch.empty(cols, device="cuda")
+    dx = ops.layernorm_bwd(dy, x, w, mu, rs, dw, db, dres=dres)
+    assert _rel(dx, xr.grad + dres.float()) < tol
+    assert _rel(dw, wr.grad) < (1e-5 if dtype == torch.float32 else 5e-3)
+    assert _rel(db, br.grad) < (1e-5 if dtype == torch.float32 else 5e-3)
+
+
+# ------------------------------------------------------------- attention ----
+def _attn_ref(q, k, v, scale, causal, key_pad):
+    s = torch.einsum("bhqd,bhkd->bhqk", q, k) * scale
+    if causal:
+        Nq, Nk = s.shape[-2:]
+        s = s.masked_fill(torch.ones(Nq, Nk, dtype=torch.bool, device=s.device).triu(1), float("-inf"))
+    if key_pad is not None:
+        s = s.masked_fill(key_pad[:, None, None, :], float("-inf"))
+    return torch.einsum("bhqk,bhkd->bhqd", torch.softmax(s, -1), v)
+
+
+@cuda
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", ["vit", "dec_self", "dec_cross_gap", "clip"])
+def test_attention_fwd_bwd(ops, dtype, case):
+    from capk.ops import HeadView
+    g = torch.Generator(device="cuda").manual_seed(5)
+    if case == "vit":
+        B, H, Nq, Nk, hd, causal, gap = 3, 4, 197, 197, 64, False, 0
+    elif case == "dec_self":
+        B, H, Nq, Nk, hd, causal, gap = 4, 8, 20, 20, 96, True, 0
+    elif case == "dec_cross_gap":
+        B, H, Nq, Nk, hd, causal, gap = 3, 8, 20, 196, 96, False, 1
+    else:
+        B, H, Nq, Nk, hd, causal, gap = 5, 12, 50, 50, 64, False, 0
+    D = H * hd
+    q = torch.randn(B * Nq, D, device="cuda", generator=g).to(dtype)
+    kvrows = (B - 1) * (Nk + gap) + Nk
+    kv = torch.randn(kvrows, 2 * D, device="cuda", generator=g).to(dtype)
+    do = torch.randn(B * Nq, D, device="cuda", generator=g).to(dtype)
+    key_pad = None
+    if case == "dec_self":
+        key_pad = torch.zeros(B, Nk, dtype=torch.bool, device="cuda")
+        key_pad[1, 15:] = True
+        key_pad[3, 19] = True
+    o = torch.empty(B * Nq, D, device="cuda", dtype=dtype)
+    qv = HeadView(q, 0, Nq * D, D)
+    kview = HeadView(kv, 0, (Nk + gap) * 2 * D, 2 * D)
+    vview = HeadView(kv, D, (Nk + gap) * 2 * D, 2 * D)
+    ov = HeadView(o, 0, Nq * D, D)
+    scale = 1.0 / math.sqrt(hd)
+    lse, kp = ops.attention_fwd(qv, kview, vview, ov, B, H, Nq, Nk, hd, scale, causal=causal, key_pad=key_pad)
+
+    def heads_of(t, rows_per_b, n, col0):
+        t = t.float()
+        out = torch.stack([t[b * rows_per_b:b * rows_per_b + n, col0:col0 + D] for b in range(B)])
+        return out.view(B, n, H, hd).transpose(1, 2).contiguous()
+
+    qr = heads_of(q, Nq, Nq, 0).requires_grad_(True)
+    kr = heads_of(kv, Nk + gap, Nk, 0).requires_grad_(True)
+    vr = heads_of(kv, Nk + gap, Nk, D).requires_grad_(True)
+    ref = _attn_ref(qr, kr, vr, scale, causal, key_pad)
+    got = o.float().view(B, Nq, H, hd).transpose(1, 2)
+    tol = 1e-5 if dtype == torch.float32 else 1.5e-2
+    assert _rel(got, ref) < tol
+    ref.backward(do.float().view(B, Nq, H, hd).transpose(1, 2))
+    dq = torch.empty_like(q)
+    dkv = torch.zeros_like(kv)
+    ops.attention_bwd(qv, kview, vview, ov, HeadView(do, 0, Nq * D, D), lse, HeadView(dq, 0, Nq * D, D),
+                      HeadView(dkv, 0, (Nk + gap) * 2 * D, 2 * D), HeadView(dkv, D, (Nk + gap) * 2 * D, 2 * D),
+                      B, H, Nq, Nk, hd, scale, causal=causal, key_pad_u8=kp)
+    tolb = 1e-4 if dtype == torch.float32 else 3e-2
+    assert _rel(dq.float().view(B, Nq, H, hd).transpose(1, 2), qr.grad) < tolb
+    assert _rel(heads_of(dkv, Nk + gap, Nk, 0), kr.grad) < tolb
+    assert _rel(heads_of(dkv, Nk + gap, Nk, D), vr.grad) < tolb
+    if gap:
+        gap_rows = torch.stack([dkv[b * (Nk + gap) + Nk] for b in range(B - 1)])
+        assert float(gap_rows.abs().max()) == 0.0
+
+
+# ------------------------------------------------------ CE / embeddings -----
+@cuda
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_shifted_ce(ops, dtype):
+    g = torch.Generator(device="cuda").manual_seed(6)
+    B, T, V = 6, 9, 50257
+    Vp = (V + 63) // 64 * 64
+    logits = torch.randn(B * T, Vp, device="cuda", generator=g).to(dtype)
+    tg = torch.randint(0, V, (B, T), device="cuda", generator=g)
+    pad = V - 1
+    tg[2, 4:] = pad
+    loss = ops.shifted_ce(logits, tg, B, T, V, pad)
+    lr = logits.float()[:, :V].view(B, T, V).requires_grad_(True)
+    ref = F.cross_entropy(lr[:, :-1].reshape(-1, V), tg[:, 1:].reshape(-1), ignore_index=pad)
+    assert abs(float(loss[0]) - float(ref)) < 1e-4 * max(1.0, abs(float(ref)))
+    ref.backward()
+    dl = torch.empty_like(logits)
+    gs = torch.tensor([0.5], device="cuda")
+    ops.shifted_ce(logits, tg, B, T, V, pad, want_loss=False, dlogits=dl, grad_scale=gs)
+    assert _rel(dl[:, :V].view(B, T, V), 0.5 * lr.grad) < (1e-5 if dtype == torch.float32 else 1e-2)
+    assert float(dl[:, V:].float().abs().max()) == 0.0
+
+
+@cuda
+def test_embedding_fwd_bwd(ops):
+    g = torch.Generator(device="cuda").manual_seed(7)
+    B, T, D, V = 4, 7, 64, 100
+    ids = torch.randint(0, V, (B, T), device="cuda", generator=g)
+    ids[0, 3] = 5
+    table = torch.randn(V, D, device="cuda", generator=g)
+    pos = torch.randn(50, D, device="cuda", generator=g)
+    out = ops.embedding_fwd(ids, table, pos, 0, torch.float32)
+    assert torch.allclose(out.view(B, T, D), table[ids] + pos[:T][None], atol=1e-6)
+    dout = torch.randn(B * T, D, device="cuda", generator=g)
+    dt = torch.zeros(V, D, device="cuda")
+    dp = torch.zeros(50, D, device="cuda")
+    ops.embedding_bwd(ids, dout, 5, dt, dp, 0)
+    ref_t = torch.zeros(V, D, device="cuda").index_add_(0, ids.reshape(-1), dout)
+    ref_t[5] = 0
+    assert torch.allclose(dt, ref_t, atol=1e-5)
+    assert torch.allclose(dp[:T], dout.view(B, T, D).sum(0), atol=1e-5)
+
+
+@cuda
+def test_adamw_matches_oracle(ops):
+    from oracle import train as otrain
+    g = torch.Generator(device="cuda").manual_seed(8)
+    n = 1000003
+    p = torch.randn(n, device="cuda", generator=g)
+    gr = torch.randn(n, device="cuda", generator=g)
+    m = torch.zeros(n, device="cuda")
+    v = torch.zeros(n, device="cuda")
+    sh = torch.empty(n, device="cuda", dtype=torch.bfloat16)
+    pc, mc, vc = p.cpu(), m.cpu(), v.cpu()
+    for step in (1, 2, 3):
+        ops.adamw(p, gr, m, v, sh, 1e-3, 0.01, 0.9, 0.999, 1e-8, step)
+        otrain.adamw_step(pc, gr.cpu(), mc, vc, step, 1e-3, 0.01)
+    torch.testing.assert_close(p.cpu(), pc, rtol=1e-6, atol=1e-7)
+    assert torch.equal(sh, p.bfloat16())
+
+
+@cuda
+def test_patchify_assemble(ops):
+    g = torch.Generator(device="cuda").manual_seed(9)
+    B, C, Hh, Ww, P, D = 3, 3, 32, 32, 8, 64
+    img = torch.randn(B, C, Hh, Ww, device="cuda", generator=g)
+    pt = ops.patchify(img, P, torch.float32)
+    ref = F.unfold(img, P, stride=P).transpose(1, 2).reshape(-1, C * P * P)
+    assert torch.equal(pt, ref)
+    Np = (Hh // P) * (Ww // P)
+    pe = torch.randn(B * Np, D, device="cuda", generator=g)
+    cls = torch.randn(D, device="cuda", generator=g)
+    pos = torch.randn(Np + 1, D, device="cuda", generator=g)
+    x = ops.vit_assemble(pe, cls, pos, B, Np, D).view(B, Np + 1, D)
+    ref = torch.cat([cls.expand(B, 1, D), pe.view(B, Np, D)], 1) + pos
+    assert torch.allclose(x, ref)
+    dx = torch.randn(B * (Np + 1), D, device="cuda", generator=g)
+    dcls = torch.empty(D, device="cuda")
+    dpos = torch.empty(Np + 1, D, device="cuda")
+    dpatch = ops.vit_assemble_bwd(dx, B, Np, D, dcls, dpos)
+    assert torch.equal(dpatch.view(B, Np, D), dx.view(B, Np + 1, D)[:, 1:])
+    assert torch.allclose(dpos, dx.view(B, Np + 1, D).sum(0), atol=1e-5)
+    assert torch.allclose(dcls, dx.view(B, Np + 1, D)[:, 0].sum(0), atol=1e-5)
