@@ -146,7 +146,7 @@ class _DecoderFn(torch.autograd.Function):
             saved_layers.append((x_in, qkv, a, lse1, kp, s1, mu1, rs1, x1, qc, kv, c, lse2, s2, mu2, rs2, x2, f_pre,
                                  f, s3, mu3, rs3))
         ol = m.output_layer
-        wout = ol._capk_pad_bf16 if dt == torch.bfloat16 else ol._capk_pad_master
+        wout = ol.weight._capk_pad_bf16 if dt == torch.bfloat16 else ol.weight._capk_pad_master
         logits_pad = ops.linear(x, wout, _pad_bias(ol))
         ctx.m = m
         ctx.dims = (B, S, T, D, H, hd, scale, V, Vp, rpb, M_ext)
@@ -170,13 +170,13 @@ class _DecoderFn(torch.autograd.Function):
         # ---- LM head
         if dlogits is not None:
             dl = _padded_grad(dlogits, ctx.logits_pad, BT, V, Vp)
-            ops.linear_dw(dl, xT, ol._capk_pad_grad)
+            ops.linear_dw(dl, xT, ol.weight._capk_pad_grad)
             ops.colsum(dl, _pad_bias_grad(ol))
-            wout = ol._capk_pad_bf16 if dt == torch.bfloat16 else ol._capk_pad_master
+            wout = ol.weight._capk_pad_bf16 if dt == torch.bfloat16 else ol.weight._capk_pad_master
             dx = ops.linear_dx(dl, wout)
         else:
             dx = torch.zeros(BT, D, dtype=dt, device=dev)
-            ops.zero_(ol._capk_pad_grad)
+            ops.zero_(ol.weight._capk_pad_grad)
             ops.zero_(_pad_bias_grad(ol))
         if dhidden is not None:
             dx = dx + dhidden.reshape(BT, D)

@@ -107,28 +107,33 @@ __device__ __forceinline__ int swz_k(int r) { return (r >> 1) & 7; }
 // c ^ (f(r)<<1), f(r) = (r&3) | ((r>>3)&1)<<2 -> conflict-free ds_read_b64_tr_b16.
 __device__ __forceinline__ int swz_t(int r) { return (((r & 3) | (((r >> 3) & 1) << 2)) << 1); }
 
+// Stage one 128 x 64 operand tile into LDS (16 KiB, 4 x 1-KiB pieces per wave).
+// K-major operands use global_load_lds; MN-major (transposed) operands use
+// range-checked buffer_load ... lds whose descriptor ends at row K, so K-tail rows
+// of a split reduction (token counts that are not multiples of 64) read as 0.
 template <bool KMAJ>
 __device__ __forceinline__ void stage_tile(const bf16* __restrict__ X, int64_t ld, int rows, int row0,
-                                           int k0, char* lds_tile, int wave, int lane) {
+                                           int k0, char* lds_tile, int wave, int lane, __amdgpu_buffer_rsrc_t rsrc) {
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int ins = wave * 4 + t;
-    const bf16* src;
     if constexpr (KMAJ) {
       const int r = ins * 8 + (lane >> 3);
       const int lc = (lane & 7) ^ swz_k(r);
       int gr = row0 + r;
       gr = gr < rows ? gr : rows - 1;
-      src = X + (int64_t)gr * ld + k0 + lc * 8;
+      const bf16* src = X + (int64_t)gr * ld + k0 + lc * 8;
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(lds_tile + ins * 1024), 16, 0, 0);
     } else {
       const int kr = ins * 4 + (lane >> 4);
       const int lc = (lane & 15) ^ swz_t(kr);
       int gc = row0 + lc * 8;
       gc = gc + 8 <= rows ? gc : rows - 8;
-      src = X + (int64_t)(k0 + kr) * ld + gc;
+      const unsigned voff = (unsigned)(((int64_t)(k0 + kr) * ld + gc) * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(lds_tile + ins * 1024),
+                                               16, voff, 0, 0, 0);
     }
-    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(lds_tile + ins * 1024),
-                                     16, 0, 0);
   }
 }
 
@@ -165,7 +170,10 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const bf16* __restric
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int split = wg / ntiles, tile = wg % ntiles;
   const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
-  const int nk_all = K / BKT;
+  const int nk_all = (K + BKT - 1) / BKT;
+  // range-checked descriptors for MN-major operands: [0, K*ld) elements are valid
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)((int64_t)K * lda * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, (int)((int64_t)K * ldb * 2), 0x00020000);
   const int kt_per = (nk_all + splits - 1) / splits;
   const int kt0 = split * kt_per;
   const int kt1 = min(nk_all, kt0 + kt_per);
@@ -178,8 +186,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const bf16* __restric
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   if (nk > 0) {
-    stage_tile<AK>(A, lda, M, m0, kt0 * BKT, smem, wave, lane);
-    stage_tile<BK>(B, ldb, N, n0, kt0 * BKT, smem + TILE_BYTES, wave, lane);
+    stage_tile<AK>(A, lda, M, m0, kt0 * BKT, smem, wave, lane, rsA);
+    stage_tile<BK>(B, ldb, N, n0, kt0 * BKT, smem + TILE_BYTES, wave, lane, rsB);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -188,8 +196,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const bf16* __restric
     char* sc = smem + cur * STAGE_BYTES;
     if (kt + 1 < nk) {
       char* sn = smem + (cur ^ 1) * STAGE_BYTES;
-      stage_tile<AK>(A, lda, M, m0, (kt0 + kt + 1) * BKT, sn, wave, lane);
-      stage_tile<BK>(B, ldb, N, n0, (kt0 + kt + 1) * BKT, sn + TILE_BYTES, wave, lane);
+      stage_tile<AK>(A, lda, M, m0, (kt0 + kt + 1) * BKT, sn, wave, lane, rsA);
+      stage_tile<BK>(B, ldb, N, n0, (kt0 + kt + 1) * BKT, sn + TILE_BYTES, wave, lane, rsB);
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -314,7 +322,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 
 static int choose_splits(int M, int N, int K) {
   const int tiles = cdiv(M, BM) * cdiv(N, BN);
-  const int nk = K / BKT;
+  const int nk = cdiv(K, BKT);
   int s = 1;
   // aim for >= 2 waves of workgroups over 256 CUs (2 WGs/CU resident)
   while (tiles * s < 512 && s * 2 <= 16 && nk / (s * 2) >= 4) s *= 2;
@@ -327,7 +335,7 @@ using namespace capk;
 
 extern "C" size_t capk_gemm_workspace(int in_dtype, int out_dtype, int M, int N, int K) {
   (void)out_dtype;
-  if (in_dtype != CAPK_BF16 || K % BKT) return 0;
+  if (in_dtype != CAPK_BF16) return 0;
   const int s = choose_splits(M, N, K);
   return s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
 }
@@ -354,11 +362,13 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
   }
   CAPK_CHECK_ARG(in_dtype == CAPK_BF16, "capk_gemm: unknown in_dtype %d", in_dtype);
   CAPK_CHECK_ARG(out_dtype == CAPK_BF16 || out_dtype == CAPK_F32, "capk_gemm: unknown out_dtype");
-  CAPK_CHECK_ARG(K % BKT == 0, "capk_gemm(bf16): K=%d must be a multiple of %d", K, BKT);
+  CAPK_CHECK_ARG(!(a_kmajor || b_kmajor) || K % BKT == 0,
+                 "capk_gemm(bf16): K=%d must be a multiple of %d when an operand is K-major", K, BKT);
   CAPK_CHECK_ARG(N % 8 == 0, "capk_gemm(bf16): N=%d must be a multiple of 8", N);
-  CAPK_CHECK_ARG(a_kmajor || M % 8 == 0, "capk_gemm(bf16): M-major A needs M %% 8 == 0");
-  CAPK_CHECK_ARG(b_kmajor || N % 8 == 0, "capk_gemm(bf16): N-major B needs N %% 8 == 0");
-  CAPK_CHECK_ARG(M >= 8 && N >= 8, "capk_gemm(bf16): M, N >= 8");
+  CAPK_CHECK_ARG(a_kmajor || (M % 8 == 0 && M >= 8), "capk_gemm(bf16): M-major A needs M %% 8 == 0");
+  CAPK_CHECK_ARG(b_kmajor || (N % 8 == 0 && N >= 8), "capk_gemm(bf16): N-major B needs N %% 8 == 0");
+  CAPK_CHECK_ARG((a_kmajor || (int64_t)K * lda * 2 < (1ll << 31)) && (b_kmajor || (int64_t)K * ldb * 2 < (1ll << 31)),
+                 "capk_gemm(bf16): MN-major operand larger than 2 GiB");
   const int64_t esz = out_dtype == CAPK_F32 ? 4 : 2;
   CAPK_CHECK_ARG(((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % 8 == 0 && ldb % 8 == 0,
                  "capk_gemm(bf16): A/B must be 16-B aligned with lda, ldb %% 8 == 0");

@@ -77,8 +77,20 @@ def test_golden_step_fp32(golden_dir):
         for k in z.files:
             if k.startswith(tag):
                 n = k[3:]
-                np.testing.assert_allclose(named[n].detach().cpu().numpy(), z[k], rtol=1e-5, atol=1e-6,
-                                           err_msg=f"{tag}{n}")
+                got, want = named[n].detach().cpu().numpy(), z[k]
+                g = z["grad/" + n] if "grad/" + n in z.files else None
+                if g is not None:
+                    # Elements whose reference gradient is pure rounding noise (the key-projection
+                    # bias of softmax attention has an analytically ZERO gradient): Adam turns noise
+                    # into +-lr updates whose sign is not reproducible on any other device, so only
+                    # the |update| <= lr bound per step is a meaningful check there.
+                    noise = np.abs(g) < 1e-7
+                    if noise.any():
+                        lim = sum(float(x) for x in lrs[:step + 1]) * 1.01
+                        p0 = z["p0/" + n]
+                        assert np.all(np.abs(got[noise] - p0[noise]) <= lim + 1e-6), f"{tag}{n}"
+                        got, want = got[~noise], want[~noise]
+                np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-6, err_msg=f"{tag}{n}")
 
 
 @cuda
