@@ -90,7 +90,7 @@ __device__ __forceinline__ void stage_rows(bf16* img, int st, const bf16* src, i
 }
 
 template <int HDP>
-__global__ __launch_bounds__(256) void attn_fwd_bf16(AttnArgs a) {
+__global__ __launch_bounds__(512) void attn_fwd_bf16(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -115,7 +115,7 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(AttnArgs a) {
 
   const int NKB = NKP / 16;
   const bf16* qsrc = (const bf16*)a.q + (int64_t)b * a.q_bs + hoff;
-  for (int qt = wave; qt * 16 < a.Nq; qt += 4) {
+  for (int qt = wave; qt * 16 < a.Nq; qt += (int)(blockDim.x >> 6)) {
     const int qi = qt * 16 + (lane & 15);
     bf16x8 qf[HDP / 32];
 #pragma unroll
@@ -191,7 +191,7 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(AttnArgs a) {
 }
 
 template <int HDP>
-__global__ __launch_bounds__(256) void attn_bwd_bf16(AttnArgs a) {
+__global__ __launch_bounds__(512) void attn_bwd_bf16(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -208,24 +208,35 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16(AttnArgs a) {
   stage_rows<HDP>(dOs, ST, (const bf16*)a.dout, (int64_t)b * a.do_bs, a.do_rs, a.Nq, NQP, hoff, a.hd);
   stage_rows<HDP>(Ks, ST, (const bf16*)a.k, (int64_t)b * a.k_bs, a.k_rs, a.Nk, NKP, hoff, a.hd);
   stage_rows<HDP>(Vs, ST, (const bf16*)a.v, (int64_t)b * a.v_bs, a.v_rs, a.Nk, NKP, hoff, a.hd);
-  // delta_q = sum_d dO*O (fp32), one wave per query row
-  for (int q = wave; q < NQP; q += 4) {
+  // lse and delta_q = sum_d dO*O (fp32): 16-B vector loads of O, dO from LDS,
+  // per-chunk partial dots -> LDS -> one thread per query sums them.
+  constexpr int NCH = HDP / 8;
+  float* part = del_s + NQP;  // [NQP][NCH]
+  for (int q = threadIdx.x; q < NQP; q += blockDim.x)
+    lse_s[q] = q < a.Nq ? a.lse_in[((int64_t)b * a.H + h) * a.Nq + q] : 0.f;
+  for (int idx = threadIdx.x; idx < NQP * NCH; idx += blockDim.x) {
+    const int q = idx / NCH, c = idx % NCH;
     float s = 0.f;
-    if (q < a.Nq) {
-      const bf16* orow = (const bf16*)a.o + (int64_t)b * a.o_bs + (int64_t)q * a.o_rs + hoff;
-      const bf16* drow = (const bf16*)a.dout + (int64_t)b * a.do_bs + (int64_t)q * a.do_rs + hoff;
-      for (int d = lane; d < a.hd; d += 64) s += (float)orow[d] * (float)drow[d];
+    if (q < a.Nq && c * 8 < a.hd) {
+      const bf16x8 ov = ld8((const bf16*)a.o + (int64_t)b * a.o_bs + (int64_t)q * a.o_rs + hoff + c * 8);
+      const bf16x8 dv = *(const bf16x8*)(dOs + q * ST + c * 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += (float)ov[i] * (float)dv[i];
     }
-    s = wave_sum(s);
-    if (lane == 0) {
-      del_s[q] = s;
-      lse_s[q] = q < a.Nq ? a.lse_in[((int64_t)b * a.H + h) * a.Nq + q] : 0.f;
-    }
+    part[idx] = s;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < NQP; q += blockDim.x) {
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) s += part[q * NCH + c];
+    del_s[q] = s;
   }
   __syncthreads();
 
   // ---- phase A: dK, dV (waves own 16-key blocks)
-  for (int kb = wave; kb < NKP / 16; kb += 4) {
+  const int nwaves = blockDim.x >> 6;
+  for (int kb = wave; kb < NKP / 16; kb += nwaves) {
     const int keyl = kb * 16 + (lane & 15);
     f32x4 dvt[HDP / 16], dkt[HDP / 16];
 #pragma unroll
@@ -275,7 +286,7 @@ __global__ __launch_bounds__(256) void attn_bwd_bf16(AttnArgs a) {
   }
 
   // ---- phase B: dQ (waves own 16-query blocks)
-  for (int qb = wave; qb < NQP / 16; qb += 4) {
+  for (int qb = wave; qb < NQP / 16; qb += nwaves) {
     const int ql = qb * 16 + (lane & 15);
     const float lq = lse_s[ql], dq_del = del_s[ql];
     f32x4 dqt[HDP / 16];
@@ -434,7 +445,7 @@ static size_t fwd_smem(int Nk, int hdp) {
 }
 static size_t bwd_smem(int Nq, int Nk, int hdp) {
   const int NQP = (Nq + 31) & ~31, NKP = (Nk + 31) & ~31;
-  return (size_t)(2 * NQP + 2 * NKP) * (hdp + 8) * 2 + (size_t)2 * NQP * 4;
+  return (size_t)(2 * NQP + 2 * NKP) * (hdp + 8) * 2 + (size_t)2 * NQP * 4 + (size_t)NQP * (hdp / 8) * 4;
 }
 
 template <typename K>
@@ -496,7 +507,7 @@ extern "C" int capk_attention_fwd(int dtype, int B, int H, int Nq, int Nk, int h
                  "capk_attention_fwd(bf16): strides must allow 16-B vector access");
   const int hdp = hdp_of(hd);
   const size_t shm = fwd_smem(Nk, hdp);
-  const dim3 grid(B * H), block(256);
+  const dim3 grid(B * H), block(Nq > 64 ? 512 : 256);
   switch (hdp) {
     case 32: return launch_dyn(attn_fwd_bf16<32>, grid, block, shm, st, a, "attn_fwd_bf16");
     case 64: return launch_dyn(attn_fwd_bf16<64>, grid, block, shm, st, a, "attn_fwd_bf16");
@@ -540,7 +551,7 @@ extern "C" int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int h
   const int hdp = hdp_of(hd);
   const size_t shm = bwd_smem(Nq, Nk, hdp);
   CAPK_CHECK_ARG(shm <= 160 * 1024, "capk_attention_bwd: LDS %zu > 160 KiB", shm);
-  const dim3 grid(B * H), block(256);
+  const dim3 grid(B * H), block((Nq > 64 || Nk > 64) ? 512 : 256);
   switch (hdp) {
     case 32: return launch_dyn(attn_bwd_bf16<32>, grid, block, shm, st, a, "attn_bwd_bf16");
     case 64: return launch_dyn(attn_bwd_bf16<64>, grid, block, shm, st, a, "attn_bwd_bf16");

@@ -110,6 +110,27 @@ __device__ __forceinline__ float act_grad(int act, float x) {
   }
 }
 
+// Fast exact-GELU forms for the bf16 epilogues: erf by Abramowitz & Stegun 7.1.26
+// (|error| <= 1.5e-7, far below bf16 resolution), with the exp(-x^2/2) shared by
+// Phi(x) and phi(x).  The fp32 parity path keeps erff (act_fwd / act_grad above).
+__device__ __forceinline__ void phi_fast(float x, float& cdf, float& pdf) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __frcp_rn(1.0f + 0.3275911f * z);
+  const float e = __expf(-z * z);
+  const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  const float erfz = 1.0f - poly * e;
+  cdf = 0.5f * (1.0f + (x >= 0.f ? erfz : -erfz));
+  pdf = 0.3989422804014327f * e;
+}
+__device__ __forceinline__ float act_fwd_fast(int act, float x) {
+  if (act == CAPK_ACT_GELU_ERF) { float c, p; phi_fast(x, c, p); return x * c; }
+  return act_fwd(act, x);
+}
+__device__ __forceinline__ float act_grad_fast(int act, float x) {
+  if (act == CAPK_ACT_GELU_ERF) { float c, p; phi_fast(x, c, p); return c + x * p; }
+  return act_grad(act, x);
+}
+
 // ------------------------------------------------------- wave reductions ----
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -16,6 +16,8 @@
 // Epilogue (both): alpha*acc + beta*C + bias[n] + residual[m,n], then forward
 // activation (optionally saving the pre-activation) or the backward form
 // acc * act'(aux).  bias is fp32; C/residual/preact/aux use the output dtype.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace capk {
@@ -61,11 +63,11 @@ __device__ __forceinline__ void epilogue8(const Epi& e, int m, int n, float (&v)
     Vec8<OutT>::load((const OutT*)e.aux + (int64_t)m * e.ldx + n, a);
     const int act = e.act & 15;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] *= act_grad(act, a[i]);
+    for (int i = 0; i < 8; ++i) v[i] *= act_grad_fast(act, a[i]);
   } else if (e.act) {
     if (e.pre) Vec8<OutT>::store((OutT*)e.pre + (int64_t)m * e.ldx + n, v);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = act_fwd(e.act, v[i]);
+    for (int i = 0; i < 8; ++i) v[i] = act_fwd_fast(e.act, v[i]);
   }
   Vec8<OutT>::store((OutT*)e.C + (int64_t)m * e.ldc + n, v);
 }
@@ -93,41 +95,62 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 }
 
 // ============================================================ bf16 kernel ===
-constexpr int BM = 128, BN = 128, BKT = 64;
-constexpr int TILE_BYTES = BM * BKT * 2;             // 16 KiB per operand tile
-constexpr int STAGE_BYTES = 2 * TILE_BYTES;          // A + B
-constexpr int EPI_LD = BN + 4;                       // fp32 staging row (floats)
-constexpr int EPI_BYTES = BM * EPI_LD * 4;
-constexpr int SMEM_BYTES = (2 * STAGE_BYTES > EPI_BYTES) ? 2 * STAGE_BYTES : EPI_BYTES;
+// Two tile configurations of one kernel template:
+//   <128, 2>: 128x128 block, 4 waves, 2-stage LDS ring (64 KiB -> 2 WGs/CU)  [small grids]
+//   <256, 3>: 256x128 block, 8 waves, 3-stage LDS ring (144 KiB -> 1 WG/CU)  [large grids]
+// Every wave owns a 64x64 output (4x4 16x16 blocks).  The ring keeps NST-1 K-tiles in
+// flight: a counted `s_waitcnt vmcnt` retires only the tile about to be read and a raw
+// s_barrier (no vmcnt(0) drain) publishes it (cdna guide §5 "Pipelining across barriers").
+constexpr int BN = 128, BKT = 64;  // BKT: K granularity required of K-major operands (max BK)
 
-// K-major image [128 rows][64 k] (128-B rows): 16-B chunk c of row r stored at
-// chunk c ^ ((r>>1)&7) -> conflict-free ds_read_b128 for the 16x16x32 operand.
-__device__ __forceinline__ int swz_k(int r) { return (r >> 1) & 7; }
-// MN-major image [64 k][128 mn] (256-B rows): chunk c of k-row r stored at
+// K-major image [rows][BK k]: 16-B chunk c of row r stored at chunk c ^ swz_k(r):
+// conflict-free ds_read_b128 of the 16x16x32 operand for 128-B (BK=64) and 64-B (BK=32) rows.
+template <int BKX>
+__device__ __forceinline__ int swz_k(int r) { return BKX == 64 ? ((r >> 1) & 7) : ((r >> 1) & 3); }
+// MN-major image [BK k][rows] (2*rows-B rows): chunk c of k-row r stored at
 // c ^ (f(r)<<1), f(r) = (r&3) | ((r>>3)&1)<<2 -> conflict-free ds_read_b64_tr_b16.
 __device__ __forceinline__ int swz_t(int r) { return (((r & 3) | (((r >> 3) & 1) << 2)) << 1); }
 
-// Stage one 128 x 64 operand tile into LDS (16 KiB, 4 x 1-KiB pieces per wave).
+template <int BMX, int BKX, int NST>
+struct Cfg {
+  static constexpr int WAVES = BMX / 32;                 // (BMX/64) x 2 waves, 64x64 outputs each
+  static constexpr int THREADS = WAVES * 64;
+  static constexpr int A_BYTES = BMX * BKX * 2;
+  static constexpr int B_BYTES = BN * BKX * 2;
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int A_PIECES = A_BYTES / 1024 / WAVES;  // 1-KiB LDS-DMA pieces per wave
+  static constexpr int B_PIECES = B_BYTES / 1024 / WAVES;
+  static constexpr int VM_PER_STAGE = A_PIECES + B_PIECES;
+  static constexpr int EPI_LD = BN + 4;
+  static constexpr int EPI_BYTES = 64 * EPI_LD * 4;       // epilogue staged 64 rows at a time
+  static constexpr int SMEM = (NST * STAGE > EPI_BYTES) ? NST * STAGE : EPI_BYTES;
+};
+
+// Stage one ROWS x BKX operand tile into LDS: NP 1-KiB pieces per wave starting at piece p0.
 // K-major operands use global_load_lds; MN-major (transposed) operands use
 // range-checked buffer_load ... lds whose descriptor ends at row K, so K-tail rows
 // of a split reduction (token counts that are not multiples of 64) read as 0.
-template <bool KMAJ>
+template <bool KMAJ, int ROWS, int BKX, int NP>
 __device__ __forceinline__ void stage_tile(const bf16* __restrict__ X, int64_t ld, int rows, int row0,
-                                           int k0, char* lds_tile, int wave, int lane, __amdgpu_buffer_rsrc_t rsrc) {
+                                           int k0, char* lds_tile, int p0, int lane, __amdgpu_buffer_rsrc_t rsrc) {
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int ins = wave * 4 + t;
+  for (int t = 0; t < NP; ++t) {
+    const int ins = p0 + t;
     if constexpr (KMAJ) {
-      const int r = ins * 8 + (lane >> 3);
-      const int lc = (lane & 7) ^ swz_k(r);
+      constexpr int CPR = BKX / 8;         // chunks per row
+      constexpr int RPP = 64 / CPR;        // rows per piece
+      const int r = ins * RPP + lane / CPR;
+      const int lc = (lane % CPR) ^ swz_k<BKX>(r);
       int gr = row0 + r;
       gr = gr < rows ? gr : rows - 1;
       const bf16* src = X + (int64_t)gr * ld + k0 + lc * 8;
       __builtin_amdgcn_global_load_lds((const void*)src,
                                        (__attribute__((address_space(3))) void*)(lds_tile + ins * 1024), 16, 0, 0);
     } else {
-      const int kr = ins * 4 + (lane >> 4);
-      const int lc = (lane & 15) ^ swz_t(kr);
+      constexpr int CPR = ROWS / 8;          // 16-B chunks per k-row
+      constexpr int RPP = 64 / CPR;          // k-rows per 1-KiB piece
+      const int kr = ins * RPP + lane / CPR;
+      const int lc = (lane % CPR) ^ swz_t(kr);
       int gc = row0 + lc * 8;
       gc = gc + 8 <= rows ? gc : rows - 8;
       const unsigned voff = (unsigned)(((int64_t)(k0 + kr) * ld + gc) * 2);
@@ -137,18 +160,19 @@ __device__ __forceinline__ void stage_tile(const bf16* __restrict__ X, int64_t l
   }
 }
 
-template <bool KMAJ>
+template <bool KMAJ, int ROWS, int BKX>
 __device__ __forceinline__ bf16x8 read_frag(const char* tile, int rbase, int s, int lane) {
   if constexpr (KMAJ) {
     const int r = rbase + (lane & 15);
     const int lc = s * 4 + (lane >> 4);
-    return *(const bf16x8*)(tile + r * 128 + ((lc ^ swz_k(r)) << 4));
+    return *(const bf16x8*)(tile + r * (BKX * 2) + ((lc ^ swz_k<BKX>(r)) << 4));
   } else {
+    constexpr int RB = ROWS * 2;
     const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
     const int lc = (rbase >> 3) + (p >> 1);
     const int kr0 = s * 32 + g * 8 + q, kr1 = kr0 + 4;
-    const char* a0 = tile + kr0 * 256 + ((lc ^ swz_t(kr0)) << 4) + (p & 1) * 8;
-    const char* a1 = tile + kr1 * 256 + ((lc ^ swz_t(kr1)) << 4) + (p & 1) * 8;
+    const char* a0 = tile + kr0 * RB + ((lc ^ swz_t(kr0)) << 4) + (p & 1) * 8;
+    const char* a1 = tile + kr1 * RB + ((lc ^ swz_t(kr1)) << 4) + (p & 1) * 8;
     bf16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, a0));
     bf16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, a1));
     bf16x8 r;
@@ -158,26 +182,47 @@ __device__ __forceinline__ bf16x8 read_frag(const char* tile, int rbase, int s, 
   }
 }
 
-template <bool AK, bool BK, typename OutT>
-__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const bf16* __restrict__ A, int64_t lda,
-                                                           const bf16* __restrict__ B, int64_t ldb,
-                                                           int M, int N, int K, int splits, Epi e,
-                                                           float* __restrict__ ws) {
-  __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
+template <int VM>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (VM == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (VM == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (VM == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (VM == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (VM == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (VM == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else static_assert(VM == 0, "unsupported vmcnt");
+}
+
+// Main loop: an NST-deep LDS ring.  Before reading K-tile kt a counted
+// `s_waitcnt vmcnt` retires only that tile (the NST-2 younger ones stay in flight),
+// then a raw s_barrier publishes it and the slot freed one iteration ago is refilled.
+template <int BMX, int BKX, int NST, bool AK, bool BK, typename OutT>
+__global__ __launch_bounds__(BMX / 32 * 64) void gemm_bf16_kernel(
+    const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb, int M, int N, int K, int splits,
+    Epi e, float* __restrict__ ws) {
+  using C = Cfg<BMX, BKX, NST>;
+  __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN, ntiles = ntm * ntn;
+  const int ntm = (M + BMX - 1) / BMX, ntn = (N + BN - 1) / BN, ntiles = ntm * ntn;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int split = wg / ntiles, tile = wg % ntiles;
-  const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
-  const int nk_all = (K + BKT - 1) / BKT;
-  // range-checked descriptors for MN-major operands: [0, K*ld) elements are valid
-  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)((int64_t)K * lda * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, (int)((int64_t)K * ldb * 2), 0x00020000);
+  const int m0 = (tile / ntn) * BMX, n0 = (tile % ntn) * BN;
+  const int nk_all = (K + BKX - 1) / BKX;
   const int kt_per = (nk_all + splits - 1) / splits;
   const int kt0 = split * kt_per;
   const int kt1 = min(nk_all, kt0 + kt_per);
   const int nk = max(0, kt1 - kt0);
+  // range-checked descriptors for MN-major operands: [0, K*ld) elements are valid
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)((int64_t)K * lda * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, (int)((int64_t)K * ldb * 2), 0x00020000);
+
+  auto stage = [&](int kt, int slot) {
+    char* base = smem + slot * C::STAGE;
+    stage_tile<AK, BMX, BKX, C::A_PIECES>(A, lda, M, m0, (kt0 + kt) * BKX, base, wave * C::A_PIECES, lane, rsA);
+    stage_tile<BK, BN, BKX, C::B_PIECES>(B, ldb, N, n0, (kt0 + kt) * BKX, base + C::A_BYTES, wave * C::B_PIECES,
+                                         lane, rsB);
+  };
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -185,63 +230,63 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const bf16* __restric
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  if (nk > 0) {
-    stage_tile<AK>(A, lda, M, m0, kt0 * BKT, smem, wave, lane, rsA);
-    stage_tile<BK>(B, ldb, N, n0, kt0 * BKT, smem + TILE_BYTES, wave, lane, rsB);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    char* sc = smem + cur * STAGE_BYTES;
-    if (kt + 1 < nk) {
-      char* sn = smem + (cur ^ 1) * STAGE_BYTES;
-      stage_tile<AK>(A, lda, M, m0, (kt0 + kt + 1) * BKT, sn, wave, lane, rsA);
-      stage_tile<BK>(B, ldb, N, n0, (kt0 + kt + 1) * BKT, sn + TILE_BYTES, wave, lane, rsB);
-    }
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+  for (int p = 0; p < NST - 1; ++p)
+    if (p < nk) stage(p, p);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + NST - 2 < nk) wait_vm<(NST - 2) * C::VM_PER_STAGE>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + NST - 1 < nk) stage(kt + NST - 1, (kt + NST - 1) % NST);
+    const char* sc = smem + (kt % NST) * C::STAGE;
+#pragma unroll
+    for (int s = 0; s < BKX / 32; ++s) {
       bf16x8 af[4], bfr[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = read_frag<AK>(sc, wm * 64 + i * 16, s, lane);
+      for (int i = 0; i < 4; ++i) af[i] = read_frag<AK, BMX, BKX>(sc, wm * 64 + i * 16, s, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = read_frag<BK>(sc + TILE_BYTES, wn * 64 + j * 16, s, lane);
+      for (int j = 0; j < 4; ++j) bfr[j] = read_frag<BK, BN, BKX>(sc + C::A_BYTES, wn * 64 + j * 16, s, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 
-  // ---- epilogue: accumulators -> LDS (fp32, row-major) -> 8-wide rows
+  // ---- epilogue, 64 rows at a time: accumulators -> LDS (fp32) -> 8-wide rows
   float* stg = (float*)smem;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int h = 0; h < BMX / 64; ++h) {
+    if (wm == h) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-        const int col = wn * 64 + j * 16 + (lane & 15);
-        stg[row * EPI_LD + col] = acc[i][j][r];
-      }
-  __syncthreads();
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-  for (int it = 0; it < 8; ++it) {
-    const int idx = it * 256 + tid;
-    const int row = idx >> 4, col = (idx & 15) * 8;
-    const int gm = m0 + row, gn = n0 + col;
-    if (gm >= M || gn >= N) continue;
-    float v[8];
-    Vec8<float>::load(stg + row * EPI_LD + col, v);
-    if (ws) {
-      Vec8<float>::store(ws + ((int64_t)split * M + gm) * N + gn, v);
-    } else {
-      epilogue8<OutT>(e, gm, gn, v);
+          for (int r = 0; r < 4; ++r) {
+            const int row = i * 16 + (lane >> 4) * 4 + r;
+            const int col = wn * 64 + j * 16 + (lane & 15);
+            stg[row * C::EPI_LD + col] = acc[i][j][r];
+          }
     }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 64 * BN / 8 / C::THREADS; ++it) {
+      const int idx = it * C::THREADS + tid;
+      const int row = idx >> 4, col = (idx & 15) * 8;
+      const int gm = m0 + h * 64 + row, gn = n0 + col;
+      if (gm < M && gn < N) {
+        float v[8];
+        Vec8<float>::load(stg + row * C::EPI_LD + col, v);
+        if (ws) Vec8<float>::store(ws + ((int64_t)split * M + gm) * N + gn, v);
+        else epilogue8<OutT>(e, gm, gn, v);
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -320,13 +365,44 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
       }
 }
 
-static int choose_splits(int M, int N, int K) {
-  const int tiles = cdiv(M, BM) * cdiv(N, BN);
-  const int nk = cdiv(K, BKT);
-  int s = 1;
-  // aim for >= 2 waves of workgroups over 256 CUs (2 WGs/CU resident)
-  while (tiles * s < 512 && s * 2 <= 16 && nk / (s * 2) >= 4) s *= 2;
-  return s;
+// Tile configuration: the 256x128 / 3-stage ring when the grid fills the chip with one
+// WG per CU, else 128x128 / 2-stage (2 WGs per CU) for small decoder-side GEMMs.
+static int cfg_override() {
+  static int v = [] {
+    const char* s = getenv("CAPK_GEMM_CFG");
+    return s ? atoi(s) : 0;
+  }();
+  return v;
+}
+// Tile configurations (CAPK_GEMM_CFG overrides for A/B measurements):
+//   1: 128x128, BK 64, 2-deep ring (64 KiB, 2 WGs/CU)
+//   2: 256x128, BK 64, 3-deep ring (144 KiB, 1 WG/CU)
+//   3: 128x128, BK 32, 4-deep ring (64 KiB, 2 WGs/CU)
+//   4: 128x128, BK 32, 3-deep ring (48 KiB, 3 WGs/CU)
+static int slots_of(int cfg) { return cfg == 2 ? 256 : cfg == 4 ? 768 : 512; }  // resident WGs on 256 CUs
+static int tiles_of(int cfg, int M, int N) { return cdiv(M, cfg == 2 ? 256 : 128) * cdiv(N, BN); }
+// Measured per shape class (tools/gemm_bench.py, profiles/): the 3-WG/CU BK-32 ring wins when
+// the epilogue carries an activation (its stores overlap other WGs' main loops) and for the
+// split-K weight-gradient GEMMs whose grid fits one round; the 2-WG/CU BK-64 ring elsewhere.
+static int choose_cfg(int M, int N, int K, int a_kmajor, int b_kmajor, int act) {
+  int o = cfg_override();
+  if (o == 2 && M < 256) o = 1;
+  if ((o == 3 || o == 4) && (a_kmajor || b_kmajor) && K % 32) o = 1;
+  if (o >= 1 && o <= 4) return o;
+  if (act && (a_kmajor || b_kmajor) && K % 32 == 0) return 4;
+  if (!a_kmajor && !b_kmajor && tiles_of(4, M, N) < slots_of(4)) return 4;
+  return 1;
+}
+// Split-K factor: fill one round of resident workgroups when the tile grid alone cannot
+// (any integer factor; every split keeps >= 4 K-tiles).
+static int choose_splits(int cfg, int M, int N, int K) {
+  const int bk = (cfg == 3 || cfg == 4) ? 32 : 64;
+  const int tiles = tiles_of(cfg, M, N), slots = slots_of(cfg);
+  const int nk = cdiv(K, bk);
+  if (2 * tiles >= slots) return 1;
+  int s = std::min(16, slots / tiles);
+  s = std::min(s, std::max(1, nk / 4));
+  return std::max(1, s);
 }
 
 }  // namespace capk
@@ -336,7 +412,9 @@ using namespace capk;
 extern "C" size_t capk_gemm_workspace(int in_dtype, int out_dtype, int M, int N, int K) {
   (void)out_dtype;
   if (in_dtype != CAPK_BF16) return 0;
-  const int s = choose_splits(M, N, K);
+  // upper bound over the configurations (the launch picks one of them)
+  int s = 1;
+  for (int c = 1; c <= 4; ++c) s = std::max(s, choose_splits(c, M, N, K));
   return s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
 }
 
@@ -373,14 +451,24 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
   CAPK_CHECK_ARG(((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % 8 == 0 && ldb % 8 == 0,
                  "capk_gemm(bf16): A/B must be 16-B aligned with lda, ldb %% 8 == 0");
   CAPK_CHECK_ARG(((uintptr_t)C % 16 == 0) && (ldc * esz) % 16 == 0, "capk_gemm(bf16): C alignment");
-  int splits = choose_splits(M, N, K);
+  const int cfg = choose_cfg(M, N, K, a_kmajor, b_kmajor, act);
+  int splits = choose_splits(cfg, M, N, K);
   if (!ws || ws_bytes < (size_t)splits * M * N * sizeof(float)) splits = 1;
-  const int tiles = cdiv(M, BM) * cdiv(N, BN);
+  const int tiles = cdiv(M, cfg == 2 ? 256 : 128) * cdiv(N, BN);
   const int grid = tiles * splits;
   float* slab = splits > 1 ? (float*)ws : nullptr;
-#define LAUNCH(AK, BKM, OT)                                                                               \
-  hipLaunchKernelGGL((gemm_bf16_kernel<AK, BKM, OT>), dim3(grid), dim3(256), 0, st, (const bf16*)A, lda, \
-                     (const bf16*)B, ldb, M, N, K, splits, e, slab)
+#define LAUNCH1(BMX, BKX, NST, AK, BKM, OT)                                                                     \
+  hipLaunchKernelGGL((gemm_bf16_kernel<BMX, BKX, NST, AK, BKM, OT>), dim3(grid), dim3(BMX / 32 * 64), 0, st, \
+                     (const bf16*)A, lda, (const bf16*)B, ldb, M, N, K, splits, e, slab)
+#define LAUNCH(AK, BKM, OT)                                    \
+  do {                                                         \
+    switch (cfg) {                                             \
+      case 2: LAUNCH1(256, 64, 3, AK, BKM, OT); break;         \
+      case 3: LAUNCH1(128, 32, 4, AK, BKM, OT); break;         \
+      case 4: LAUNCH1(128, 32, 3, AK, BKM, OT); break;         \
+      default: LAUNCH1(128, 64, 2, AK, BKM, OT); break;        \
+    }                                                          \
+  } while (0)
 #define DISPATCH(OT)                          \
   if (a_kmajor && b_kmajor) LAUNCH(true, true, OT);     \
   else if (a_kmajor) LAUNCH(true, false, OT);           \
@@ -389,6 +477,7 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
   if (out_dtype == CAPK_BF16) { DISPATCH(bf16) } else { DISPATCH(float) }
 #undef DISPATCH
 #undef LAUNCH
+#undef LAUNCH1
   CAPK_LAUNCH_CHECK("gemm_bf16_kernel");
   if (splits > 1) {
     const int64_t n8 = (int64_t)M * N / 8;

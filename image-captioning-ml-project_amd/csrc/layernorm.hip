@@ -139,17 +139,26 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T
   }
 }
 
-__global__ void ln_bwd_finish_kernel(int nblocks, int cols, const float* __restrict__ part, float* __restrict__ dw,
-                                     float* __restrict__ db, int accumulate) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 2 * cols) return;
+// sum the per-block partials: 64 columns x 4 row-phases per 256-thread block, coalesced
+__global__ __launch_bounds__(256) void ln_bwd_finish_kernel(int nblocks, int cols, const float* __restrict__ part,
+                                                            float* __restrict__ dw, float* __restrict__ db,
+                                                            int accumulate) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;  // index into [2*cols]
   float s = 0.f;
-  for (int bidx = 0; bidx < nblocks; ++bidx) s += part[(int64_t)bidx * 2 * cols + i];
-  float* dst = i < cols ? dw + i : db + (i - cols);
-  *dst = accumulate ? *dst + s : s;
+  if (i < 2 * cols)
+    for (int bidx = ph; bidx < nblocks; bidx += 4) s += part[(int64_t)bidx * 2 * cols + i];
+  red[ph][lane] = s;
+  __syncthreads();
+  if (ph == 0 && i < 2 * cols) {
+    s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    float* dst = i < cols ? dw + i : db + (i - cols);
+    *dst = accumulate ? *dst + s : s;
+  }
 }
 
-static int ln_bwd_blocks(int rows) { return std::max(1, std::min(512, (rows + 3) / 4)); }
+static int ln_bwd_blocks(int rows) { return std::max(1, std::min(1024, (rows + 15) / 16)); }
 
 }  // namespace capk
 
@@ -192,7 +201,7 @@ extern "C" int capk_layernorm_bwd(int dtype, int rows, int cols, const void* dy,
   else { set_error("capk_layernorm_bwd: dtype"); return CAPK_EINVAL; }
 #undef L
   CAPK_LAUNCH_CHECK("ln_bwd_kernel");
-  hipLaunchKernelGGL(ln_bwd_finish_kernel, dim3(cdiv(2 * cols, 256)), dim3(256), 0, st, nb, cols, (const float*)ws, dw,
+  hipLaunchKernelGGL(ln_bwd_finish_kernel, dim3(cdiv(2 * cols, 64)), dim3(256), 0, st, nb, cols, (const float*)ws, dw,
                      db, accumulate);
   CAPK_LAUNCH_CHECK("ln_bwd_finish_kernel");
   return CAPK_OK;

@@ -206,7 +206,7 @@ __global__ void ce_finish_kernel(int rows, const float* __restrict__ row_loss, c
 }
 
 // ------------------------------------------------------------ colsum --------
-constexpr int CS_ROWS_PER_SPLIT = 512;
+constexpr int CS_ROWS_PER_SPLIT = 128;
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_kernel(int M, int N, const T* __restrict__ dy, int64_t ldy,
                                                      float* __restrict__ part) {
@@ -232,11 +232,18 @@ __global__ __launch_bounds__(256) void colsum_kernel(int M, int N, const T* __re
   }
 }
 
-__global__ void colsum_finish_kernel(int splits, int N, const float* __restrict__ part, float* __restrict__ out,
-                                     int accumulate) {
-  for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < N; n += gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += part[(int64_t)k * N + n];
+__global__ __launch_bounds__(256) void colsum_finish_kernel(int splits, int N, const float* __restrict__ part,
+                                                            float* __restrict__ out, int accumulate) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (n < N)
+    for (int k = ph; k < splits; k += 4) s += part[(int64_t)k * N + n];
+  red[ph][lane] = s;
+  __syncthreads();
+  if (ph == 0 && n < N) {
+    s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
     out[n] = accumulate ? out[n] + s : s;
   }
 }
@@ -363,7 +370,7 @@ extern "C" int capk_colsum(int dtype, int M, int N, const void* dy, int64_t ldy,
   DT_DISPATCH(dtype, L, 0)
 #undef L
   CAPK_LAUNCH_CHECK("colsum_kernel");
-  hipLaunchKernelGGL(colsum_finish_kernel, dim3(grid_for(N)), dim3(256), 0, S(stream), splits, N, (const float*)ws, db,
+  hipLaunchKernelGGL(colsum_finish_kernel, dim3(cdiv(N, 64)), dim3(256), 0, S(stream), splits, N, (const float*)ws, db,
                      accumulate);
   CAPK_LAUNCH_CHECK("colsum_finish_kernel");
   return CAPK_OK;

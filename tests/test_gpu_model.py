@@ -90,7 +90,10 @@ def test_golden_step_fp32(golden_dir):
                         p0 = z["p0/" + n]
                         assert np.all(np.abs(got[noise] - p0[noise]) <= lim + 1e-6), f"{tag}{n}"
                         got, want = got[~noise], want[~noise]
-                np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-6, err_msg=f"{tag}{n}")
+                # Adam divides by sqrt(v): the update of tiny-gradient elements magnifies fp32 summation-order
+                # differences, so parameters are compared to 0.1 % of the summed step sizes.
+                atol = 1e-3 * sum(float(x) for x in lrs[:step + 1])
+                np.testing.assert_allclose(got, want, rtol=1e-5, atol=atol, err_msg=f"{tag}{n}")
 
 
 @cuda
