@@ -8,8 +8,8 @@
 //       lane holds one query's scores (column = lane&15); row max / sum need
 //       only two xor-shuffles (16, 32).  P^T stays in registers and is the B
 //       operand of O^T = V^T P^T with the k (=key) order permuted to match the
-//       accumulator layout; V is staged transposed (Vt[d][key]) so the A operand
-//       is two ds_read_b64.  LSE is saved for backward.
+//       accumulator layout; V is staged row-major and its V^T fragments are read
+//       with ds_read_b64_tr_b16.  LSE is saved for backward.
 //  bwd: phase A (waves own 16-key blocks): S, dP, dS recomputed with the key on
 //       the lane; dV^T += dO^T P and dK^T += Q^T dS take dO^T / Q^T from the
 //       row-major LDS images via ds_read_b64_tr_b16.  Phase B (waves own 16-query
@@ -40,6 +40,12 @@ __device__ __forceinline__ bool key_ok(const AttnArgs& a, int b, int key, int q)
   if (a.key_pad && a.key_pad[(int64_t)b * a.Nk + key]) return false;
   return true;
 }
+
+// a 16-key block with no causal / padding / tail mask (wave-uniform test)
+__device__ __forceinline__ bool full_kb(const AttnArgs& a, int kb) {
+  return !a.causal && !a.key_pad && (kb + 1) * 16 <= a.Nk;
+}
+constexpr float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
 
 __device__ __forceinline__ bf16x8 ld8(const bf16* p) { return *(const bf16x8*)p; }
 __device__ __forceinline__ bf16x8 zero8() {
@@ -76,16 +82,46 @@ __device__ __forceinline__ bf16x8 tr_read8(const bf16* img, int st, int r0, int 
   return r;
 }
 
-// stage rows [0, NP) x [0, HDP) of one head into a row-major LDS image (stride st)
-template <int HDP>
-__device__ __forceinline__ void stage_rows(bf16* img, int st, const bf16* src, int64_t bs_off, int64_t rs, int n,
-                                           int NP, int hoff, int hd) {
+// Stage up to NIMG row-major [NP x HDP] head images into LDS (row stride HDP+8).
+// Every global load of every image is issued before the first LDS write, so a
+// workgroup pays one memory round trip for its whole staging, not one per chunk.
+struct StageSrc {
+  bf16* img;
+  const bf16* src;  // already offset to batch b and head column h*hd
+  int64_t rs;
+  int n, NP;
+};
+template <int HDP, int NIMG, int MINTHR>
+__device__ __forceinline__ void stage_images(const StageSrc (&S)[NIMG], int hd) {
   constexpr int NCH = HDP / 8;
-  for (int c = threadIdx.x; c < NP * NCH; c += blockDim.x) {
-    const int r = c / NCH, dc = c % NCH;
-    bf16x8 v = zero8();
-    if (r < n && dc * 8 < hd) v = ld8(src + bs_off + (int64_t)r * rs + hoff + dc * 8);
-    *(bf16x8*)(img + r * st + dc * 8) = v;
+  constexpr int ST = HDP + 8;
+  constexpr int MAXIT = (256 * NCH + MINTHR - 1) / MINTHR;  // NP <= 256
+  bf16x8 v[NIMG][MAXIT];
+#pragma unroll
+  for (int im = 0; im < NIMG; ++im)
+#pragma unroll
+    for (int it = 0; it < MAXIT; ++it) {
+      const int c = threadIdx.x + it * blockDim.x;
+      const int r = c / NCH, dc = c % NCH;
+      v[im][it] = (r < S[im].n && dc * 8 < hd) ? ld8(S[im].src + (int64_t)r * S[im].rs + dc * 8) : zero8();
+    }
+#pragma unroll
+  for (int im = 0; im < NIMG; ++im)
+#pragma unroll
+    for (int it = 0; it < MAXIT; ++it) {
+      const int c = threadIdx.x + it * blockDim.x;
+      const int r = c / NCH, dc = c % NCH;
+      if (r < S[im].NP) *(bf16x8*)(S[im].img + r * ST + dc * 8) = v[im][it];
+    }
+}
+
+template <int HDP>
+__device__ __forceinline__ void load_q_frags(const AttnArgs& a, const bf16* qsrc, int qt, int lane, bf16x8 (&qf)[HDP / 32]) {
+  const int qi = qt * 16 + (lane & 15);
+#pragma unroll
+  for (int s = 0; s < HDP / 32; ++s) {
+    const int d = s * 32 + 8 * (lane >> 4);
+    qf[s] = (qi < a.Nq && d < a.hd) ? ld8(qsrc + (int64_t)qi * a.q_rs + d) : zero8();
   }
 }
 
@@ -93,36 +129,28 @@ template <int HDP>
 __global__ __launch_bounds__(512) void attn_fwd_bf16(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
   const int NKP = (a.Nk + 31) & ~31;
-  const int KST = HDP + 8, VST = NKP + 8;
+  constexpr int ST = HDP + 8;
   bf16* Ks = (bf16*)smem;
-  bf16* Vt = Ks + NKP * KST;
+  bf16* Vs = Ks + NKP * ST;
   const int hoff = h * a.hd;
-  stage_rows<HDP>(Ks, KST, (const bf16*)a.k, (int64_t)b * a.k_bs, a.k_rs, a.Nk, NKP, hoff, a.hd);
+  const bf16* qsrc = (const bf16*)a.q + (int64_t)b * a.q_bs + hoff;
+  // issue this wave's first Q tile before the K/V staging so the latencies overlap
+  bf16x8 qf[HDP / 32];
+  load_q_frags<HDP>(a, qsrc, wave, lane, qf);
   {
-    constexpr int NCH = HDP / 8;
-    const bf16* vsrc = (const bf16*)a.v + (int64_t)b * a.v_bs + hoff;
-    for (int c = threadIdx.x; c < NKP * NCH; c += blockDim.x) {
-      const int r = c / NCH, dc = c % NCH;
-      bf16x8 v = zero8();
-      if (r < a.Nk && dc * 8 < a.hd) v = ld8(vsrc + (int64_t)r * a.v_rs + dc * 8);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) Vt[(dc * 8 + i) * VST + r] = v[i];
-    }
+    const StageSrc S[2] = {{Ks, (const bf16*)a.k + (int64_t)b * a.k_bs + hoff, a.k_rs, a.Nk, NKP},
+                           {Vs, (const bf16*)a.v + (int64_t)b * a.v_bs + hoff, a.v_rs, a.Nk, NKP}};
+    stage_images<HDP, 2, 512>(S, a.hd);
   }
   __syncthreads();
 
   const int NKB = NKP / 16;
-  const bf16* qsrc = (const bf16*)a.q + (int64_t)b * a.q_bs + hoff;
-  for (int qt = wave; qt * 16 < a.Nq; qt += (int)(blockDim.x >> 6)) {
+  const float sl2 = a.scale * kLog2e;  // scores kept in the log2 domain: exp2(s*scale*log2e - max)
+  for (int qt = wave; qt * 16 < a.Nq; qt += nwaves) {
+    if (qt != wave) load_q_frags<HDP>(a, qsrc, qt, lane, qf);
     const int qi = qt * 16 + (lane & 15);
-    bf16x8 qf[HDP / 32];
-#pragma unroll
-    for (int s = 0; s < HDP / 32; ++s) {
-      const int d = s * 32 + 8 * (lane >> 4);
-      qf[s] = (qi < a.Nq && d < a.hd) ? ld8(qsrc + (int64_t)qi * a.q_rs + d) : zero8();
-    }
     f32x4 sc[16];
     float mx = -INFINITY;
 #pragma unroll
@@ -131,13 +159,17 @@ __global__ __launch_bounds__(512) void attn_fwd_bf16(AttnArgs a) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < HDP / 32; ++s) {
-          bf16x8 kf = *(const bf16x8*)(Ks + (kb * 16 + (lane & 15)) * KST + s * 32 + 8 * (lane >> 4));
+          bf16x8 kf = *(const bf16x8*)(Ks + (kb * 16 + (lane & 15)) * ST + s * 32 + 8 * (lane >> 4));
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s], acc, 0, 0, 0);
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int key = kb * 16 + (lane >> 4) * 4 + r;
-          acc[r] = key_ok(a, b, key, qi) ? acc[r] * a.scale : -INFINITY;
+          if (full_kb(a, kb)) {
+            acc[r] *= sl2;
+          } else {
+            const int key = kb * 16 + (lane >> 4) * 4 + r;
+            acc[r] = key_ok(a, b, key, qi) ? acc[r] * sl2 : -INFINITY;
+          }
           mx = fmaxf(mx, acc[r]);
         }
         sc[kb] = acc;
@@ -151,7 +183,7 @@ __global__ __launch_bounds__(512) void attn_fwd_bf16(AttnArgs a) {
       if (kb < NKB) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = __expf(sc[kb][r] - mx);
+          const float p = exp2f(sc[kb][r] - mx);
           sc[kb][r] = p;
           l += p;
         }
@@ -167,14 +199,8 @@ __global__ __launch_bounds__(512) void attn_fwd_bf16(AttnArgs a) {
       if (2 * t < NKB) {
         const bf16x8 pb = pack8(sc[2 * t], sc[2 * t + 1]);
 #pragma unroll
-        for (int db = 0; db < HDP / 16; ++db) {
-          const bf16* vr = Vt + (db * 16 + (lane & 15)) * VST + 32 * t + 4 * (lane >> 4);
-          bf16x4 v0 = *(const bf16x4*)vr, v1 = *(const bf16x4*)(vr + 16);
-          bf16x8 va;
-          va[0] = v0[0]; va[1] = v0[1]; va[2] = v0[2]; va[3] = v0[3];
-          va[4] = v1[0]; va[5] = v1[1]; va[6] = v1[2]; va[7] = v1[3];
-          o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, o[db], 0, 0, 0);
-        }
+        for (int db = 0; db < HDP / 16; ++db)  // O^T += V^T P^T, V^T fragments by transposed LDS reads
+          o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_read8(Vs, ST, 32 * t, db * 16, lane), pb, o[db], 0, 0, 0);
       }
     }
     if (qi < a.Nq) {
@@ -185,7 +211,7 @@ __global__ __launch_bounds__(512) void attn_fwd_bf16(AttnArgs a) {
         const int d0 = db * 16 + (lane >> 4) * 4;
         if (d0 < a.hd) store4(orow + d0, o[db], inv);
       }
-      if ((lane >> 4) == 0) a.lse[((int64_t)b * a.H + h) * a.Nq + qi] = mx + __logf(l);
+      if ((lane >> 4) == 0) a.lse[((int64_t)b * a.H + h) * a.Nq + qi] = (mx + __log2f(l)) * kLn2;
     }
   }
 }
@@ -204,16 +230,20 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16(AttnArgs a) {
   float* lse_s = (float*)(Vs + NKP * ST);
   float* del_s = lse_s + NQP;
   const int hoff = h * a.hd;
-  stage_rows<HDP>(Qs, ST, (const bf16*)a.q, (int64_t)b * a.q_bs, a.q_rs, a.Nq, NQP, hoff, a.hd);
-  stage_rows<HDP>(dOs, ST, (const bf16*)a.dout, (int64_t)b * a.do_bs, a.do_rs, a.Nq, NQP, hoff, a.hd);
-  stage_rows<HDP>(Ks, ST, (const bf16*)a.k, (int64_t)b * a.k_bs, a.k_rs, a.Nk, NKP, hoff, a.hd);
-  stage_rows<HDP>(Vs, ST, (const bf16*)a.v, (int64_t)b * a.v_bs, a.v_rs, a.Nk, NKP, hoff, a.hd);
+  {
+    const StageSrc S[4] = {{Qs, (const bf16*)a.q + (int64_t)b * a.q_bs + hoff, a.q_rs, a.Nq, NQP},
+                           {dOs, (const bf16*)a.dout + (int64_t)b * a.do_bs + hoff, a.do_rs, a.Nq, NQP},
+                           {Ks, (const bf16*)a.k + (int64_t)b * a.k_bs + hoff, a.k_rs, a.Nk, NKP},
+                           {Vs, (const bf16*)a.v + (int64_t)b * a.v_bs + hoff, a.v_rs, a.Nk, NKP}};
+    stage_images<HDP, 4, 512>(S, a.hd);
+  }
   // lse and delta_q = sum_d dO*O (fp32): 16-B vector loads of O, dO from LDS,
   // per-chunk partial dots -> LDS -> one thread per query sums them.
   constexpr int NCH = HDP / 8;
   float* part = del_s + NQP;  // [NQP][NCH]
   for (int q = threadIdx.x; q < NQP; q += blockDim.x)
-    lse_s[q] = q < a.Nq ? a.lse_in[((int64_t)b * a.H + h) * a.Nq + q] : 0.f;
+    lse_s[q] = q < a.Nq ? a.lse_in[((int64_t)b * a.H + h) * a.Nq + q] * kLog2e : 0.f;  // log2 domain
+  const float sl2 = a.scale * kLog2e;
   for (int idx = threadIdx.x; idx < NQP * NCH; idx += blockDim.x) {
     const int q = idx / NCH, c = idx % NCH;
     float s = 0.f;
@@ -258,8 +288,8 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16(AttnArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int q = t * 32 + c * 16 + (lane >> 4) * 4 + r;
-          const bool ok = q < a.Nq && key_ok(a, b, keyl, q);
-          const float pv = ok ? __expf(s_acc[r] * a.scale - lse_s[q]) : 0.f;
+          const bool ok = q < a.Nq && (full_kb(a, kb) || key_ok(a, b, keyl, q));
+          const float pv = ok ? exp2f(s_acc[r] * sl2 - lse_s[q]) : 0.f;
           p[c][r] = pv;
           ds[c][r] = pv * (dp_acc[r] - del_s[q]);
         }
@@ -309,8 +339,8 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16(AttnArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = t * 32 + c * 16 + (lane >> 4) * 4 + r;
-          const bool ok = ql < a.Nq && key_ok(a, b, key, ql);
-          const float pv = ok ? __expf(s_acc[r] * a.scale - lq) : 0.f;
+          const bool ok = ql < a.Nq && (full_kb(a, 2 * t + c) || key_ok(a, b, key, ql));
+          const float pv = ok ? exp2f(s_acc[r] * sl2 - lq) : 0.f;
           ds[c][r] = pv * (dp_acc[r] - dq_del);
         }
       }
@@ -441,7 +471,7 @@ __global__ __launch_bounds__(64) void attn_bwd_dkv_f32(AttnArgs a) {
 
 static size_t fwd_smem(int Nk, int hdp) {
   const int NKP = (Nk + 31) & ~31;
-  return (size_t)NKP * (hdp + 8) * 2 + (size_t)hdp * (NKP + 8) * 2;
+  return (size_t)2 * NKP * (hdp + 8) * 2;
 }
 static size_t bwd_smem(int Nq, int Nk, int hdp) {
   const int NQP = (Nq + 31) & ~31, NKP = (Nk + 31) & ~31;
@@ -507,7 +537,7 @@ extern "C" int capk_attention_fwd(int dtype, int B, int H, int Nq, int Nk, int h
                  "capk_attention_fwd(bf16): strides must allow 16-B vector access");
   const int hdp = hdp_of(hd);
   const size_t shm = fwd_smem(Nk, hdp);
-  const dim3 grid(B * H), block(Nq > 64 ? 512 : 256);
+  const dim3 grid(B * H), block(512);
   switch (hdp) {
     case 32: return launch_dyn(attn_fwd_bf16<32>, grid, block, shm, st, a, "attn_fwd_bf16");
     case 64: return launch_dyn(attn_fwd_bf16<64>, grid, block, shm, st, a, "attn_fwd_bf16");
@@ -551,7 +581,7 @@ extern "C" int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int h
   const int hdp = hdp_of(hd);
   const size_t shm = bwd_smem(Nq, Nk, hdp);
   CAPK_CHECK_ARG(shm <= 160 * 1024, "capk_attention_bwd: LDS %zu > 160 KiB", shm);
-  const dim3 grid(B * H), block((Nq > 64 || Nk > 64) ? 512 : 256);
+  const dim3 grid(B * H), block(512);
   switch (hdp) {
     case 32: return launch_dyn(attn_bwd_bf16<32>, grid, block, shm, st, a, "attn_bwd_bf16");
     case 64: return launch_dyn(attn_bwd_bf16<64>, grid, block, shm, st, a, "attn_bwd_bf16");
