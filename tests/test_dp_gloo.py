@@ -1,0 +1,99 @@
+"""Data-parallel semantics on CPU (gloo, world_size 2): the flat-gradient all-reduce
+of capk.train.dp makes a DP step equal to a single-process step on the
+concatenated batch.  Gradients are produced by the CPU oracle on
+each rank's shard and written into the ParamStore's flat buffers, then averaged
+with the same bucketed all_reduce bench.py uses (RCCL on the GPU node)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _tiny(golden):
+    import sys
+    for p in (ROOT, os.path.join(ROOT, "image-captioning-ml-project_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    z = np.load(golden, allow_pickle=False)
+    from capk import config as C
+    from capk.models import captioning_model as cm
+    from capk.models import encoders as E
+    D, Le, He, Ld, Hd, V, pad, patch, img = [int(x) for x in z["meta/dims"]]
+    cfg = C.Config()
+    cfg.model.encoder = C.EncoderConfig(encoder_type="vit", feature_dim=D)
+    cfg.model.decoder = C.DecoderConfig(decoder_type="transformer", hidden_dim=D, num_layers=Ld, num_heads=Hd)
+    cfg.model.vocab_size, cfg.model.pad_token_id = V, pad
+    arch = dict(hidden_size=D, num_hidden_layers=Le, num_attention_heads=He, intermediate_size=2 * D,
+                image_size=img, patch_size=patch, num_channels=3, layer_norm_eps=1e-12)
+    orig = E.VIT_ARCHS["google/vit-base-patch16-224"]
+    E.VIT_ARCHS["google/vit-base-patch16-224"] = arch
+    try:
+        m = cm.ImageCaptioningModel(cfg)
+    finally:
+        E.VIT_ARCHS["google/vit-base-patch16-224"] = orig
+    sd = {k[3:]: torch.from_numpy(z[k].copy()) for k in z.files if k.startswith("p0/")}
+    m.load_state_dict(sd)
+    return m, sd, (D, Le, He, Ld, Hd, V, pad, patch, img)
+
+
+def _oracle_grads(sd, dims, images, caps):
+    from oracle import decoders as odec
+    from oracle import encoders as oenc
+    from oracle import train as otrain
+    D, Le, He, Ld, Hd, V, pad, patch, img = dims
+    p = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    sub = lambda pre: {k[len(pre):]: v for k, v in p.items() if k.startswith(pre)}
+    enc = oenc.vit_encoder(sub("encoder.model."), images, Le, He, patch)
+    logits = odec.transformer_decoder(sub("decoder."), enc["features"], caps, Ld, Hd, pad)
+    otrain.shifted_ce(logits, caps, pad).backward()
+    return {k: (v.grad if v.grad is not None else torch.zeros_like(v)) for k, v in p.items()}
+
+
+def _worker(rank, world, port, golden, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    m, sd, dims = _tiny(golden)
+    from capk.params import attach
+    from capk.train.dp import allreduce_grads
+    store = attach(m, "cpu")
+    D, Le, He, Ld, Hd, V, pad, patch, img = dims
+    g = torch.Generator().manual_seed(123)
+    images = torch.randn(4, 3, img, img, generator=g)
+    caps = torch.randint(0, V - 1, (4, 7), generator=g)  # no pad: equal token counts per shard
+    shard = slice(rank * 2, rank * 2 + 2)
+    grads = _oracle_grads(sd, dims, images[shard], caps[shard])
+    named = dict(m.named_parameters())
+    with torch.no_grad():
+        for n, t in grads.items():
+            named[n]._capk_grad.copy_(t)
+    allreduce_grads(store, bucket_elems=1000)  # small buckets: exercise the chunking
+    if rank == 0:
+        full = _oracle_grads(sd, dims, images, caps)
+        err = max(float((named[n]._capk_grad - full[n]).abs().max()) for n in full)
+        torch.save({"err": err}, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_allreduce_equals_full_batch(tmp_path, golden_dir):
+    out = str(tmp_path / "dp.pt")
+    golden = os.path.join(golden_dir, "vit_transformer_step.npz")
+    mp.spawn(_worker, args=(2, _free_port(), golden, out), nprocs=2, join=True)
+    res = torch.load(out, weights_only=True)
+    assert res["err"] < 1e-5, res
