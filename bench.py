@@ -80,6 +80,7 @@ def main():
     captions = torch.randint(0, 50256, (B, 20), device=device, generator=g1)
     total_steps = 10_000
     step_no = [0]
+    model.train()  # trainer.py:210: decoder dropout (p=0.1) active in the timed step
 
     def step():
         out = model(images=images, captions=captions, caption_lengths=None)

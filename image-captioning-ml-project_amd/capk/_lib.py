@@ -22,6 +22,8 @@ _i = ctypes.c_int
 _i64 = ctypes.c_int64
 _f = ctypes.c_float
 _sz = ctypes.c_size_t
+_u32 = ctypes.c_uint32
+_u64 = ctypes.c_uint64
 
 # name -> (restype, [argtypes])  — must mirror include/capk.h exactly
 SIGNATURES = {
@@ -30,22 +32,26 @@ SIGNATURES = {
     "capk_device_arch": (_i, [ctypes.c_char_p, _i]),
     "capk_gemm_workspace": (_sz, [_i, _i, _i, _i, _i]),
     "capk_gemm": (_i, [_i, _i, _i, _i, _i, _c_p, _i64, _i, _c_p, _i64, _i, _c_p, _i64, _f, _f,
-                       _c_p, _c_p, _i64, _i, _c_p, _c_p, _i64, _c_p, _sz, _c_p]),
+                       _c_p, _c_p, _i64, _i, _c_p, _c_p, _i64, _f, _u32, _c_p, _sz, _c_p]),
+    "capk_dropout_mask": (_i, [_i64, _u64, _f, _u32, _c_p, _c_p]),
     "capk_layernorm_fwd": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _c_p, _f, _c_p, _i64, _c_p, _c_p, _c_p]),
     "capk_layernorm_bwd_workspace": (_sz, [_i, _i]),
     "capk_layernorm_bwd": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p, _c_p, _c_p, _c_p, _i64, _c_p, _i64,
-                                _c_p, _c_p, _i, _c_p, _sz, _c_p]),
+                                _c_p, _c_p, _i, _f, _u32, _c_p, _i64, _c_p, _sz, _c_p]),
     "capk_attention_fwd": (_i, [_i, _i, _i, _i, _i, _i, _f, _i, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _i64,
-                                _i64, _c_p, _c_p, _i64, _i64, _c_p, _c_p]),
-    "capk_attention_bwd": (_i, [_i, _i, _i, _i, _i, _i, _f, _i, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _i64,
-                                _i64, _c_p, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _c_p, _i64, _i64, _c_p,
-                                _i64, _i64, _c_p, _i64, _i64, _c_p]),
+                                _i64, _c_p, _c_p, _i64, _i64, _c_p, _f, _u32, _c_p]),
+    "capk_attention_bwd": (_i, [_i, _i, _i, _i, _i, _i, _f, _i,            # dtype B H Nq Nk hd scale causal
+                                _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _i64, _i64,  # q k v
+                                _c_p,                                          # key_pad
+                                _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p,      # o, dout, lse
+                                _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _i64, _i64,  # dq dk dv
+                                _f, _u32, _c_p]),
     "capk_patchify": (_i, [_i, _i, _i, _i, _i, _i, _c_p, _c_p, _c_p]),
     "capk_vit_assemble": (_i, [_i, _i, _i, _i, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "capk_vit_assemble_bwd_workspace": (_sz, [_i, _i, _i]),
     "capk_vit_assemble_bwd": (_i, [_i, _i, _i, _i, _c_p, _c_p, _c_p, _c_p, _c_p, _sz, _c_p]),
-    "capk_embedding_fwd": (_i, [_i, _i, _i, _i, _c_p, _c_p, _c_p, _i, _c_p, _c_p]),
-    "capk_embedding_bwd": (_i, [_i, _i, _i, _i, _c_p, _c_p, _i, _c_p, _c_p, _i, _c_p]),
+    "capk_embedding_fwd": (_i, [_i, _i, _i, _i, _c_p, _c_p, _c_p, _i, _f, _u32, _c_p, _c_p]),
+    "capk_embedding_bwd": (_i, [_i, _i, _i, _i, _c_p, _c_p, _i, _c_p, _c_p, _i, _f, _u32, _c_p]),
     "capk_shifted_ce_workspace": (_sz, [_i, _i]),
     "capk_shifted_ce": (_i, [_i, _i, _i, _i, _i64, _c_p, _c_p, _i, _c_p, _c_p, _c_p, _c_p, _sz, _c_p]),
     "capk_zero": (_i, [_c_p, _sz, _c_p]),

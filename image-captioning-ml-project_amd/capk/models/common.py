@@ -14,6 +14,18 @@ from .. import ops
 from ..ops import HeadView
 
 
+_SEED = [None]
+
+
+def next_seed():
+    """Fresh 32-bit dropout seed (host counter; no device sync).  Seeded from torch's
+    initial seed so runs are reproducible under torch.manual_seed."""
+    if _SEED[0] is None:
+        _SEED[0] = (torch.initial_seed() * 0x9E3779B1) & 0xFFFFFFFF
+    _SEED[0] = (_SEED[0] * 1664525 + 1013904223) & 0xFFFFFFFF
+    return _SEED[0]
+
+
 def compute_dtype(m):
     return getattr(m, "_capk_dtype", torch.bfloat16)
 
@@ -59,7 +71,7 @@ class CapkModule(nn.Module):
 
 
 def linear_bwd(dy, x, w_param, b_param, dtype, *, fused=None, need_dx=True, act_bwd=0, aux=None,
-               dw_accumulate=False):
+               dw_accumulate=False, drop=(0.0, 0)):
     """Backward of y = x W^T + b: dW, db into the grad buffer; returns dX (or None)."""
     if fused is not None:
         wmat, gw = fused[0].w(dtype), fused[0].grad
@@ -72,7 +84,7 @@ def linear_bwd(dy, x, w_param, b_param, dtype, *, fused=None, need_dx=True, act_
         ops.colsum(dy, gb, accumulate=dw_accumulate)
     if not need_dx:
         return None
-    return ops.linear_dx(dy, wmat, act_bwd=act_bwd, aux=aux)
+    return ops.linear_dx(dy, wmat, act_bwd=act_bwd, aux=aux, drop=drop)
 
 
 def heads(buf, col_off, B, N, row_stride_rows=None):

@@ -34,7 +34,6 @@ class TransformerDecoder(TransformerDecoderCore, CaptionDecoder):
         TransformerDecoderCore.__init__(self, config.hidden_dim, config.num_layers, config.num_heads,
                                         config.dropout, config.max_length, vocab_size, pad_token_id)
         self.num_layers = config.num_layers
-        self.dropout_p = config.dropout
         self.bos_token_id = bos_token_id
         self.eos_token_id = eos_token_id
 

@@ -27,7 +27,7 @@ import torch.nn as nn
 
 from .. import ops
 from .._lib import ACT_GELU_ERF
-from .common import G, CapkModule, W, heads, linear_bwd
+from .common import G, CapkModule, W, heads, linear_bwd, next_seed
 from ..ops import HeadView
 
 
@@ -70,6 +70,7 @@ class TransformerDecoderCore(CapkModule):
         self.vocab_size = vocab_size
         self.vocab_pad = _pad64(vocab_size)
         self.pad_token_id = pad_token_id
+        self.dropout_p = dropout
         self.embedding = nn.Embedding(vocab_size, hidden_dim, padding_idx=pad_token_id)
         self.position_encoding = nn.Embedding(max_length, hidden_dim)
         layer = _DecoderLayerParams(hidden_dim, num_heads, hidden_dim * 4, dropout)
@@ -116,17 +117,26 @@ class _DecoderFn(torch.autograd.Function):
         vp = m.visual_projection
         mem = ops.linear(feat_mem, W(vp.weight, dt), vp.bias.detach())  # [M_ext, D]
         tgt_pad = (captions == m.pad_token_id) if use_pad_mask else None  # bool [B,T] mask bookkeeping
-        x = ops.embedding_fwd(captions, m.embedding.weight.detach(), m.position_encoding.weight.detach(), 0, dt)
+        # dropout (train mode, p = DecoderConfig.dropout): decoders.py:417 on the embeddings and,
+        # per nn.TransformerDecoderLayer, MHA probabilities (self, cross), dropout1/2/3 on the
+        # residual branches and the FFN inner dropout.  Masks are hashes of a per-site seed.
+        p = m.dropout_p if m.training else 0.0
+        seed = (lambda: (p, next_seed())) if p > 0 else (lambda: ops.NO_DROP)
+        d_emb = seed()
+        x = ops.embedding_fwd(captions, m.embedding.weight.detach(), m.position_encoding.weight.detach(), 0, dt,
+                              drop=d_emb)
         BT = B * T
         saved_layers = []
         for L in m.transformer_decoder.layers:
             sa, ca = L.self_attn, L.multihead_attn
+            drops = tuple(seed() for _ in range(6))  # sa-prob, dropout1, ca-prob, dropout2, ffn, dropout3
             x_in = x
             qkv = ops.linear(x, W(sa.in_proj_weight, dt), sa.in_proj_bias.detach())
             a = torch.empty(BT, D, dtype=dt, device=x.device)
             lse1, kp = ops.attention_fwd(heads(qkv, 0, B, T), heads(qkv, D, B, T), heads(qkv, 2 * D, B, T),
-                                         heads(a, 0, B, T), B, H, T, T, hd, scale, causal=True, key_pad=tgt_pad)
-            s1 = ops.linear(a, W(sa.out_proj.weight, dt), sa.out_proj.bias.detach(), residual=x)
+                                         heads(a, 0, B, T), B, H, T, T, hd, scale, causal=True, key_pad=tgt_pad,
+                                         drop=drops[0])
+            s1 = ops.linear(a, W(sa.out_proj.weight, dt), sa.out_proj.bias.detach(), residual=x, drop=drops[1])
             x1, mu1, rs1 = ops.layernorm_fwd(s1, L.norm1.weight.detach(), L.norm1.bias.detach(), L.norm1.eps)
             wca = W(ca.in_proj_weight, dt)
             bca = ca.in_proj_bias.detach()
@@ -135,20 +145,23 @@ class _DecoderFn(torch.autograd.Function):
             c = torch.empty(BT, D, dtype=dt, device=x.device)
             kvh_k = HeadView(kv, 0, rpb * 2 * D, 2 * D)
             kvh_v = HeadView(kv, D, rpb * 2 * D, 2 * D)
-            lse2, _ = ops.attention_fwd(heads(qc, 0, B, T), kvh_k, kvh_v, heads(c, 0, B, T), B, H, T, S, hd, scale)
-            s2 = ops.linear(c, W(ca.out_proj.weight, dt), ca.out_proj.bias.detach(), residual=x1)
+            lse2, _ = ops.attention_fwd(heads(qc, 0, B, T), kvh_k, kvh_v, heads(c, 0, B, T), B, H, T, S, hd, scale,
+                                        drop=drops[2])
+            s2 = ops.linear(c, W(ca.out_proj.weight, dt), ca.out_proj.bias.detach(), residual=x1, drop=drops[3])
             x2, mu2, rs2 = ops.layernorm_fwd(s2, L.norm2.weight.detach(), L.norm2.bias.detach(), L.norm2.eps)
             I = L.linear1.weight.shape[0]
             f_pre = torch.empty(BT, I, dtype=dt, device=x.device)
-            f = ops.linear(x2, W(L.linear1.weight, dt), L.linear1.bias.detach(), act=ACT_GELU_ERF, preact=f_pre)
-            s3 = ops.linear(f, W(L.linear2.weight, dt), L.linear2.bias.detach(), residual=x2)
+            f = ops.linear(x2, W(L.linear1.weight, dt), L.linear1.bias.detach(), act=ACT_GELU_ERF, preact=f_pre,
+                           drop=drops[4])
+            s3 = ops.linear(f, W(L.linear2.weight, dt), L.linear2.bias.detach(), residual=x2, drop=drops[5])
             x, mu3, rs3 = ops.layernorm_fwd(s3, L.norm3.weight.detach(), L.norm3.bias.detach(), L.norm3.eps)
             saved_layers.append((x_in, qkv, a, lse1, kp, s1, mu1, rs1, x1, qc, kv, c, lse2, s2, mu2, rs2, x2, f_pre,
-                                 f, s3, mu3, rs3))
+                                 f, s3, mu3, rs3, drops))
         ol = m.output_layer
         wout = ol.weight._capk_pad_bf16 if dt == torch.bfloat16 else ol.weight._capk_pad_master
         logits_pad = ops.linear(x, wout, _pad_bias(ol))
         ctx.m = m
+        ctx.d_emb = d_emb
         ctx.dims = (B, S, T, D, H, hd, scale, V, Vp, rpb, M_ext)
         ctx.saved = (feat_mem, mem, captions, saved_layers, x)
         ctx.features_meta = (features.shape, features.stride())
@@ -187,17 +200,30 @@ class _DecoderFn(torch.autograd.Function):
             L = m.transformer_decoder.layers[li]
             sa, ca = L.self_attn, L.multihead_attn
             (x_in, qkv, a, lse1, kp, s1, mu1, rs1, x1, qc, kv, c, lse2, s2, mu2, rs2, x2, f_pre, f, s3, mu3,
-             rs3) = saved_layers[li]
+             rs3, drops) = saved_layers[li]
             saved_layers[li] = None
-            # norm3(x2 + FFN(x2))
-            ds3 = ops.layernorm_bwd(dx, s3, L.norm3.weight.detach(), mu3, rs3, G(L.norm3.weight), G(L.norm3.bias))
-            dfp = linear_bwd(ds3, f, L.linear2.weight, L.linear2.bias, dt, act_bwd=ACT_GELU_ERF, aux=f_pre)
+            on = drops[1][0] > 0
+
+            def ln_bwd(dy, s, norm, mu, rs, drop):
+                """grad of s = x + dropout(branch) through norm: (ds, ds * mask)."""
+                if not on:
+                    g = ops.layernorm_bwd(dy, s, norm.weight.detach(), mu, rs, G(norm.weight), G(norm.bias))
+                    return g, g
+                gm = torch.empty_like(s)
+                g = ops.layernorm_bwd(dy, s, norm.weight.detach(), mu, rs, G(norm.weight), G(norm.bias), drop=drop,
+                                      out_drop=gm)
+                return g, gm
+
+            # norm3(x2 + dropout3(linear2(dropout(gelu(linear1(x2))))))
+            ds3, ds3m = ln_bwd(dx, s3, L.norm3, mu3, rs3, drops[5])
+            dfp = linear_bwd(ds3m, f, L.linear2.weight, L.linear2.bias, dt, act_bwd=ACT_GELU_ERF, aux=f_pre,
+                             drop=drops[4])
             ops.linear_dw(dfp, x2, G(L.linear1.weight))
             ops.colsum(dfp, G(L.linear1.bias))
             ops.linear_dx(dfp, W(L.linear1.weight, dt), out=ds3, beta=1.0)  # dx2 = ds3 + dfp W1
-            # norm2(x1 + MHA(x1, mem))
-            ds2 = ops.layernorm_bwd(ds3, s2, L.norm2.weight.detach(), mu2, rs2, G(L.norm2.weight), G(L.norm2.bias))
-            dc = linear_bwd(ds2, c, ca.out_proj.weight, ca.out_proj.bias, dt)
+            # norm2(x1 + dropout2(MHA(x1, mem)))
+            ds2, ds2m = ln_bwd(ds3, s2, L.norm2, mu2, rs2, drops[3])
+            dc = linear_bwd(ds2m, c, ca.out_proj.weight, ca.out_proj.bias, dt)
             dqc = torch.empty(BT, D, dtype=dt, device=dev)
             dkv = torch.empty(M_ext, 2 * D, dtype=dt, device=dev)
             if rpb != S:
@@ -205,7 +231,7 @@ class _DecoderFn(torch.autograd.Function):
             ops.attention_bwd(heads(qc, 0, B, T), HeadView(kv, 0, rpb * 2 * D, 2 * D),
                               HeadView(kv, D, rpb * 2 * D, 2 * D), heads(c, 0, B, T), heads(dc, 0, B, T), lse2,
                               heads(dqc, 0, B, T), HeadView(dkv, 0, rpb * 2 * D, 2 * D),
-                              HeadView(dkv, D, rpb * 2 * D, 2 * D), B, H, T, S, hd, scale)
+                              HeadView(dkv, D, rpb * 2 * D, 2 * D), B, H, T, S, hd, scale, drop=drops[2])
             gW, gB = G(ca.in_proj_weight), G(ca.in_proj_bias)
             wca = W(ca.in_proj_weight, dt)
             ops.linear_dw(dkv, mem, gW[D:])
@@ -215,13 +241,14 @@ class _DecoderFn(torch.autograd.Function):
             ops.linear_dw(dqc, x1, gW[:D])
             ops.colsum(dqc, gB[:D])
             ops.linear_dx(dqc, wca[:D], out=ds2, beta=1.0)  # dx1 = ds2 + dqc Wq
-            # norm1(x + SA(x))
-            ds1 = ops.layernorm_bwd(ds2, s1, L.norm1.weight.detach(), mu1, rs1, G(L.norm1.weight), G(L.norm1.bias))
-            da = linear_bwd(ds1, a, sa.out_proj.weight, sa.out_proj.bias, dt)
+            # norm1(x + dropout1(SA(x)))
+            ds1, ds1m = ln_bwd(ds2, s1, L.norm1, mu1, rs1, drops[1])
+            da = linear_bwd(ds1m, a, sa.out_proj.weight, sa.out_proj.bias, dt)
             dqkv = torch.empty_like(qkv)
             ops.attention_bwd(heads(qkv, 0, B, T), heads(qkv, D, B, T), heads(qkv, 2 * D, B, T), heads(a, 0, B, T),
                               heads(da, 0, B, T), lse1, heads(dqkv, 0, B, T), heads(dqkv, D, B, T),
-                              heads(dqkv, 2 * D, B, T), B, H, T, T, hd, scale, causal=True, key_pad_u8=kp)
+                              heads(dqkv, 2 * D, B, T), B, H, T, T, hd, scale, causal=True, key_pad_u8=kp,
+                              drop=drops[0])
             ops.linear_dw(dqkv, x_in, G(sa.in_proj_weight))
             ops.colsum(dqkv, G(sa.in_proj_bias))
             ops.linear_dx(dqkv, W(sa.in_proj_weight, dt), out=ds1, beta=1.0)  # dx = ds1 + dqkv Win
@@ -229,7 +256,8 @@ class _DecoderFn(torch.autograd.Function):
         # embeddings (scatter-add into zeroed grads; padding_idx rows skipped)
         ops.zero_(G(m.embedding.weight))
         ops.zero_(G(m.position_encoding.weight))
-        ops.embedding_bwd(captions, dx, m.pad_token_id, G(m.embedding.weight), G(m.position_encoding.weight), 0)
+        ops.embedding_bwd(captions, dx, m.pad_token_id, G(m.embedding.weight), G(m.position_encoding.weight), 0,
+                          drop=ctx.d_emb)
         # visual projection
         vp = m.visual_projection
         # gap rows of dmem are exactly zero: every dkv gap row is zero (see above)

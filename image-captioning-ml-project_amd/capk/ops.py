@@ -74,8 +74,11 @@ class KernelTimer:
 GEMM_TIMER = KernelTimer()
 
 
+NO_DROP = (0.0, 0)
+
+
 def gemm(A, a_kmajor, B, b_kmajor, M, N, K, C, *, lda, ldb, ldc, alpha=1.0, beta=0.0, bias=None,
-         residual=None, ldr=0, act=0, preact=None, aux=None, ldx=0):
+         residual=None, ldr=0, act=0, preact=None, aux=None, ldx=0, drop=NO_DROP):
     """C[m,n] = alpha*sum_k A(m,k)B(n,k) + beta*C + bias + residual -> act (see capk.h)."""
     _need_gpu(A, B, C)
     L = lib()
@@ -89,7 +92,7 @@ def gemm(A, a_kmajor, B, b_kmajor, M, N, K, C, *, lda, ldb, ldc, alpha=1.0, beta
         ev0.record()
     rc = L.capk_gemm(it, ot, M, N, K, _p(A), lda, int(a_kmajor), _p(B), ldb, int(b_kmajor), _p(C), ldc,
                      float(alpha), float(beta), _p(bias), _p(residual), ldr, int(act), _p(preact), _p(aux), ldx,
-                     _p(ws), wsb if ws is not None else 0, _stream())
+                     float(drop[0]), int(drop[1]) & 0xFFFFFFFF, _p(ws), wsb if ws is not None else 0, _stream())
     check(rc, "capk_gemm")
     if timed:
         ev1.record()
@@ -97,26 +100,27 @@ def gemm(A, a_kmajor, B, b_kmajor, M, N, K, C, *, lda, ldb, ldc, alpha=1.0, beta
     return C
 
 
-def linear(x, w, b=None, *, out=None, residual=None, act=0, preact=None, out_dtype=None):
-    """y = x @ w^T + b (+ residual) (act); x [M,K] (row stride may exceed K), w [N,K] contiguous."""
+def linear(x, w, b=None, *, out=None, residual=None, act=0, preact=None, out_dtype=None, drop=NO_DROP):
+    """y = dropout(act(x @ w^T + b)) + residual; x [M,K] (row stride may exceed K), w [N,K] contiguous."""
     M, K = x.shape
     N = w.shape[0]
     if out is None:
         out = torch.empty(M, N, dtype=out_dtype or x.dtype, device=x.device)
     gemm(x, True, w, True, M, N, K, out, lda=x.stride(0), ldb=w.stride(0), ldc=out.stride(0), bias=b,
          residual=residual, ldr=residual.stride(0) if residual is not None else 0, act=act, preact=preact,
-         ldx=preact.stride(0) if preact is not None else 0)
+         ldx=preact.stride(0) if preact is not None else 0, drop=drop)
     return out
 
 
-def linear_dx(dy, w, *, out=None, act_bwd=0, aux=None, beta=0.0):
-    """dX[M,K] = dY[M,N] @ W[N,K]  (optionally * act'(aux) for a fused activation backward)."""
+def linear_dx(dy, w, *, out=None, act_bwd=0, aux=None, beta=0.0, drop=NO_DROP):
+    """dX[M,K] = dY[M,N] @ W[N,K]  (optionally * act'(aux) * dropout-mask: fused activation backward)."""
     M, N = dy.shape
     K = w.shape[1]
     if out is None:
         out = torch.empty(M, K, dtype=dy.dtype, device=dy.device)
     gemm(dy, True, w, False, M, K, N, out, lda=dy.stride(0), ldb=w.stride(0), ldc=out.stride(0), beta=beta,
-         act=(ACT_BWD | act_bwd) if act_bwd else 0, aux=aux, ldx=aux.stride(0) if aux is not None else 0)
+         act=(ACT_BWD | act_bwd) if act_bwd else 0, aux=aux, ldx=aux.stride(0) if aux is not None else 0,
+         drop=drop)
     return out
 
 
@@ -154,7 +158,9 @@ def layernorm_fwd(x, w, b, eps, out=None):
     return out, mean, rstd
 
 
-def layernorm_bwd(dy, x, w, mean, rstd, dw, db, *, dres=None, out=None, accumulate=False):
+def layernorm_bwd(dy, x, w, mean, rstd, dw, db, *, dres=None, out=None, accumulate=False, drop=NO_DROP,
+                  out_drop=None):
+    """dx = LN'(dy) (+ dres); with drop != off also fills out_drop = LN'(dy) * mask."""
     L = lib()
     rows, cols = x.shape
     if out is None:
@@ -164,7 +170,9 @@ def layernorm_bwd(dy, x, w, mean, rstd, dw, db, *, dres=None, out=None, accumula
     check(L.capk_layernorm_bwd(dtype_code(x), rows, cols, _p(dy), dy.stride(0), _p(x), x.stride(0), _p(w),
                                _p(mean), _p(rstd), _p(out), out.stride(0), _p(dres),
                                dres.stride(0) if dres is not None else 0, _p(dw), _p(db), int(accumulate),
-                               _p(ws), wsb, _stream()), "capk_layernorm_bwd")
+                               float(drop[0]), int(drop[1]) & 0xFFFFFFFF, _p(out_drop),
+                               out_drop.stride(0) if out_drop is not None else 0, _p(ws), wsb, _stream()),
+          "capk_layernorm_bwd")
     return out
 
 
@@ -181,22 +189,24 @@ class HeadView:
         return self.t.data_ptr() + self.off * self.t.element_size()
 
 
-def attention_fwd(q, k, v, o, B, H, Nq, Nk, hd, scale, causal=False, key_pad=None):
+def attention_fwd(q, k, v, o, B, H, Nq, Nk, hd, scale, causal=False, key_pad=None, drop=NO_DROP):
     """q/k/v/o: HeadView.  Returns lse [B,H,Nq] fp32."""
     lse = torch.empty(B, H, Nq, dtype=torch.float32, device=q.t.device)
     kp = None if key_pad is None else key_pad.to(torch.uint8).contiguous()
     check(lib().capk_attention_fwd(dtype_code(q.t), B, H, Nq, Nk, hd, float(scale), int(causal),
                                    q.ptr(), q.bs, q.rs, k.ptr(), k.bs, k.rs, v.ptr(), v.bs, v.rs, _p(kp),
-                                   o.ptr(), o.bs, o.rs, _p(lse), _stream()), "capk_attention_fwd")
+                                   o.ptr(), o.bs, o.rs, _p(lse), float(drop[0]), int(drop[1]) & 0xFFFFFFFF,
+                                   _stream()), "capk_attention_fwd")
     return lse, kp
 
 
-def attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Nq, Nk, hd, scale, causal=False, key_pad_u8=None):
+def attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Nq, Nk, hd, scale, causal=False, key_pad_u8=None,
+                  drop=NO_DROP):
     check(lib().capk_attention_bwd(dtype_code(q.t), B, H, Nq, Nk, hd, float(scale), int(causal),
                                    q.ptr(), q.bs, q.rs, k.ptr(), k.bs, k.rs, v.ptr(), v.bs, v.rs,
                                    _p(key_pad_u8), o.ptr(), o.bs, o.rs, do.ptr(), do.bs, do.rs, _p(lse),
                                    dq.ptr(), dq.bs, dq.rs, dk.ptr(), dk.bs, dk.rs, dv.ptr(), dv.bs, dv.rs,
-                                   _stream()), "capk_attention_bwd")
+                                   float(drop[0]), int(drop[1]) & 0xFFFFFFFF, _stream()), "capk_attention_bwd")
 
 
 # ------------------------------------------------------ embeddings / misc ---
@@ -226,21 +236,23 @@ def vit_assemble_bwd(dx, B, Np, D, dcls, dpos):
     return dpatch
 
 
-def embedding_fwd(ids, table, pos, pos_offset, out_dtype):
+def embedding_fwd(ids, table, pos, pos_offset, out_dtype, drop=NO_DROP):
     B, T = ids.shape
     D = table.shape[1]
     out = torch.empty(B * T, D, dtype=out_dtype, device=table.device)
-    check(lib().capk_embedding_fwd(_DT[out_dtype], B, T, D, _p(ids), _p(table), _p(pos), int(pos_offset), _p(out),
-                                   _stream()), "capk_embedding_fwd")
+    check(lib().capk_embedding_fwd(_DT[out_dtype], B, T, D, _p(ids), _p(table), _p(pos), int(pos_offset),
+                                   float(drop[0]), int(drop[1]) & 0xFFFFFFFF, _p(out), _stream()),
+          "capk_embedding_fwd")
     return out
 
 
-def embedding_bwd(ids, dout, padding_idx, dtable, dpos, pos_offset=0):
+def embedding_bwd(ids, dout, padding_idx, dtable, dpos, pos_offset=0, drop=NO_DROP):
     B, T = ids.shape
     D = dout.shape[1]
     check(lib().capk_embedding_bwd(dtype_code(dout), B, T, D, _p(ids), _p(dout),
                                    -1 if padding_idx is None else int(padding_idx), _p(dtable), _p(dpos),
-                                   int(pos_offset), _stream()), "capk_embedding_bwd")
+                                   int(pos_offset), float(drop[0]), int(drop[1]) & 0xFFFFFFFF, _stream()),
+          "capk_embedding_bwd")
 
 
 def shifted_ce(logits2d, targets, B, T, V, ignore_index, *, want_loss=True, dlogits=None, grad_scale=None):
@@ -253,6 +265,14 @@ def shifted_ce(logits2d, targets, B, T, V, ignore_index, *, want_loss=True, dlog
                             int(ignore_index), _p(grad_scale), _p(loss), _p(dlogits), _p(ws), wsb, _stream()),
           "capk_shifted_ce")
     return loss
+
+
+def dropout_mask(n, p, seed, offset=0, device="cuda"):
+    """uint8 [n]: the keep mask the kernels use for (p, seed) at indices offset..offset+n-1."""
+    out = torch.empty(n, dtype=torch.uint8, device=device)
+    check(lib().capk_dropout_mask(int(n), int(offset), float(p), int(seed) & 0xFFFFFFFF, _p(out), _stream()),
+          "capk_dropout_mask")
+    return out
 
 
 def zero_(t):

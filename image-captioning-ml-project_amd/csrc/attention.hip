@@ -32,7 +32,11 @@ struct AttnArgs {
   const float* lse_in;
   void *dq, *dk, *dv;
   int64_t dq_bs, dq_rs, dk_bs, dk_rs, dv_bs, dv_rs;
+  Drop drop;  // attention-probability dropout, mask index ((b*H + h)*Nq + q)*Nk + key
 };
+__device__ __forceinline__ float pdrop(const AttnArgs& a, int b, int h, int q, int key) {
+  return a.drop.mul((((uint64_t)b * a.H + h) * a.Nq + q) * a.Nk + key);
+}
 
 __device__ __forceinline__ bool key_ok(const AttnArgs& a, int b, int key, int q) {
   if (key >= a.Nk) return false;
@@ -191,6 +195,13 @@ __global__ __launch_bounds__(512) void attn_fwd_bf16(AttnArgs a) {
     }
     l += __shfl_xor(l, 16, 64);
     l += __shfl_xor(l, 32, 64);
+    if (a.drop.on()) {  // dropout on the normalised probabilities (normaliser l unchanged)
+#pragma unroll
+      for (int kb = 0; kb < 16; ++kb)
+        if (kb < NKB)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sc[kb][r] *= pdrop(a, b, h, qi, kb * 16 + (lane >> 4) * 4 + r);
+    }
     f32x4 o[HDP / 16];
 #pragma unroll
     for (int db = 0; db < HDP / 16; ++db) o[db] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -290,8 +301,9 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16(AttnArgs a) {
           const int q = t * 32 + c * 16 + (lane >> 4) * 4 + r;
           const bool ok = q < a.Nq && (full_kb(a, kb) || key_ok(a, b, keyl, q));
           const float pv = ok ? exp2f(s_acc[r] * sl2 - lse_s[q]) : 0.f;
-          p[c][r] = pv;
-          ds[c][r] = pv * (dp_acc[r] - del_s[q]);
+          const float mk = a.drop.on() && q < a.Nq ? pdrop(a, b, h, q, keyl) : 1.f;
+          p[c][r] = pv * mk;
+          ds[c][r] = pv * (dp_acc[r] * mk - del_s[q]);
         }
       }
       const bf16x8 pb = pack8(p[0], p[1]), dsb = pack8(ds[0], ds[1]);
@@ -341,7 +353,8 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16(AttnArgs a) {
           const int key = t * 32 + c * 16 + (lane >> 4) * 4 + r;
           const bool ok = ql < a.Nq && (full_kb(a, 2 * t + c) || key_ok(a, b, key, ql));
           const float pv = ok ? exp2f(s_acc[r] * sl2 - lq) : 0.f;
-          ds[c][r] = pv * (dp_acc[r] - dq_del);
+          const float mk = a.drop.on() && ok ? pdrop(a, b, h, ql, key) : 1.f;
+          ds[c][r] = pv * (dp_acc[r] * mk - dq_del);
         }
       }
       const bf16x8 dsb = pack8(ds[0], ds[1]);
@@ -389,8 +402,9 @@ __global__ __launch_bounds__(64) void attn_fwd_f32(AttnArgs a) {
     for (int d = 0; d < HD; ++d) s += qv[d] * kb[(int64_t)j * a.k_rs + d];
     const float p = expf(s * a.scale - mx);
     l += p;
+    const float pd = a.drop.on() ? p * pdrop(a, b, h, q, j) : p;
 #pragma unroll
-    for (int d = 0; d < HD; ++d) o[d] += p * vb[(int64_t)j * a.v_rs + d];
+    for (int d = 0; d < HD; ++d) o[d] += pd * vb[(int64_t)j * a.v_rs + d];
   }
   float* orow = (float*)a.out + (int64_t)b * a.out_bs + (int64_t)q * a.out_rs + hoff;
 #pragma unroll
@@ -423,7 +437,8 @@ __global__ __launch_bounds__(64) void attn_bwd_dq_f32(AttnArgs a) {
       dp += dov[d] * vb[(int64_t)j * a.v_rs + d];
     }
     const float p = expf(s * a.scale - lse);
-    const float ds = p * (dp - del);
+    const float mk = a.drop.on() ? pdrop(a, b, h, q, j) : 1.f;
+    const float ds = p * (dp * mk - del);
 #pragma unroll
     for (int d = 0; d < HD; ++d) dq[d] += ds * kb[(int64_t)j * a.k_rs + d];
   }
@@ -456,10 +471,11 @@ __global__ __launch_bounds__(64) void attn_bwd_dkv_f32(AttnArgs a) {
       del += dorow[d] * orow[d];
     }
     const float p = expf(s * a.scale - a.lse_in[((int64_t)b * a.H + h) * a.Nq + q]);
-    const float ds = p * (dp - del);
+    const float mk = a.drop.on() ? pdrop(a, b, h, q, j) : 1.f;
+    const float ds = p * (dp * mk - del);
 #pragma unroll
     for (int d = 0; d < HD; ++d) {
-      dv[d] += p * dorow[d];
+      dv[d] += p * mk * dorow[d];
       dk[d] += ds * qr[d];
     }
   }
@@ -518,13 +534,15 @@ using namespace capk;
 extern "C" int capk_attention_fwd(int dtype, int B, int H, int Nq, int Nk, int hd, float scale, int causal,
                                   const void* q, int64_t q_bs, int64_t q_rs, const void* k, int64_t k_bs,
                                   int64_t k_rs, const void* v, int64_t v_bs, int64_t v_rs, const uint8_t* key_pad,
-                                  void* o, int64_t o_bs, int64_t o_rs, float* lse, void* stream) {
+                                  void* o, int64_t o_bs, int64_t o_rs, float* lse, float drop_p, uint32_t drop_seed,
+                                  void* stream) {
   int rc = check_common(dtype, B, H, Nq, Nk, hd);
   if (rc) return rc;
   AttnArgs a{};
   a.B = B; a.H = H; a.Nq = Nq; a.Nk = Nk; a.hd = hd; a.causal = causal; a.scale = scale;
   a.q = q; a.k = k; a.v = v; a.q_bs = q_bs; a.q_rs = q_rs; a.k_bs = k_bs; a.k_rs = k_rs; a.v_bs = v_bs; a.v_rs = v_rs;
   a.key_pad = key_pad; a.out = o; a.out_bs = o_bs; a.out_rs = o_rs; a.lse = lse;
+  a.drop = make_drop(drop_p, drop_seed);
   hipStream_t st = S(stream);
   if (dtype == CAPK_F32) {
     dim3 grid(B * H, cdiv(Nq, 64));
@@ -552,7 +570,7 @@ extern "C" int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int h
                                   const void* o, int64_t o_bs, int64_t o_rs, const void* dout, int64_t do_bs,
                                   int64_t do_rs, const float* lse, void* dq, int64_t dq_bs, int64_t dq_rs, void* dk,
                                   int64_t dk_bs, int64_t dk_rs, void* dv, int64_t dv_bs, int64_t dv_rs,
-                                  void* stream) {
+                                  float drop_p, uint32_t drop_seed, void* stream) {
   int rc = check_common(dtype, B, H, Nq, Nk, hd);
   if (rc) return rc;
   AttnArgs a{};
@@ -561,6 +579,7 @@ extern "C" int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int h
   a.key_pad = key_pad; a.o = o; a.o_bs = o_bs; a.o_rs = o_rs; a.dout = dout; a.do_bs = do_bs; a.do_rs = do_rs;
   a.lse_in = lse; a.dq = dq; a.dq_bs = dq_bs; a.dq_rs = dq_rs; a.dk = dk; a.dk_bs = dk_bs; a.dk_rs = dk_rs;
   a.dv = dv; a.dv_bs = dv_bs; a.dv_rs = dv_rs;
+  a.drop = make_drop(drop_p, drop_seed);
   hipStream_t st = S(stream);
   if (dtype == CAPK_F32) {
     {

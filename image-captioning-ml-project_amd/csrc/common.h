@@ -131,6 +131,33 @@ __device__ __forceinline__ float act_grad_fast(int act, float x) {
   return act_grad(act, x);
 }
 
+// --------------------------------------------------------------- dropout ----
+// Counter-based dropout mask: keep(seed, idx) = fmix32(seed ^ mix(idx)) >= p * 2^32.
+// The same (seed, idx) regenerates the identical mask in backward, so no mask tensor
+// is stored.  Index conventions per site are documented in include/capk.h.
+__host__ __device__ __forceinline__ uint32_t drop_hash(uint32_t seed, uint64_t idx) {
+  uint32_t x = seed ^ ((uint32_t)idx * 0x9E3779B9u) ^ ((uint32_t)(idx >> 32) * 0x7FEB352Du);
+  x ^= x >> 16; x *= 0x85EBCA6Bu; x ^= x >> 13; x *= 0xC2B2AE35u; x ^= x >> 16;
+  return x;
+}
+struct Drop {
+  uint32_t thr;   // keep iff hash >= thr ; thr == 0 -> dropout off
+  uint32_t seed;
+  float scale;    // 1 / (1 - p)
+  __device__ __forceinline__ bool on() const { return thr != 0; }
+  __device__ __forceinline__ float mul(uint64_t idx) const { return drop_hash(seed, idx) >= thr ? scale : 0.f; }
+};
+inline Drop make_drop(float p, uint32_t seed) {
+  Drop d;
+  if (p <= 0.f) { d.thr = 0; d.seed = 0; d.scale = 1.f; return d; }
+  double t = (double)p * 4294967296.0;
+  d.thr = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+  if (d.thr == 0) d.thr = 1;
+  d.seed = seed;
+  d.scale = 1.0f / (1.0f - p);
+  return d;
+}
+
 // ------------------------------------------------------- wave reductions ----
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -34,6 +34,7 @@ struct Epi {
   const void* aux;
   int64_t ldx;
   int M, N;
+  Drop drop;  // mask index m*N + n, applied after the activation (or with act'), before the residual
 };
 
 template <typename OutT>
@@ -52,12 +53,6 @@ __device__ __forceinline__ void epilogue8(const Epi& e, int m, int n, float (&v)
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] += b[i];
   }
-  if (e.res) {
-    float r[8];
-    Vec8<OutT>::load((const OutT*)e.res + (int64_t)m * e.ldr + n, r);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] += r[i];
-  }
   if (e.act & CAPK_ACT_BWD) {
     float a[8];
     Vec8<OutT>::load((const OutT*)e.aux + (int64_t)m * e.ldx + n, a);
@@ -69,6 +64,17 @@ __device__ __forceinline__ void epilogue8(const Epi& e, int m, int n, float (&v)
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = act_fwd_fast(e.act, v[i]);
   }
+  if (e.drop.on()) {
+    const uint64_t base = (uint64_t)m * e.N + n;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] *= e.drop.mul(base + i);
+  }
+  if (e.res) {
+    float r[8];
+    Vec8<OutT>::load((const OutT*)e.res + (int64_t)m * e.ldr + n, r);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] += r[i];
+  }
   Vec8<OutT>::store((OutT*)e.C + (int64_t)m * e.ldc + n, v);
 }
 
@@ -77,13 +83,14 @@ __device__ __forceinline__ void epilogue1(const Epi& e, int m, int n, float v) {
   v *= e.alpha;
   if (e.beta != 0.f) v += e.beta * to_f32(((const OutT*)e.C)[(int64_t)m * e.ldc + n]);
   if (e.bias) v += e.bias[n];
-  if (e.res) v += to_f32(((const OutT*)e.res)[(int64_t)m * e.ldr + n]);
   if (e.act & CAPK_ACT_BWD) {
     v *= act_grad(e.act & 15, to_f32(((const OutT*)e.aux)[(int64_t)m * e.ldx + n]));
   } else if (e.act) {
     if (e.pre) ((OutT*)e.pre)[(int64_t)m * e.ldx + n] = from_f32<OutT>(v);
     v = act_fwd(e.act, v);
   }
+  if (e.drop.on()) v *= e.drop.mul((uint64_t)m * e.N + n);
+  if (e.res) v += to_f32(((const OutT*)e.res)[(int64_t)m * e.ldr + n]);
   ((OutT*)e.C)[(int64_t)m * e.ldc + n] = from_f32<OutT>(v);
 }
 
@@ -421,12 +428,12 @@ extern "C" size_t capk_gemm_workspace(int in_dtype, int out_dtype, int M, int N,
 extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const void* A, int64_t lda,
                          int a_kmajor, const void* B, int64_t ldb, int b_kmajor, void* C, int64_t ldc,
                          float alpha, float beta, const float* bias, const void* residual, int64_t ldr,
-                         int act, void* preact, const void* aux, int64_t ldx, void* ws, size_t ws_bytes,
-                         void* stream) {
+                         int act, void* preact, const void* aux, int64_t ldx, float drop_p, uint32_t drop_seed,
+                         void* ws, size_t ws_bytes, void* stream) {
   CAPK_CHECK_ARG(M > 0 && N > 0 && K > 0, "capk_gemm: bad sizes M=%d N=%d K=%d", M, N, K);
   CAPK_CHECK_ARG(A && B && C, "capk_gemm: null operand");
   CAPK_CHECK_ARG(!(act & CAPK_ACT_BWD) || aux, "capk_gemm: backward activation needs aux");
-  Epi e{C, ldc, alpha, beta, bias, residual, ldr, act, preact, aux, ldx, M, N};
+  Epi e{C, ldc, alpha, beta, bias, residual, ldr, act, preact, aux, ldx, M, N, make_drop(drop_p, drop_seed)};
   hipStream_t st = S(stream);
   if (in_dtype == CAPK_F32) {
     CAPK_CHECK_ARG(out_dtype == CAPK_F32, "capk_gemm: f32 inputs need f32 output");

@@ -65,7 +65,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T
                                                      const float* __restrict__ w, const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, T* __restrict__ dx,
                                                      int64_t lddx, const T* __restrict__ dres, int64_t ldres,
-                                                     float* __restrict__ part) {
+                                                     float* __restrict__ part, Drop drop, T* __restrict__ dxd,
+                                                     int64_t lddxd) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // [4 waves][2][cols]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nch = cols >> 3;
@@ -110,6 +111,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T
         float o[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] = rs * (g[c][i] - m1 - xh[c][i] * m2);
+        if (dxd) {  // masked copy dx * keep/(1-p): gradient of the dropped branch feeding this LN
+          float od[8];
+          const uint64_t base = (uint64_t)row * cols + ch * 8;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) od[i] = o[i] * drop.mul(base + i);
+          Vec8<T>::store(dxd + (int64_t)row * lddxd + ch * 8, od);
+        }
         if (dres) {
           float r[8];
           Vec8<T>::load(dres + (int64_t)row * ldres + ch * 8, r);
@@ -187,7 +195,8 @@ extern "C" size_t capk_layernorm_bwd_workspace(int rows, int cols) {
 extern "C" int capk_layernorm_bwd(int dtype, int rows, int cols, const void* dy, int64_t lddy, const void* x,
                                   int64_t ldx, const float* w, const float* mean, const float* rstd, void* dx,
                                   int64_t lddx, const void* dres, int64_t ldres, float* dw, float* db,
-                                  int accumulate, void* ws, size_t ws_bytes, void* stream) {
+                                  int accumulate, float drop_p, uint32_t drop_seed, void* dx_drop,
+                                  int64_t lddx_drop, void* ws, size_t ws_bytes, void* stream) {
   CAPK_CHECK_ARG(rows > 0 && cols > 0 && cols % 8 == 0 && cols <= 2048, "capk_layernorm_bwd: cols=%d", cols);
   const int nb = ln_bwd_blocks(rows);
   CAPK_CHECK_ARG(ws && ws_bytes >= (size_t)nb * 2 * cols * sizeof(float), "capk_layernorm_bwd: workspace too small");
@@ -195,7 +204,8 @@ extern "C" int capk_layernorm_bwd(int dtype, int rows, int cols, const void* dy,
   const size_t shm = (size_t)8 * cols * sizeof(float);
 #define L(T, MC)                                                                                              \
   hipLaunchKernelGGL((ln_bwd_kernel<T, MC>), dim3(nb), dim3(256), shm, st, rows, cols, (const T*)dy, lddy,  \
-                     (const T*)x, ldx, w, mean, rstd, (T*)dx, lddx, (const T*)dres, ldres, (float*)ws)
+                     (const T*)x, ldx, w, mean, rstd, (T*)dx, lddx, (const T*)dres, ldres, (float*)ws,       \
+                     make_drop(drop_p, drop_seed), (T*)dx_drop, lddx_drop)
   if (dtype == CAPK_BF16) { if (cols <= 1024) L(bf16, 2); else L(bf16, 4); }
   else if (dtype == CAPK_F32) { if (cols <= 1024) L(float, 2); else L(float, 4); }
   else { set_error("capk_layernorm_bwd: dtype"); return CAPK_EINVAL; }

@@ -50,7 +50,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void embedding_fwd_kernel(int B, int T_, int D, const int64_t* __restrict__ ids,
                                                             const float* __restrict__ table,
                                                             const float* __restrict__ pos, int pos_offset,
-                                                            T* __restrict__ out) {
+                                                            T* __restrict__ out, Drop drop) {
   const int dch = D / 8;
   const int64_t total = (int64_t)B * T_ * dch;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -65,6 +65,11 @@ __global__ __launch_bounds__(256) void embedding_fwd_kernel(int B, int T_, int D
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] += pv[k];
     }
+    if (drop.on()) {
+      const uint64_t base = (uint64_t)row * D + c * 8;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] *= drop.mul(base + k);
+    }
     Vec8<T>::store(out + row * D + c * 8, v);
   }
 }
@@ -73,12 +78,12 @@ template <typename T>
 __global__ __launch_bounds__(256) void embedding_bwd_kernel(int B, int T_, int D, const int64_t* __restrict__ ids,
                                                             const T* __restrict__ dout, int padding_idx,
                                                             float* __restrict__ dtable, float* __restrict__ dpos,
-                                                            int pos_offset) {
+                                                            int pos_offset, Drop drop) {
   const int64_t total = (int64_t)B * T_ * D;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int d = (int)(i % D);
     const int64_t row = i / D;
-    const float g = to_f32(dout[i]);
+    const float g = drop.on() ? to_f32(dout[i]) * drop.mul((uint64_t)i) : to_f32(dout[i]);
     const int64_t id = ids[row];
     if (dtable && id != padding_idx) atomicAdd(dtable + id * D + d, g);
     if (dpos) atomicAdd(dpos + (int64_t)(pos_offset + (int)(row % T_)) * D + d, g);
@@ -398,10 +403,11 @@ extern "C" int capk_vit_assemble_bwd(int dtype, int B, int Np, int D, const void
 }
 
 extern "C" int capk_embedding_fwd(int dtype, int B, int T, int D, const int64_t* ids, const float* table,
-                                  const float* pos, int pos_offset, void* out, void* stream) {
+                                  const float* pos, int pos_offset, float drop_p, uint32_t drop_seed, void* out,
+                                  void* stream) {
   CAPK_CHECK_ARG(B > 0 && T > 0 && D % 8 == 0, "capk_embedding_fwd: bad shape");
   const int64_t work = (int64_t)B * T * D / 8;
-#define L(T_, _) hipLaunchKernelGGL(embedding_fwd_kernel<T_>, dim3(grid_for(work)), dim3(256), 0, S(stream), B, T, D, ids, table, pos, pos_offset, (T_*)out)
+#define L(T_, _) hipLaunchKernelGGL(embedding_fwd_kernel<T_>, dim3(grid_for(work)), dim3(256), 0, S(stream), B, T, D, ids, table, pos, pos_offset, (T_*)out, make_drop(drop_p, drop_seed))
   DT_DISPATCH(dtype, L, 0)
 #undef L
   CAPK_LAUNCH_CHECK("embedding_fwd_kernel");
@@ -409,10 +415,11 @@ extern "C" int capk_embedding_fwd(int dtype, int B, int T, int D, const int64_t*
 }
 
 extern "C" int capk_embedding_bwd(int dtype, int B, int T, int D, const int64_t* ids, const void* dout,
-                                  int padding_idx, float* dtable, float* dpos, int pos_offset, void* stream) {
+                                  int padding_idx, float* dtable, float* dpos, int pos_offset, float drop_p,
+                                  uint32_t drop_seed, void* stream) {
   CAPK_CHECK_ARG(B > 0 && T > 0 && D > 0, "capk_embedding_bwd: bad shape");
   const int64_t work = (int64_t)B * T * D;
-#define L(T_, _) hipLaunchKernelGGL(embedding_bwd_kernel<T_>, dim3(grid_for(work)), dim3(256), 0, S(stream), B, T, D, ids, (const T_*)dout, padding_idx, dtable, dpos, pos_offset)
+#define L(T_, _) hipLaunchKernelGGL(embedding_bwd_kernel<T_>, dim3(grid_for(work)), dim3(256), 0, S(stream), B, T, D, ids, (const T_*)dout, padding_idx, dtable, dpos, pos_offset, make_drop(drop_p, drop_seed))
   DT_DISPATCH(dtype, L, 0)
 #undef L
   CAPK_LAUNCH_CHECK("embedding_bwd_kernel");
@@ -497,5 +504,18 @@ extern "C" int capk_zero(void* ptr, size_t bytes, void* stream) {
   CAPK_CHECK_ARG(ptr, "capk_zero: null");
   hipError_t e = hipMemsetAsync(ptr, 0, bytes, S(stream));
   if (e != hipSuccess) return hip_status(e, "capk_zero");
+  return CAPK_OK;
+}
+
+// Debug/test view of the dropout mask: out[i] = keep(seed, offset + i) ? 1 : 0.
+__global__ void drop_mask_kernel(int64_t n, uint64_t offset, Drop d, uint8_t* out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = d.mul(offset + (uint64_t)i) != 0.f;
+}
+extern "C" int capk_dropout_mask(int64_t n, uint64_t offset, float p, uint32_t seed, uint8_t* out, void* stream) {
+  CAPK_CHECK_ARG(n >= 0 && out, "capk_dropout_mask: bad args");
+  if (n == 0) return CAPK_OK;
+  hipLaunchKernelGGL(drop_mask_kernel, dim3(grid_for(n)), dim3(256), 0, S(stream), n, offset, make_drop(p, seed), out);
+  CAPK_LAUNCH_CHECK("drop_mask_kernel");
   return CAPK_OK;
 }

@@ -45,11 +45,20 @@ const char* capk_last_error(void);
 int capk_version(void);
 int capk_device_arch(char* buf, int len); /* writes gcnArchName of the current device */
 
+/* --------------------------------------------------------------- dropout ----
+ * Dropout masks are never stored: keep(seed, idx) = fmix32(seed ^ mix(idx)) >= p*2^32
+ * is recomputed wherever needed, scale 1/(1-p).  drop_p = 0 disables.  Index per site:
+ *   GEMM epilogue: m*N + n of the output;  LN backward masked copy: row*cols + col;
+ *   attention probabilities: ((b*H + h)*Nq + q)*Nk + key;  embedding: (b*T + t)*D + d.
+ * capk_dropout_mask() materialises a mask for tests. */
+int capk_dropout_mask(int64_t n, uint64_t offset, float p, uint32_t seed, uint8_t* out, void* stream);
+
 /* ---------------------------------------------------------------- GEMM -----
- * C[m,n] = alpha * sum_k A(m,k) * B(n,k)  + beta * C[m,n]
- *          + bias[n] + residual[m,n]        (each optional; bias fp32)
- * then  act:  CAPK_ACT_x            -> preact (optional) = pre, C = act(pre)
- *             CAPK_ACT_BWD|CAPK_ACT_x -> C = pre * act'(aux[m,n])
+ * pre[m,n] = alpha * sum_k A(m,k) * B(n,k) + beta * C[m,n] + bias[n]   (bias fp32, optional)
+ * then  act:  CAPK_ACT_x              -> preact (optional) = pre, v = act(pre)
+ *             CAPK_ACT_BWD|CAPK_ACT_x -> v = pre * act'(aux[m,n])
+ *             CAPK_ACT_NONE           -> v = pre
+ * C[m,n] = dropout(v) + residual[m,n]   (dropout and residual optional)
  * A(m,k) = a_kmajor ? A[m*lda + k] : A[k*lda + m]
  * B(n,k) = b_kmajor ? B[n*ldb + k] : B[k*ldb + n]
  * Replaces every nn.Linear / Conv1D / patch-conv GEMM (and its two backward
@@ -66,6 +75,7 @@ int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K,
               void* C, int64_t ldc, float alpha, float beta,
               const float* bias, const void* residual, int64_t ldr,
               int act, void* preact, const void* aux, int64_t ldx,
+              float drop_p, uint32_t drop_seed,
               void* ws, size_t ws_bytes, void* stream);
 
 /* -------------------------------------------------------- LayerNorm -------
@@ -77,13 +87,16 @@ int capk_layernorm_fwd(int dtype, int rows, int cols, const void* x, int64_t ldx
                        const float* w, const float* b, float eps,
                        void* y, int64_t ldy, float* mean, float* rstd, void* stream);
 /* dx = LN'(dy) (+ dres if non-NULL); dw/db (fp32 [cols]) = sum over rows
- * (accumulate into existing dw/db when accumulate != 0).  ws: capk_layernorm_bwd_workspace. */
+ * (accumulate into existing dw/db when accumulate != 0).  If dx_drop != NULL it also
+ * receives LN'(dy) * dropout-mask (the gradient of a dropped residual branch, e.g.
+ * nn.TransformerDecoderLayer dropout1..3).  ws: capk_layernorm_bwd_workspace. */
 size_t capk_layernorm_bwd_workspace(int rows, int cols);
 int capk_layernorm_bwd(int dtype, int rows, int cols, const void* dy, int64_t lddy,
                        const void* x, int64_t ldx, const float* w,
                        const float* mean, const float* rstd,
                        void* dx, int64_t lddx, const void* dres, int64_t ldres,
                        float* dw, float* db, int accumulate,
+                       float drop_p, uint32_t drop_seed, void* dx_drop, int64_t lddx_drop,
                        void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------- Attention --------
@@ -100,7 +113,8 @@ int capk_attention_fwd(int dtype, int B, int H, int Nq, int Nk, int hd, float sc
                        const void* k, int64_t k_bs, int64_t k_rs,
                        const void* v, int64_t v_bs, int64_t v_rs,
                        const uint8_t* key_pad,
-                       void* o, int64_t o_bs, int64_t o_rs, float* lse, void* stream);
+                       void* o, int64_t o_bs, int64_t o_rs, float* lse,
+                       float drop_p, uint32_t drop_seed, void* stream);
 int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int hd, float scale, int causal,
                        const void* q, int64_t q_bs, int64_t q_rs,
                        const void* k, int64_t k_bs, int64_t k_rs,
@@ -110,7 +124,8 @@ int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int hd, float sc
                        const void* dout, int64_t do_bs, int64_t do_rs, const float* lse,
                        void* dq, int64_t dq_bs, int64_t dq_rs,
                        void* dk, int64_t dk_bs, int64_t dk_rs,
-                       void* dv, int64_t dv_bs, int64_t dv_rs, void* stream);
+                       void* dv, int64_t dv_bs, int64_t dv_rs,
+                       float drop_p, uint32_t drop_seed, void* stream);
 
 /* ------------------------------------------------- Embedding / patches ----
  * ViT patchify (im2col of Conv2d k=s=P, modeling_vit.py:60-69): images fp32
@@ -129,12 +144,14 @@ int capk_vit_assemble_bwd(int dtype, int B, int Np, int D, const void* dx, void*
 /* token + position embedding:  out[b*T+t] = table[ids[b*T+t]] + pos[pos_offset+t]
  * (decoders.py:409-414; GPT-2 wte+wpe).  pos may be NULL. */
 int capk_embedding_fwd(int dtype, int B, int T, int D, const int64_t* ids, const float* table,
-                       const float* pos, int pos_offset, void* out, void* stream);
+                       const float* pos, int pos_offset, float drop_p, uint32_t drop_seed,
+                       void* out, void* stream);
 /* dtable[ids] += dout (rows whose id == padding_idx skipped, nn.Embedding
  * padding_idx semantics, decoders.py:337-339); dpos[pos_offset+t] += sum_b dout.
  * dtable/dpos fp32, accumulated (caller zeroes). */
 int capk_embedding_bwd(int dtype, int B, int T, int D, const int64_t* ids, const void* dout,
-                       int padding_idx, float* dtable, float* dpos, int pos_offset, void* stream);
+                       int padding_idx, float* dtable, float* dpos, int pos_offset,
+                       float drop_p, uint32_t drop_seed, void* stream);
 
 /* --------------------------------------------------- Loss ------------------
  * Shifted cross entropy (CombinedLoss, src/train/losses.py:236-247):

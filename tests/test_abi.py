@@ -29,9 +29,21 @@ def test_library_exports_every_header_symbol():
         assert hasattr(lib, n), n
 
 
+def _arg_counts():
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(capk_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", src):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if args in ("", "void") else args.count(",") + 1
+    return out
+
+
 def test_ctypes_table_matches_header():
     from capk import _lib
     assert sorted(_lib.SIGNATURES) == _declared()
+    counts = _arg_counts()
+    for name, (_, args) in _lib.SIGNATURES.items():
+        assert len(args) == counts[name], (name, len(args), counts[name])
     lib = _lib.load()
     assert lib.capk_version() >= 100
 

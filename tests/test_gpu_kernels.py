@@ -34,8 +34,8 @@ def test_linear_fwd_epilogues(ops, dtype, M, N, K):
     r = torch.randn(M, N, device="cuda", generator=g).to(dtype)
     pre = torch.empty(M, N, device="cuda", dtype=dtype)
     y = ops.linear(x, w, b, residual=r, act=ACT_GELU_ERF, preact=pre)
-    ref_pre = x.float() @ w.float().t() + b + r.float()
-    ref = F.gelu(ref_pre)
+    ref_pre = x.float() @ w.float().t() + b
+    ref = F.gelu(ref_pre) + r.float()  # capk.h: C = dropout(act(pre)) + residual
     tol = 1e-5 if dtype == torch.float32 else 1e-2
     assert _rel(pre, ref_pre) < tol
     assert _rel(y, ref) < tol
@@ -277,3 +277,53 @@ def test_patchify_assemble(ops):
     assert torch.equal(dpatch.view(B, Np, D), dx.view(B, Np + 1, D)[:, 1:])
     assert torch.allclose(dpos, dx.view(B, Np + 1, D).sum(0), atol=1e-5)
     assert torch.allclose(dcls, dx.view(B, Np + 1, D)[:, 0].sum(0), atol=1e-5)
+
+
+# ---------------------------------------------------------------- dropout ---
+@cuda
+def test_dropout_mask_statistics_and_gemm_epilogue(ops):
+    from capk._lib import ACT_GELU_ERF
+    m = ops.dropout_mask(1 << 20, 0.1, 1234).float()
+    assert abs(float(m.mean()) - 0.9) < 3e-3
+    g = torch.Generator(device="cuda").manual_seed(11)
+    M, N, K = 300, 256, 128
+    x = torch.randn(M, K, device="cuda", generator=g)
+    w = torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)
+    b = torch.randn(N, device="cuda", generator=g)
+    r = torch.randn(M, N, device="cuda", generator=g)
+    mk = ops.dropout_mask(M * N, 0.25, 77).view(M, N).float() / 0.75
+    for dt, tol in ((torch.float32, 1e-5), (torch.bfloat16, 1e-2)):
+        pre = torch.empty(M, N, device="cuda", dtype=dt)
+        y = ops.linear(x.to(dt), w.to(dt), b, residual=r.to(dt), act=ACT_GELU_ERF, preact=pre, drop=(0.25, 77))
+        ref = F.gelu(x.to(dt).float() @ w.to(dt).float().t() + b) * mk + r.to(dt).float()
+        assert _rel(y, ref) < tol
+
+
+@cuda
+def test_attention_dropout_fwd_bwd(ops):
+    from capk.ops import HeadView
+    g = torch.Generator(device="cuda").manual_seed(12)
+    B, H, Nq, Nk, hd, p, seed = 3, 4, 20, 37, 32, 0.2, 4242
+    D = H * hd
+    for dt, tol, tolb in ((torch.float32, 1e-5, 1e-4), (torch.bfloat16, 1.5e-2, 3e-2)):
+        q = torch.randn(B * Nq, D, device="cuda", generator=g).to(dt)
+        kv = torch.randn(B * Nk, 2 * D, device="cuda", generator=g).to(dt)
+        do = torch.randn(B * Nq, D, device="cuda", generator=g).to(dt)
+        o = torch.empty(B * Nq, D, device="cuda", dtype=dt)
+        Q, K_, V_, O = HeadView(q, 0, Nq * D, D), HeadView(kv, 0, Nk * 2 * D, 2 * D), HeadView(kv, D, Nk * 2 * D, 2 * D), HeadView(o, 0, Nq * D, D)
+        sc = 1 / math.sqrt(hd)
+        lse, _ = ops.attention_fwd(Q, K_, V_, O, B, H, Nq, Nk, hd, sc, drop=(p, seed))
+        mk = ops.dropout_mask(B * H * Nq * Nk, p, seed).view(B, H, Nq, Nk).float() / (1 - p)
+        qr = q.float().view(B, Nq, H, hd).transpose(1, 2).requires_grad_(True)
+        kr = kv.float()[:, :D].reshape(B, Nk, H, hd).transpose(1, 2).detach().requires_grad_(True)
+        vr = kv.float()[:, D:].reshape(B, Nk, H, hd).transpose(1, 2).detach().requires_grad_(True)
+        ref = (torch.softmax(qr @ kr.transpose(-1, -2) * sc, -1) * mk) @ vr
+        assert _rel(o.float().view(B, Nq, H, hd).transpose(1, 2), ref) < tol
+        ref.backward(do.float().view(B, Nq, H, hd).transpose(1, 2))
+        dq, dkv = torch.empty_like(q), torch.empty_like(kv)
+        ops.attention_bwd(Q, K_, V_, O, HeadView(do, 0, Nq * D, D), lse, HeadView(dq, 0, Nq * D, D),
+                          HeadView(dkv, 0, Nk * 2 * D, 2 * D), HeadView(dkv, D, Nk * 2 * D, 2 * D), B, H, Nq, Nk, hd,
+                          sc, drop=(p, seed))
+        assert _rel(dq.float().view(B, Nq, H, hd).transpose(1, 2), qr.grad) < tolb
+        assert _rel(dkv.float()[:, :D].reshape(B, Nk, H, hd).transpose(1, 2), kr.grad) < tolb
+        assert _rel(dkv.float()[:, D:].reshape(B, Nk, H, hd).transpose(1, 2), vr.grad) < tolb

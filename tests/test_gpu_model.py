@@ -45,6 +45,7 @@ def _tiny_model(z, precision):
     missing, unexpected = model.load_state_dict(sd, strict=False)
     assert not unexpected and not missing, (missing, unexpected)
     store = capk.prepare(model, "cuda", precision)
+    model.eval()  # the reference fixtures were produced with dropout off
     return model, store, cfg
 
 
@@ -119,6 +120,7 @@ def _full_model(precision, seed=42):
     model = cm.ImageCaptioningModel(cfg)
     cpu_sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
     store = capk.prepare(model, "cuda", precision)
+    model.eval()
     return model, store, cfg, cpu_sd
 
 
@@ -171,6 +173,7 @@ def test_bf16_train_steps_reduce_loss():
     g = torch.Generator(device="cuda").manual_seed(0)
     images = torch.randn(B, 3, 224, 224, device="cuda", generator=g)
     caps = torch.randint(0, 50256, (B, 20), device="cuda", generator=g)
+    model.train()  # decoder dropout p=0.1 active, as in the reference trainer
     opt = CapkAdamW(store, lr=1e-4)
     loss_fn = CombinedLoss(50256)
     losses = []
@@ -182,3 +185,91 @@ def test_bf16_train_steps_reduce_loss():
         losses.append(float(loss))
     assert all(np.isfinite(losses)), losses
     assert losses[-1] < losses[0], losses
+
+
+@cuda
+def test_decoder_train_mode_dropout_matches_masked_reference(golden_dir):
+    """Train-mode decoder (p=0.1 at 7 sites) vs a PyTorch reference applying the SAME masks
+    (materialised with capk_dropout_mask from the intercepted per-site seeds): logits and
+    every decoder gradient.  Mask index conventions: include/capk.h."""
+    import math
+
+    import torch.nn.functional as F
+
+    from capk import ops
+    from capk.models import transformer as tr
+    from capk.train import CombinedLoss
+    z = np.load(os.path.join(golden_dir, "vit_transformer_step.npz"), allow_pickle=False)
+    model, store, cfg = _tiny_model(z, "fp32")
+    dec = model.decoder
+    dec.dropout_p = 0.1
+    dec.train()
+    D, Le, He, Ld, Hd, V, pad, patch, img = [int(x) for x in z["meta/dims"]]
+    seeds = []
+    orig = tr.next_seed
+    tr.next_seed = lambda: (seeds.append(1000 + 7919 * len(seeds)) or seeds[-1])
+    try:
+        images = torch.from_numpy(z["in/images"]).cuda()
+        caps = torch.from_numpy(z["in/captions"]).cuda()
+        with torch.no_grad():
+            feats = model.encoder(images)["features"].contiguous().clone()
+        feats.requires_grad_(True)
+        out = dec({"features": feats, "pooled_features": None, "attention_mask": None}, caps)
+        loss = CombinedLoss(pad)(out["logits"], caps)["total_loss"]
+        loss.backward()
+        torch.cuda.synchronize()
+    finally:
+        tr.next_seed = orig
+    p = 0.1
+    B, T = caps.shape
+    S = feats.shape[1]
+    H, hd = Hd, D // Hd
+
+    def mask(n, seed, shape):
+        return ops.dropout_mask(n, p, seed).view(shape).float() / (1 - p)
+
+    P = {n: t.detach().clone().requires_grad_(True) for n, t in dec.named_parameters()}
+    fr = feats.detach().clone().requires_grad_(True)
+    mem = F.linear(fr, P["visual_projection.weight"], P["visual_projection.bias"])
+    si = iter(seeds)
+    x = P["embedding.weight"][caps] + P["position_encoding.weight"][:T][None]
+    x = x * mask(B * T * D, next(si), (B, T, D))
+    tgt_pad = caps == pad
+
+    def mha(xq, xkv, w, b, wo, bo, causal, kpad, seed, Nk):
+        q = F.linear(xq, w[:D], b[:D]).view(B, T, H, hd).transpose(1, 2)
+        k = F.linear(xkv, w[D:2 * D], b[D:2 * D]).view(B, Nk, H, hd).transpose(1, 2)
+        v = F.linear(xkv, w[2 * D:], b[2 * D:]).view(B, Nk, H, hd).transpose(1, 2)
+        s = q @ k.transpose(-1, -2) / math.sqrt(hd)
+        if causal:
+            s = s.masked_fill(torch.ones(T, Nk, dtype=torch.bool, device=s.device).triu(1), float("-inf"))
+        if kpad is not None:
+            s = s.masked_fill(kpad[:, None, None, :], float("-inf"))
+        a = torch.softmax(s, -1) * mask(B * H * T * Nk, seed, (B, H, T, Nk))
+        return F.linear((a @ v).transpose(1, 2).reshape(B, T, D), wo, bo)
+
+    for i in range(Ld):
+        pre = f"transformer_decoder.layers.{i}."
+        s_sa, s_d1, s_ca, s_d2, s_ffn, s_d3 = [next(si) for _ in range(6)]
+        y = mha(x, x, P[pre + "self_attn.in_proj_weight"], P[pre + "self_attn.in_proj_bias"],
+                P[pre + "self_attn.out_proj.weight"], P[pre + "self_attn.out_proj.bias"], True, tgt_pad, s_sa, T)
+        x = F.layer_norm(x + y * mask(B * T * D, s_d1, (B, T, D)), (D,), P[pre + "norm1.weight"],
+                         P[pre + "norm1.bias"], 1e-5)
+        y = mha(x, mem, P[pre + "multihead_attn.in_proj_weight"], P[pre + "multihead_attn.in_proj_bias"],
+                P[pre + "multihead_attn.out_proj.weight"], P[pre + "multihead_attn.out_proj.bias"], False, None,
+                s_ca, S)
+        x = F.layer_norm(x + y * mask(B * T * D, s_d2, (B, T, D)), (D,), P[pre + "norm2.weight"],
+                         P[pre + "norm2.bias"], 1e-5)
+        I = P[pre + "linear1.weight"].shape[0]
+        f = F.gelu(F.linear(x, P[pre + "linear1.weight"], P[pre + "linear1.bias"])) * mask(B * T * I, s_ffn,
+                                                                                            (B, T, I))
+        y = F.linear(f, P[pre + "linear2.weight"], P[pre + "linear2.bias"])
+        x = F.layer_norm(x + y * mask(B * T * D, s_d3, (B, T, D)), (D,), P[pre + "norm3.weight"],
+                         P[pre + "norm3.bias"], 1e-5)
+    ref = F.linear(x, P["output_layer.weight"], P["output_layer.bias"])
+    torch.testing.assert_close(out["logits"].detach(), ref.detach(), rtol=1e-4, atol=1e-5)
+    F.cross_entropy(ref[:, :-1].reshape(-1, V), caps[:, 1:].reshape(-1), ignore_index=pad).backward()
+    torch.testing.assert_close(feats.grad, fr.grad, rtol=1e-3, atol=1e-6)
+    for n, t in dec.named_parameters():
+        g = P[n].grad if P[n].grad is not None else torch.zeros_like(P[n])
+        torch.testing.assert_close(t._capk_grad, g, rtol=1e-3, atol=1e-6, msg=n)
