@@ -45,12 +45,29 @@ class TransformerDecoder(TransformerDecoderCore, CaptionDecoder):
         return {"logits": logits, "hidden_states": hidden}
 
     @torch.no_grad()
-    def generate(self, encoder_features, max_length, **kwargs):
-        """Greedy decoding (decoders.py:439-493): start from bos, append argmax of the
-        last position, stop when every sequence emitted eos.  Same arithmetic as the
-        reference's full re-decode per step (pad mask off: no pad in a generated prefix)."""
+    def generate(self, encoder_features, max_length, num_beams=1, length_penalty=1.0, early_stopping=False,
+                 **kwargs):
+        """num_beams == 1: greedy decoding (decoders.py:439-493): start from bos, append
+        argmax of the last position, stop when every sequence emitted eos.  Same
+        arithmetic as the reference's full re-decode per step (pad mask off: no pad in a
+        generated prefix).
+
+        num_beams > 1: HF beam search semantics (the reference's
+        only beam search is GPT2Decoder.generate -> GenerationMixin._beam_search,
+        decoders.py:645-654) on the KV-cached decoder; returns (sequences [B, <=max_length],
+        {"sequences_scores", "beam_indices"})."""
         feats = encoder_features["features"]
         B = feats.shape[0]
+        if num_beams > 1:
+            from ..beam import beam_search
+            from .transformer import KVDecodeRunner
+            runner = KVDecodeRunner(self, feats, num_beams, max_length)
+            prompt = torch.full((B,), self.bos_token_id, dtype=torch.long, device=feats.device)
+            out = beam_search(runner.step, B, num_beams, max_length, prompt, self.eos_token_id,
+                              pad_token_id=self.pad_token_id, length_penalty=length_penalty,
+                              early_stopping=early_stopping, vocab_size=self.vocab_size)
+            return out["sequences"], {"sequences_scores": out["sequences_scores"],
+                                      "beam_indices": out["beam_indices"]}
         ids = torch.full((B, 1), self.bos_token_id, dtype=torch.long, device=feats.device)
         for _ in range(max_length - 1):
             logits, _ = self.forward_logits(feats, ids, use_pad_mask=False)

@@ -287,3 +287,92 @@ def _padded_grad(dlogits, logits_pad, BT, V, Vp):
     out = torch.zeros(BT, Vp, dtype=logits_pad.dtype, device=logits_pad.device)
     out[:, :V].copy_(dlogits.reshape(BT, V))
     return out
+
+
+class KVDecodeRunner:
+    """KV-cached incremental decode of the Transformer decoder for beam search
+    (SURVEY §8a A14 on the A4 model; HF's per-step ``past_key_values`` path).
+
+    Same arithmetic per position as the teacher-forced pass (eval mode, no pad mask,
+    as ``generate`` runs it, decoders.py:473-477), one new token per beam per step:
+
+    * memory side, once per image: visual projection and every layer's cross K/V
+      ``[B*(S+gap), 2D]`` — the k beams of image b share them (the cross-attention runs
+      with the k beam queries of image b as one batch entry: Nq = k);
+    * self side: the fused QKV GEMM of the new token writes straight into the layer's
+      cache slot ``cache[l, r, t, :]`` (layout [layers, B*k, max_length, 3D]); the
+      attention reads keys/values 0..t of row r in place;
+    * after each beam step the caches of all layers are reordered in one gather launch
+      (ping-pong buffers) — HF ``Cache.reorder_cache(beam_idx)`` (utils.py:3479-3489).
+    """
+
+    def __init__(self, m, features, num_beams, max_length):
+        dt = m.cdtype
+        self.m, self.dt, self.k, self.Lmax = m, dt, num_beams, max_length
+        B, S, D = features.shape
+        self.B, self.S, self.D = B, S, D
+        self.H = m.num_heads
+        self.hd = D // self.H
+        self.scale = 1.0 / math.sqrt(self.hd)
+        if features.dtype != dt:
+            raise TypeError(f"capk TransformerDecoder: features dtype {features.dtype} != compute dtype {dt}")
+        feat_mem, self.rpb, _ = _mem_geometry(features)
+        vp = m.visual_projection
+        mem = ops.linear(feat_mem, W(vp.weight, dt), vp.bias.detach())
+        self.mem_kv = []
+        for L in m.transformer_decoder.layers:
+            ca = L.multihead_attn
+            self.mem_kv.append(ops.linear(mem, W(ca.in_proj_weight, dt)[D:], ca.in_proj_bias.detach()[D:]))
+        nl = len(m.transformer_decoder.layers)
+        R = B * num_beams
+        self.R = R
+        shape = (nl, R, max_length, 3 * D)
+        self.cache = torch.empty(shape, dtype=dt, device=features.device)
+        self.spare = torch.empty(shape, dtype=dt, device=features.device)
+        ol = m.output_layer
+        self.wout = ol.weight._capk_pad_bf16 if dt == torch.bfloat16 else ol.weight._capk_pad_master
+        self.bout = _pad_bias(ol)
+
+    def reorder(self, idx, t):
+        """Rows r <- idx[r] for cache positions [0, t) of every layer (one launch)."""
+        if t <= 0:
+            return
+        c = self.cache
+        nl, R, Lm, C3 = c.shape
+        check = ops.check
+        check(ops.lib().capk_gather_rows(ops.dtype_code(c), nl, R, t * C3, idx.data_ptr(), c.data_ptr(), Lm * C3,
+                                         R * Lm * C3, self.spare.data_ptr(), Lm * C3, R * Lm * C3, ops._stream()),
+              "capk_gather_rows")
+        self.cache, self.spare = self.spare, self.cache
+
+    def step(self, cur_len, ids, reorder_idx):
+        """Feed the tokens at position t = cur_len-1 for all B*k rows -> logits [R, Vp]."""
+        m, dt, D, H, hd, R, k = self.m, self.dt, self.D, self.H, self.hd, self.R, self.k
+        t = cur_len - 1
+        if reorder_idx is not None:
+            self.reorder(reorder_idx, t)
+        Lm = self.Lmax
+        x = ops.embedding_fwd(ids.view(R, 1), m.embedding.weight.detach(), m.position_encoding.weight.detach(), t, dt)
+        rs_cache = Lm * 3 * D
+        for li, L in enumerate(m.transformer_decoder.layers):
+            sa, ca = L.self_attn, L.multihead_attn
+            cl = self.cache[li]                      # [R, Lm, 3D]
+            ops.linear(x, W(sa.in_proj_weight, dt), sa.in_proj_bias.detach(), out=cl[:, t, :])
+            a = torch.empty(R, D, dtype=dt, device=x.device)
+            ops.attention_fwd(HeadView(cl, t * 3 * D, rs_cache, 3 * D), HeadView(cl, D, rs_cache, 3 * D),
+                              HeadView(cl, 2 * D, rs_cache, 3 * D), HeadView(a, 0, D, D), R, H, 1, t + 1, hd,
+                              self.scale)
+            s1 = ops.linear(a, W(sa.out_proj.weight, dt), sa.out_proj.bias.detach(), residual=x)
+            x1, _, _ = ops.layernorm_fwd(s1, L.norm1.weight.detach(), L.norm1.bias.detach(), L.norm1.eps)
+            qc = ops.linear(x1, W(ca.in_proj_weight, dt)[:D], ca.in_proj_bias.detach()[:D])
+            c = torch.empty(R, D, dtype=dt, device=x.device)
+            kv = self.mem_kv[li]
+            ops.attention_fwd(HeadView(qc, 0, k * D, D), HeadView(kv, 0, self.rpb * 2 * D, 2 * D),
+                              HeadView(kv, D, self.rpb * 2 * D, 2 * D), HeadView(c, 0, k * D, D), self.B, H, k,
+                              self.S, hd, self.scale)
+            s2 = ops.linear(c, W(ca.out_proj.weight, dt), ca.out_proj.bias.detach(), residual=x1)
+            x2, _, _ = ops.layernorm_fwd(s2, L.norm2.weight.detach(), L.norm2.bias.detach(), L.norm2.eps)
+            f = ops.linear(x2, W(L.linear1.weight, dt), L.linear1.bias.detach(), act=ACT_GELU_ERF)
+            s3 = ops.linear(f, W(L.linear2.weight, dt), L.linear2.bias.detach(), residual=x2)
+            x, _, _ = ops.layernorm_fwd(s3, L.norm3.weight.detach(), L.norm3.bias.detach(), L.norm3.eps)
+        return ops.linear(x, self.wout, self.bout)

@@ -1,0 +1,493 @@
+// Beam search on the device.
+//
+// Semantics: transformers 5.15 GenerationMixin._beam_search
+// (transformers/generation/utils.py:3208-3535), decoder-only, prompt length 1,
+// one EOS id, MaxLength + EOS stopping — the search GPT2Decoder.generate reaches
+// (src/models/decoders.py:645-654) and, per SURVEY D16, the one applied to every
+// decoder through a per-step logits callback.
+//
+// One step = two kernels:
+//   beam_rows_kernel   grid = B*k rows, 256 threads.  Streams one row of logits
+//                      (V valid columns of a padded row) once from HBM: online
+//                      max / sum-exp (log_softmax statistics) and the row's top-2k
+//                      logits.  Within a row log_softmax(x) + running_score is
+//                      monotone in x, so the image's top-2k over [k*V] is contained
+//                      in the union of its rows' top-2k.
+//   beam_update_kernel grid = B, one wave.  Candidate scores
+//                      ((x - max) - logsum) + running_score exactly as torch
+//                      log_softmax + add, top-2k (score desc, flat index asc),
+//                      EOS / max-length hits, next running beams (top-k after the
+//                      -1e9 penalty), finished-beam merge with the length penalty,
+//                      early-stop heuristic, and the cache-reorder indices.
+// All search state (running/finished sequences, scores, beam indices, flags)
+// lives in one device buffer; the host reads 3 flag words per step to decide
+// whether to continue (HF's batch-global stopping rule).
+#include "common.h"
+
+namespace capk {
+
+static constexpr int BEAM_KMAX = 8;            // num_beams <= 8
+static constexpr int BEAM_K2MAX = 2 * BEAM_KMAX;
+static constexpr int BEAM_LMAX = 256;          // max_length <= 256
+static constexpr int ROWS_THREADS = 256;
+
+struct BeamState {
+  int* flags;      // [4]: any improvement possible, any batch not all finished, any valid continuation
+  int* rseq;       // [B][k][L] running sequences
+  float* rscore;   // [B][k]
+  int* rbi;        // [B][k][L-1] running beam indices
+  int* seq;        // [B][k][L] finished sequences
+  float* score;    // [B][k]
+  int* bi;         // [B][k][L-1]
+  int* fin;        // [B][k]
+  int* unsat;      // [B]
+};
+
+__host__ __device__ inline size_t al64(size_t x) { return (x + 63) & ~(size_t)63; }
+
+__host__ __device__ inline size_t beam_layout(int B, int k, int L, char* base, BeamState* s) {
+  size_t off = 0;
+  auto take = [&](size_t bytes) { char* p = base + off; off += al64(bytes); return p; };
+  const size_t Bk = (size_t)B * k;
+  char* p;
+  p = take(16);                          if (s) s->flags = (int*)p;
+  p = take(Bk * L * 4);                  if (s) s->rseq = (int*)p;
+  p = take(Bk * 4);                      if (s) s->rscore = (float*)p;
+  p = take(Bk * (L - 1) * 4);            if (s) s->rbi = (int*)p;
+  p = take(Bk * L * 4);                  if (s) s->seq = (int*)p;
+  p = take(Bk * 4);                      if (s) s->score = (float*)p;
+  p = take(Bk * (L - 1) * 4);            if (s) s->bi = (int*)p;
+  p = take(Bk * 4);                      if (s) s->fin = (int*)p;
+  p = take((size_t)B * 4);               if (s) s->unsat = (int*)p;
+  // per-row candidates written by beam_rows_kernel
+  return off;
+}
+
+// candidate scratch after the state: [B*k][K2] values + tokens, [B*k] max, logsum
+__host__ __device__ inline size_t beam_scratch_bytes(int B, int k) {
+  const size_t Bk = (size_t)B * k;
+  return al64(Bk * 2 * k * 4) * 2 + al64(Bk * 4) * 2;
+}
+
+// order-preserving float -> uint32 (larger float -> larger key)
+__device__ __forceinline__ uint32_t fkey(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float funkey(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k ^ 0x80000000u) : ~k);
+}
+// (value desc, index asc) as one u64 maximised
+__device__ __forceinline__ uint64_t ckey(float v, int idx) {
+  return ((uint64_t)fkey(v) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)idx);
+}
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int o) {
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  lo = __shfl_xor(lo, o, 64);
+  hi = __shfl_xor(hi, o, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    uint64_t w = shfl_xor_u64(v, o);
+    v = w > v ? w : v;
+  }
+  return v;
+}
+
+// merge (m, s) log-sum-exp partials; m = -inf means empty
+__device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2) {
+  if (m2 == -INFINITY) return;
+  if (m == -INFINITY) { m = m2; s = s2; return; }
+  if (m2 > m) { s = s * __expf(m - m2) + s2; m = m2; }
+  else s += s2 * __expf(m2 - m);
+}
+
+template <typename T>
+__global__ __launch_bounds__(ROWS_THREADS) void beam_rows_kernel(const T* __restrict__ logits, int64_t ld, int V,
+                                                                 int K2, int* flags, float* cand_val, int* cand_tok,
+                                                                 float* row_max, float* row_logsum) {
+  const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (r == 0 && tid < 4) flags[tid] = 0;
+  const T* x = logits + (int64_t)r * ld;
+  uint64_t keys[BEAM_K2MAX];
+#pragma unroll
+  for (int j = 0; j < BEAM_K2MAX; ++j) keys[j] = 0;
+  float m = -INFINITY, s = 0.f;
+  auto insert = [&](uint64_t key) {
+    if (key <= keys[BEAM_K2MAX - 1]) return;
+#pragma unroll
+    for (int j = BEAM_K2MAX - 1; j > 0; --j) {
+      const uint64_t a = keys[j - 1], b = keys[j];
+      keys[j] = key > a ? a : (key > b ? key : b);
+    }
+    keys[0] = key > keys[0] ? key : keys[0];
+  };
+  const int V8 = V & ~7;
+  for (int i = tid * 8; i < V8; i += ROWS_THREADS * 8) {
+    float v[8];
+    Vec8<T>::load(x + i, v);
+    float cm = v[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) cm = fmaxf(cm, v[j]);
+    if (cm > m) { s = (m == -INFINITY) ? 0.f : s * __expf(m - cm); m = cm; }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s += __expf(v[j] - m);
+      insert(ckey(v[j], i + j));
+    }
+  }
+  for (int i = V8 + tid; i < V; i += ROWS_THREADS) {
+    const float v = to_f32(x[i]);
+    if (v > m) { s = (m == -INFINITY) ? 0.f : s * __expf(m - v); m = v; }
+    s += __expf(v - m);
+    insert(ckey(v, i));
+  }
+  // log-sum-exp statistics: wave, then block
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    lse_merge(m, s, m2, s2);
+  }
+  __shared__ float sm[4], ss[4];
+  __shared__ uint64_t wk[4][BEAM_K2MAX];
+  if (lane == 0) { sm[w] = m; ss[w] = s; }
+  // wave top-K2: K2 rounds of wave argmax over each lane's sorted list head
+  for (int j = 0; j < K2; ++j) {
+    const uint64_t best = wave_max_u64(keys[0]);
+    if (keys[0] == best && best != 0) {
+#pragma unroll
+      for (int t = 0; t < BEAM_K2MAX - 1; ++t) keys[t] = keys[t + 1];
+      keys[BEAM_K2MAX - 1] = 0;
+    }
+    if (lane == 0) wk[w][j] = best;
+  }
+  __syncthreads();
+  if (w == 0) {
+    float M = sm[0], Ssum = ss[0];
+    for (int q = 1; q < 4; ++q) lse_merge(M, Ssum, sm[q], ss[q]);
+    // final top-K2 of the 4*K2 wave candidates by rank counting
+    const int nc = 4 * K2;
+    uint64_t mine = lane < nc ? wk[lane / K2][lane % K2] : 0;
+    int rank = 0;
+    for (int c = 0; c < nc; ++c) {
+      const uint64_t o = wk[c / K2][c % K2];
+      rank += (o > mine) ? 1 : 0;
+    }
+    if (lane < nc && rank < K2 && mine != 0) {
+      cand_val[(int64_t)r * K2 + rank] = funkey((uint32_t)(mine >> 32));
+      cand_tok[(int64_t)r * K2 + rank] = (int)(0xFFFFFFFFu - (uint32_t)mine);
+    }
+    if (lane == 0) { row_max[r] = M; row_logsum[r] = logf(Ssum); }
+  }
+}
+
+// ---------------------------------------------------------------- update ----
+__global__ __launch_bounds__(64) void beam_update_kernel(BeamState st, int k, int L, int V, int cur_len, int eos,
+                                                         float fin_div, float best_div, int early_true,
+                                                         const float* __restrict__ cand_val,
+                                                         const int* __restrict__ cand_tok,
+                                                         const float* __restrict__ row_max,
+                                                         const float* __restrict__ row_logsum, int* reorder,
+                                                         int64_t* next_ids) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int K2 = 2 * k, Lb = L - 1;
+  extern __shared__ int sh[];
+  int* o_rseq = sh;                       // [k][L]
+  int* o_rbi = o_rseq + k * L;            // [k][L-1]
+  int* o_seq = o_rbi + k * Lb;            // [k][L]
+  int* o_bi = o_seq + k * L;              // [k][L-1]
+  __shared__ float t_lp[BEAM_K2MAX];      // top-2k accumulated log-probs
+  __shared__ int t_beam[BEAM_K2MAX], t_tok[BEAM_K2MAX], t_hit[BEAM_K2MAX];
+  __shared__ int nxt[BEAM_KMAX];          // running selection (index into top-2k)
+  __shared__ int msel[BEAM_KMAX];         // finished selection (index into merged k + 2k)
+  __shared__ float m_score[BEAM_KMAX + BEAM_K2MAX];
+  __shared__ int m_fin[BEAM_KMAX + BEAM_K2MAX];
+  __shared__ float n_rscore[BEAM_KMAX];
+  __shared__ float t_trl[BEAM_K2MAX];
+  const size_t sb = (size_t)b * k;
+  // 0. stash the old sequences / indices of this image
+  for (int e = lane; e < k * L; e += 64) { o_rseq[e] = st.rseq[sb * L + e]; o_seq[e] = st.seq[sb * L + e]; }
+  for (int e = lane; e < k * Lb; e += 64) { o_rbi[e] = st.rbi[sb * Lb + e]; o_bi[e] = st.bi[sb * Lb + e]; }
+  const int unsat_old = st.unsat[b];
+  // 1. candidates: k rows x K2, score = ((x - max) - logsum) + running (torch log_softmax + add)
+  const int nc = k * K2;  // <= 128
+  float cs[2];
+  uint64_t ck[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c = lane + 64 * h;
+    ck[h] = 0;
+    cs[h] = 0.f;
+    if (c < nc) {
+      const int rr = c / K2;
+      const int64_t row = (int64_t)sb + rr;
+      const float xv = cand_val[row * K2 + (c % K2)];
+      const int tok = cand_tok[row * K2 + (c % K2)];
+      const float lp = (xv - row_max[row]) - row_logsum[row];
+      cs[h] = lp + st.rscore[row];
+      ck[h] = ckey(cs[h], rr * V + tok);
+    }
+  }
+  // rank-count over all candidates (keys unique: flat index unique)
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    int rank = 0;
+    for (int c2 = 0; c2 < nc; ++c2) {
+      const uint64_t o = __shfl(ck[c2 >= 64 ? 1 : 0], c2 & 63, 64);
+      rank += (o > ck[h]) ? 1 : 0;
+    }
+    const int c = lane + 64 * h;
+    if (c < nc && rank < K2) {
+      const int flat = (int)(0xFFFFFFFFu - (uint32_t)ck[h]);
+      t_lp[rank] = cs[h];
+      t_beam[rank] = flat / V;
+      t_tok[rank] = flat % V;
+    }
+  }
+  __syncthreads();
+  // 2. stopping criteria per continuation; running log-probs with the -1e9 penalty
+  if (lane < K2) {
+    const int hit = (t_tok[lane] == eos) || (cur_len + 1 >= L);
+    t_hit[lane] = hit;
+    t_trl[lane] = t_lp[lane] + (hit ? -1.0e9f : -0.0f);
+    // finished-candidate score: lp / len^lp, + full, + !unsat, + !just_finished penalties (utils.py:3175-3190)
+    float sc = t_lp[lane] / fin_div;
+    int full = 1;
+    for (int i = 0; i < k; ++i) full &= (st.fin[sb + i] != 0);
+    sc += (full && early_true) ? -1.0e9f : -0.0f;
+    sc += unsat_old ? -0.0f : -1.0e9f;
+    const int jf = hit && (lane < k);
+    sc += jf ? -0.0f : -1.0e9f;
+    m_score[k + lane] = sc;
+    m_fin[k + lane] = jf;
+  }
+  if (lane < k) { m_score[lane] = st.score[sb + lane]; m_fin[lane] = st.fin[sb + lane]; }
+  __syncthreads();
+  // 3. top-k running (ties: lower position first) and top-k finished over the merged list
+  if (lane < K2) {
+    const uint64_t me = ckey(t_trl[lane], lane);
+    int rank = 0;
+    for (int j = 0; j < K2; ++j) rank += (ckey(t_trl[j], j) > me) ? 1 : 0;
+    if (rank < k) { nxt[rank] = lane; n_rscore[rank] = t_trl[lane]; }
+  }
+  const int nm = k + K2;
+  if (lane < nm) {
+    const uint64_t me = ckey(m_score[lane], lane);
+    int rank = 0;
+    for (int j = 0; j < nm; ++j) rank += (ckey(m_score[j], j) > me) ? 1 : 0;
+    if (rank < k) msel[rank] = lane;
+  }
+  __syncthreads();
+  // 4. write the new running state
+  for (int e = lane; e < k * L; e += 64) {
+    const int i = e / L, p = e % L, j = nxt[i];
+    st.rseq[sb * L + e] = (p == cur_len) ? t_tok[j] : o_rseq[t_beam[j] * L + p];
+  }
+  for (int e = lane; e < k * Lb; e += 64) {
+    const int i = e / Lb, p = e % Lb, j = nxt[i];
+    st.rbi[sb * Lb + e] = (p == cur_len - 1) ? (int)sb + t_beam[j] : o_rbi[t_beam[j] * Lb + p];
+  }
+  if (lane < k) {
+    const int j = nxt[lane];
+    st.rscore[sb + lane] = n_rscore[lane];
+    reorder[sb + lane] = (int)sb + t_beam[j];
+    next_ids[sb + lane] = t_tok[j];
+  }
+  // 5. finished state from the merged selection
+  for (int e = lane; e < k * L; e += 64) {
+    const int i = e / L, p = e % L, mi = msel[i];
+    int v;
+    if (mi < k) v = o_seq[mi * L + p];
+    else {
+      const int j = mi - k;
+      v = (p == cur_len) ? t_tok[j] : o_rseq[t_beam[j] * L + p];
+    }
+    st.seq[sb * L + e] = v;
+  }
+  for (int e = lane; e < k * Lb; e += 64) {
+    const int i = e / Lb, p = e % Lb, mi = msel[i];
+    int v;
+    if (mi < k) v = o_bi[mi * Lb + p];
+    else {
+      const int j = mi - k;
+      v = (p == cur_len - 1) ? (int)sb + t_beam[j] : o_rbi[t_beam[j] * Lb + p];
+    }
+    st.bi[sb * Lb + e] = v;
+  }
+  __syncthreads();
+  if (lane == 0) {
+    // 6. finished scores/flags, early-stop heuristic (utils.py:3008-3053), global flags
+    float worst = 3.4e38f;
+    int all_fin = 1;
+    float nsc[BEAM_KMAX];
+    int nfin[BEAM_KMAX];
+    for (int i = 0; i < k; ++i) {
+      nsc[i] = m_score[msel[i]];
+      nfin[i] = m_fin[msel[i]];
+      st.score[sb + i] = nsc[i];
+      st.fin[sb + i] = nfin[i];
+      worst = fminf(worst, nsc[i]);
+      all_fin &= nfin[i];
+    }
+    const float best_running = n_rscore[0] / best_div;
+    int any = 0;
+    for (int i = 0; i < k; ++i) any |= best_running > (nfin[i] ? worst : -1.0e9f);
+    const int unsat_new = unsat_old && any;
+    st.unsat[b] = unsat_new;
+    int any_valid = 0;
+    for (int j = 0; j < K2; ++j) any_valid |= !t_hit[j];
+    if (unsat_new) atomicOr(&st.flags[0], 1);
+    if (!all_fin) atomicOr(&st.flags[1], 1);
+    if (any_valid) atomicOr(&st.flags[2], 1);
+  }
+}
+
+__global__ void beam_init_kernel(BeamState st, int B, int k, int L, const int64_t* prompt, int fill) {
+  const int64_t n = (int64_t)B * k * L;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int p = (int)(e % L);
+    const int b = (int)(e / ((int64_t)k * L));
+    const int v = p == 0 ? (int)prompt[b] : fill;
+    st.rseq[e] = v;
+    st.seq[e] = v;
+    const int64_t row = e / L;
+    if (p < L - 1) { st.rbi[row * (L - 1) + p] = -1; st.bi[row * (L - 1) + p] = -1; }
+    if (p == 0) {
+      st.rscore[row] = (row % k) == 0 ? 0.f : -1.0e9f;
+      st.score[row] = -1.0e9f;
+      st.fin[row] = 0;
+      if (row % k == 0) st.unsat[b] = 1;
+    }
+  }
+}
+
+__global__ void beam_finalize_kernel(BeamState st, int B, int k, int L, int64_t* sequences, float* scores,
+                                     int* beam_indices) {
+  const int64_t n = (int64_t)B * k * L;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    sequences[e] = st.seq[e];
+    const int p = (int)(e % L);
+    const int64_t row = e / L;
+    if (p < L - 1) beam_indices[row * (L - 1) + p] = st.bi[row * (L - 1) + p];
+    if (p == 0) scores[row] = st.score[row];
+  }
+}
+
+template <typename T>
+__global__ void gather_rows_kernel(int G, int R, int cols, const int* __restrict__ idx, const T* __restrict__ x,
+                                   int64_t ldx, int64_t gsx, T* __restrict__ y, int64_t ldy, int64_t gsy) {
+  const int c8 = cols / 8;
+  const int64_t n = (int64_t)G * R * c8;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % c8) * 8;
+    const int64_t gr = e / c8;
+    const int r = (int)(gr % R), g = (int)(gr / R);
+    float v[8];
+    Vec8<T>::load(x + g * gsx + (int64_t)idx[r] * ldx + c, v);
+    Vec8<T>::store(y + g * gsy + (int64_t)r * ldy + c, v);
+  }
+}
+
+static int grid_of(int64_t work) {
+  int64_t g = (work + 255) / 256;
+  return (int)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
+}
+
+}  // namespace capk
+
+using namespace capk;
+
+extern "C" size_t capk_beam_state_bytes(int B, int num_beams, int max_length) {
+  if (B <= 0 || num_beams <= 0 || max_length < 2) return 0;
+  return beam_layout(B, num_beams, max_length, nullptr, nullptr) + beam_scratch_bytes(B, num_beams);
+}
+
+static int check_dims(int B, int k, int L, const char* who) {
+  CAPK_CHECK_ARG(B > 0 && k >= 1 && k <= BEAM_KMAX && L >= 2 && L <= BEAM_LMAX, "%s: need B>0, 1<=num_beams<=%d, "
+                 "2<=max_length<=%d (got B=%d k=%d L=%d)", who, BEAM_KMAX, BEAM_LMAX, B, k, L);
+  return CAPK_OK;
+}
+
+extern "C" int capk_beam_init(int B, int num_beams, int max_length, const int64_t* prompt, int64_t fill, void* state,
+                              size_t state_bytes, void* stream) {
+  if (int rc = check_dims(B, num_beams, max_length, "capk_beam_init")) return rc;
+  CAPK_CHECK_ARG(state && prompt && state_bytes >= capk_beam_state_bytes(B, num_beams, max_length),
+                 "capk_beam_init: state buffer too small");
+  BeamState st;
+  beam_layout(B, num_beams, max_length, (char*)state, &st);
+  hipLaunchKernelGGL(beam_init_kernel, dim3(grid_of((int64_t)B * num_beams * max_length)), dim3(256), 0, S(stream),
+                     st, B, num_beams, max_length, prompt, (int)fill);
+  CAPK_LAUNCH_CHECK("beam_init_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_beam_step(int dtype, int B, int num_beams, int max_length, int V, int64_t ld, const void* logits,
+                              int cur_len, int64_t eos, float fin_div, float best_div, int early_stopping,
+                              void* state, size_t state_bytes, int32_t* reorder, int64_t* next_ids, void* stream) {
+  if (int rc = check_dims(B, num_beams, max_length, "capk_beam_step")) return rc;
+  const int k = num_beams, L = max_length;
+  CAPK_CHECK_ARG(state && state_bytes >= capk_beam_state_bytes(B, k, L), "capk_beam_step: state buffer too small");
+  CAPK_CHECK_ARG(V >= 2 * k && ld >= V && ld % 8 == 0 && cur_len >= 1 && cur_len < L && fin_div > 0.f &&
+                 best_div > 0.f && (int64_t)k * V < 0x7FFFFFFF, "capk_beam_step: bad V/ld/cur_len/penalty");
+  CAPK_CHECK_ARG(dtype == CAPK_F32 || dtype == CAPK_BF16, "capk_beam_step: dtype");
+  BeamState st;
+  const size_t sz = beam_layout(B, k, L, (char*)state, &st);
+  char* scr = (char*)state + sz;
+  const size_t Bk = (size_t)B * k;
+  float* cand_val = (float*)scr;
+  int* cand_tok = (int*)(scr + al64(Bk * 2 * k * 4));
+  float* row_max = (float*)(scr + 2 * al64(Bk * 2 * k * 4));
+  float* row_logsum = (float*)(scr + 2 * al64(Bk * 2 * k * 4) + al64(Bk * 4));
+  hipStream_t s = S(stream);
+  if (dtype == CAPK_F32)
+    hipLaunchKernelGGL(beam_rows_kernel<float>, dim3((unsigned)Bk), dim3(ROWS_THREADS), 0, s, (const float*)logits,
+                       ld, V, 2 * k, st.flags, cand_val, cand_tok, row_max, row_logsum);
+  else
+    hipLaunchKernelGGL(beam_rows_kernel<bf16>, dim3((unsigned)Bk), dim3(ROWS_THREADS), 0, s, (const bf16*)logits,
+                       ld, V, 2 * k, st.flags, cand_val, cand_tok, row_max, row_logsum);
+  CAPK_LAUNCH_CHECK("beam_rows_kernel");
+  const size_t lds = (size_t)(2 * k * L + 2 * k * (L - 1)) * sizeof(int);
+  hipLaunchKernelGGL(beam_update_kernel, dim3(B), dim3(64), lds, s, st, k, L, V, cur_len, (int)eos, fin_div,
+                     best_div, early_stopping == 1 ? 1 : 0, cand_val, cand_tok, row_max, row_logsum, reorder,
+                     next_ids);
+  CAPK_LAUNCH_CHECK("beam_update_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_beam_finalize(int B, int num_beams, int max_length, const void* state, int64_t* sequences,
+                                  float* scores, int32_t* beam_indices, void* stream) {
+  if (int rc = check_dims(B, num_beams, max_length, "capk_beam_finalize")) return rc;
+  BeamState st;
+  beam_layout(B, num_beams, max_length, (char*)state, &st);
+  hipLaunchKernelGGL(beam_finalize_kernel, dim3(grid_of((int64_t)B * num_beams * max_length)), dim3(256), 0,
+                     S(stream), st, B, num_beams, max_length, sequences, scores, beam_indices);
+  CAPK_LAUNCH_CHECK("beam_finalize_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_beam_flags(const void* state, int32_t* flags_out, void* stream) {
+  CAPK_CHECK_ARG(state && flags_out, "capk_beam_flags: null");
+  hipError_t e = hipMemcpyAsync(flags_out, state, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, S(stream));
+  if (e != hipSuccess) return hip_status(e, "capk_beam_flags");
+  e = hipStreamSynchronize(S(stream));
+  if (e != hipSuccess) return hip_status(e, "capk_beam_flags");
+  return CAPK_OK;
+}
+
+extern "C" int capk_gather_rows(int dtype, int groups, int rows, int cols, const int32_t* idx, const void* x,
+                                int64_t ldx, int64_t gsx, void* y, int64_t ldy, int64_t gsy, void* stream) {
+  CAPK_CHECK_ARG(groups > 0 && rows > 0 && cols > 0 && cols % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 &&
+                 gsx % 8 == 0 && gsy % 8 == 0, "capk_gather_rows: need cols/strides multiples of 8");
+  const int64_t work = (int64_t)groups * rows * (cols / 8);
+  if (dtype == CAPK_F32)
+    hipLaunchKernelGGL(gather_rows_kernel<float>, dim3(grid_of(work)), dim3(256), 0, S(stream), groups, rows, cols,
+                       idx, (const float*)x, ldx, gsx, (float*)y, ldy, gsy);
+  else if (dtype == CAPK_BF16)
+    hipLaunchKernelGGL(gather_rows_kernel<bf16>, dim3(grid_of(work)), dim3(256), 0, S(stream), groups, rows, cols,
+                       idx, (const bf16*)x, ldx, gsx, (bf16*)y, ldy, gsy);
+  else CAPK_CHECK_ARG(false, "capk_gather_rows: dtype");
+  CAPK_LAUNCH_CHECK("gather_rows_kernel");
+  return CAPK_OK;
+}

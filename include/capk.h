@@ -189,6 +189,40 @@ int capk_adamw(int64_t n, float* param, const float* grad, float* m, float* v,
                void* param_bf16, float lr, float weight_decay, float beta1, float beta2,
                float eps, float bc1, float bc2, void* stream);
 
+/* --------------------------------------------------- Beam search (A14) -----
+ * transformers 5.15 GenerationMixin._beam_search (generation/utils.py:3208-3535)
+ * as reached by GPT2Decoder.generate (src/models/decoders.py:645-654; SURVEY D16:
+ * the same search for every decoder).  Prompt length 1, one EOS id, MaxLength +
+ * EOS stopping.  All search state lives in one device buffer of
+ * capk_beam_state_bytes(B, num_beams, max_length) bytes (num_beams <= 8,
+ * max_length <= 256).  Per decode step the caller produces logits [B*k, ld]
+ * (V valid columns; rows b*k..b*k+k-1 are image b's beams) and calls
+ * capk_beam_step with cur_len = current sequence length (1 at the first step),
+ * fin_div = float((cur_len+1-1) ** length_penalty) and best_div = the
+ * early-stop heuristic's float(best_len ** length_penalty) (utils.py:3008-3053,
+ * 3175); early_stopping 0 = False, 1 = True, 2 = "never".  It writes the next
+ * token of every running beam (next_ids [B*k] int64) and the cache-reorder
+ * index (reorder [B*k]: row b*k+i continues from row reorder[b*k+i];
+ * utils.py:3479-3489).  capk_beam_flags copies the three batch-global flags
+ * (any improvement possible, any image with an unfinished slot, any valid
+ * continuation) to host memory and synchronises the stream; HF stops when
+ * !(f0 && !(early_stopping==True && !f1) && f2) (utils.py:3055-3075).
+ * capk_beam_finalize writes finished sequences [B,k,L] int64 (unfilled = fill),
+ * scores [B,k] and beam indices [B,k,L-1] int32 (-1 = not generated). */
+size_t capk_beam_state_bytes(int B, int num_beams, int max_length);
+int capk_beam_init(int B, int num_beams, int max_length, const int64_t* prompt, int64_t fill, void* state,
+                   size_t state_bytes, void* stream);
+int capk_beam_step(int dtype, int B, int num_beams, int max_length, int V, int64_t ld, const void* logits,
+                   int cur_len, int64_t eos, float fin_div, float best_div, int early_stopping, void* state,
+                   size_t state_bytes, int32_t* reorder, int64_t* next_ids, void* stream);
+int capk_beam_flags(const void* state, int32_t* flags_out, void* stream);
+int capk_beam_finalize(int B, int num_beams, int max_length, const void* state, int64_t* sequences,
+                       float* scores, int32_t* beam_indices, void* stream);
+/* y[g][r] = x[g][idx[r]] row gather over G groups (KV-cache reorder after a beam
+ * step, all layers in one launch; HF Cache.reorder_cache = index_select on dim 0). */
+int capk_gather_rows(int dtype, int groups, int rows, int cols, const int32_t* idx, const void* x, int64_t ldx,
+                     int64_t gsx, void* y, int64_t ldy, int64_t gsy, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -88,3 +88,14 @@ def transformer_greedy(p, features, max_length, num_layers, num_heads, bos, eos)
         if (nxt == eos).all():
             break
     return ids
+
+
+def transformer_last_logits(p, mem, ids, num_layers, num_heads):
+    """Last-position logits of the decoder re-run on the prefix ``ids`` [R, T] against
+    projected memory ``mem`` [R, S, D] (generate's per-step computation,
+    decoders.py:463-483, no pad mask) — the beam-search logits callback."""
+    T = ids.shape[1]
+    x = p["embedding.weight"][ids] + p["position_encoding.weight"][:T][None]
+    for i in range(num_layers):
+        x = decoder_layer(p, i, x, mem, num_heads, None)
+    return F.linear(x[:, -1], p["output_layer.weight"], p["output_layer.bias"])

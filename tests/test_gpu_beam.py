@@ -1,0 +1,222 @@
+"""Beam search on the GPU.
+
+* The device search (csrc/beam.hip via capk.beam.beam_search) driven by the logits of
+  the tiny GPT-2 models in tests/golden/beam_gpt2.npz reproduces HF
+  ``generate(num_beams=…)`` exactly: sequences and beam indices bit-exact, scores
+  within fp32 rounding (3 cases: k=5 bos==eos==pad; k=4 with length penalty 0.8;
+  early_stopping=True).
+* Large-vocabulary search (V = 50257, k = 5) on random fp32 logits vs oracle/beam.py
+  on the same logits: bit-exact.
+* KV-cached decode step == teacher-forced forward at every position (fp32, 1e-5).
+* Transformer decoder beam-5 (tiny golden model and the full config-3 architecture,
+  fp32) vs oracle/beam.py over the oracle decoder: sequences/beam indices bit-exact.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.beam import beam_search as oracle_beam
+
+pytestmark = pytest.mark.gpu
+cuda = pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+class HostLogits:
+    """step_fn for capk.beam.beam_search computing logits on the CPU from the running
+    sequences it reconstructs (ids + reorder), uploaded as fp32 (or bf16)."""
+
+    def __init__(self, fn, prompt_rows, dtype=torch.float32, pad_cols=0):
+        self.fn, self.seqs, self.dtype, self.pad_cols = fn, prompt_rows.clone(), dtype, pad_cols
+
+    def __call__(self, cur_len, ids, reorder):
+        ids = ids.cpu()
+        if reorder is None:
+            assert torch.equal(ids, self.seqs[:, 0])
+        else:
+            self.seqs = torch.cat([self.seqs[reorder.cpu().long()], ids[:, None]], 1)
+        assert self.seqs.shape[1] == cur_len
+        lg = self.fn(self.seqs).float()
+        if self.pad_cols:
+            lg = torch.cat([lg, torch.full((lg.shape[0], self.pad_cols), 1e4)], 1)  # must be ignored (ld > V)
+        return lg.to(self.dtype).cuda()
+
+
+def _gpt2(z, name):
+    from transformers import GPT2Config, GPT2LMHeadModel
+    cfg = GPT2Config(vocab_size=61, n_positions=32, n_embd=32, n_layer=2, n_head=2, resid_pdrop=0.0, embd_pdrop=0.0,
+                     attn_pdrop=0.0, bos_token_id=0, eos_token_id=7)
+    m = GPT2LMHeadModel(cfg).eval()
+    pre = f"{name}/w/"
+    m.load_state_dict({k[len(pre):]: torch.from_numpy(z[k]) for k in z.files if k.startswith(pre)}, strict=False)
+    return m
+
+
+@cuda
+@pytest.mark.parametrize("name", ["ref_like_k5", "eos_k4_lp08", "eos_k5_es"])
+def test_device_beam_matches_hf_generate(name):
+    from capk.beam import beam_search
+    z = np.load(os.path.join(GOLD, "beam_gpt2.npz"))
+    B, k, L, bos, eos, es = (int(v) for v in z[f"{name}/args"])
+    lp = float(z[f"{name}/length_penalty"])
+    m = _gpt2(z, name)
+    prompt = torch.from_numpy(z[f"{name}/input_ids"])[:, 0]
+
+    def fn(seqs):
+        with torch.no_grad():
+            return m(input_ids=seqs).logits[:, -1, :]
+
+    step = HostLogits(fn, prompt.repeat_interleave(k)[:, None], pad_cols=3)
+    out = beam_search(step, B, k, L, prompt.cuda(), eos, pad_token_id=eos, length_penalty=lp,
+                      early_stopping=bool(es), vocab_size=61)
+    np.testing.assert_array_equal(out["sequences"].cpu().numpy(), z[f"{name}/sequences"])
+    np.testing.assert_array_equal(out["beam_indices"].cpu().numpy(), z[f"{name}/beam_indices"])
+    np.testing.assert_allclose(out["sequences_scores"].cpu().numpy(), z[f"{name}/sequences_scores"], rtol=1e-5,
+                               atol=1e-6)
+
+
+@cuda
+@pytest.mark.parametrize("early_stopping,lp", [(False, 1.0), ("never", 0.8), (True, 1.2)])
+def test_device_beam_large_vocab_vs_oracle(early_stopping, lp):
+    """V = 50257, k = 5, B = 6, max_length 12, EOS = 50256 made likely; logits are a
+    deterministic function of (last token, length) so both searches see identical inputs."""
+    from capk.beam import beam_search
+    V, B, k, L, eos = 50257, 6, 5, 12, 50256
+    g = torch.Generator().manual_seed(3)
+    table = torch.randn(V, 64, generator=g)
+    proj = torch.randn(64, V, generator=g) * 0.6
+    proj[:, eos] += 0.35
+
+    def fn(seqs):
+        h = table[seqs[:, -1]] + 0.1 * seqs.shape[1] + 0.01 * table[seqs[:, 0]]
+        return h @ proj
+
+    prompt = torch.tensor([50256, 11, 400, 9000, 50000, 7])
+    ref = oracle_beam(fn, B, k, L, bos=None, eos=eos, pad=eos, length_penalty=lp, early_stopping=early_stopping,
+                      prompt=prompt[:, None])
+    step = HostLogits(fn, prompt.repeat_interleave(k)[:, None], pad_cols=47)
+    out = beam_search(step, B, k, L, prompt.cuda(), eos, pad_token_id=eos, length_penalty=lp,
+                      early_stopping=early_stopping, vocab_size=V)
+    assert torch.equal(out["sequences"].cpu(), ref["sequences"])
+    assert torch.equal(out["beam_indices"].cpu(), ref["beam_indices"])
+    torch.testing.assert_close(out["sequences_scores"].cpu(), ref["sequences_scores"], rtol=1e-5, atol=1e-5)
+    fin = ref["is_sent_finished"]
+    got_all = out["all_sequences"].cpu()
+    assert torch.equal(got_all[fin], ref["all_sequences"][fin])  # every real finished hypothesis
+
+
+@cuda
+def test_device_beam_bf16_logits_runs():
+    """bf16 logits (the throughput path): same search on bf16-rounded logits; the oracle
+    sees the same rounded values in fp32.  bf16 rounding creates exact ties, whose order
+    torch.topk leaves unspecified, so this checks the best score and that >= 5/6 of the
+    best sequences agree."""
+    from capk.beam import beam_search
+    V, B, k, L, eos = 50257, 6, 5, 10, 50256
+    g = torch.Generator().manual_seed(4)
+    table = torch.randn(V, 32, generator=g)
+    proj = torch.randn(32, V, generator=g)
+
+    def fn(seqs):
+        return (table[seqs[:, -1]] @ proj).bfloat16().float()
+
+    prompt = torch.arange(B) * 1000
+    ref = oracle_beam(fn, B, k, L, bos=None, eos=eos, pad=eos, prompt=prompt[:, None])
+    step = HostLogits(fn, prompt.repeat_interleave(k)[:, None], dtype=torch.bfloat16, pad_cols=47)
+    out = beam_search(step, B, k, L, prompt.cuda(), eos, pad_token_id=eos, vocab_size=V)
+    torch.testing.assert_close(out["sequences_scores"].cpu(), ref["sequences_scores"], rtol=1e-4, atol=1e-4)
+    n = min(out["sequences"].shape[1], ref["sequences"].shape[1])
+    same = (out["sequences"].cpu()[:, :n] == ref["sequences"][:, :n]).all(1).float().mean()
+    assert same >= 5 / 6
+
+
+@cuda
+def test_gather_rows_kernel():
+    from capk import ops
+    x = torch.randn(3, 10, 7, 24, device="cuda")
+    y = torch.zeros_like(x)
+    idx = torch.tensor([3, 3, 0, 9, 1, 2, 5, 5, 8, 4], dtype=torch.int32, device="cuda")
+    t = 4
+    ops.check(ops.lib().capk_gather_rows(ops.F32, 3, 10, t * 24, idx.data_ptr(), x.data_ptr(), 7 * 24, 10 * 7 * 24,
+                                         y.data_ptr(), 7 * 24, 10 * 7 * 24, ops._stream()), "gather")
+    assert torch.equal(y[:, :, :t], x[:, idx.long(), :t])
+    assert float(y[:, :, t:].abs().max()) == 0.0
+
+
+def _tiny(precision="fp32"):
+    from test_gpu_model import _tiny_model
+    z = np.load(os.path.join(GOLD, "vit_transformer_step.npz"), allow_pickle=False)
+    model, store, cfg = _tiny_model(z, precision)
+    return z, model, cfg
+
+
+@cuda
+def test_kv_decode_step_matches_forward_fp32():
+    """Feeding a fixed caption one token at a time through the KV cache (identity
+    reorder) gives the teacher-forced logits at every position."""
+    from capk.models.transformer import KVDecodeRunner
+    z, model, cfg = _tiny()
+    images = torch.from_numpy(z["in/images"]).cuda()
+    B = images.shape[0]
+    k = 2
+    caps = torch.randint(0, 60, (B * k, 6), generator=torch.Generator().manual_seed(5)).cuda()
+    with torch.no_grad():
+        enc = model.encoder(images)
+        feats = enc["features"]
+        rep = feats.repeat_interleave(k, 0).contiguous()
+        ref, _ = model.decoder.forward_logits(rep, caps, use_pad_mask=False)
+        run = KVDecodeRunner(model.decoder, feats, k, 6)
+        ident = torch.arange(B * k, dtype=torch.int32, device="cuda")
+        for t in range(6):
+            lg = run.step(t + 1, caps[:, t].contiguous(), ident if t else None)[:, :cfg.model.vocab_size]
+            torch.testing.assert_close(lg, ref[:, t], rtol=1e-5, atol=1e-5)
+
+
+def _oracle_decoder_beam(sd, feats_cpu, k, L, bos, eos, pad, nl, nh, **kw):
+    import torch.nn.functional as F
+    from oracle import decoders as odec
+    p = {kk[len("decoder."):]: v for kk, v in sd.items() if kk.startswith("decoder.")}
+    B = feats_cpu.shape[0]
+    mem = F.linear(feats_cpu, p["visual_projection.weight"], p["visual_projection.bias"]).repeat_interleave(k, 0)
+
+    def fn(seqs):
+        with torch.no_grad():
+            return odec.transformer_last_logits(p, mem, seqs, nl, nh)
+
+    return oracle_beam(fn, B, k, L, bos=bos, eos=eos, pad=pad, **kw)
+
+
+@cuda
+def test_transformer_beam5_tiny_vs_oracle_fp32():
+    z, model, cfg = _tiny()
+    images = torch.from_numpy(z["in/images"]).cuda()
+    pad = cfg.model.pad_token_id
+    with torch.no_grad():
+        feats = model.encoder(images)["features"]
+        ids, info = model.decoder.generate({"features": feats}, max_length=9, num_beams=5)
+    sd = {k: v.detach().cpu().float() for k, v in model.state_dict().items()}
+    ref = _oracle_decoder_beam(sd, feats.float().cpu(), 5, 9, pad, pad, pad, int(z["meta/dims"][3]),
+                               int(z["meta/dims"][4]))
+    assert torch.equal(ids.cpu(), ref["sequences"])
+    assert torch.equal(info["beam_indices"].cpu(), ref["beam_indices"])
+    torch.testing.assert_close(info["sequences_scores"].cpu(), ref["sequences_scores"], rtol=1e-4, atol=1e-5)
+
+
+@cuda
+def test_transformer_beam5_config3_fp32_vs_oracle():
+    """Full config-3 model (ViT-B/16 + 6L/8H decoder, V = 50257), fp32, beam-5,
+    max_length 20 (InferenceConfig): beam indices bit-exact vs the CPU reference path."""
+    from test_gpu_model import _full_model
+    from oracle import encoders as oenc
+    model, store, cfg, sd = _full_model("fp32")
+    images = torch.randn(2, 3, 224, 224, generator=torch.Generator().manual_seed(0))
+    with torch.no_grad():
+        ids, info = model.generate(images=images.cuda(), max_length=20, num_beams=5)
+        enc = oenc.vit_encoder({k[len("encoder.model."):]: v for k, v in sd.items() if k.startswith("encoder.model.")},
+                               images, 12, 12, 16)
+    ref = _oracle_decoder_beam(sd, enc["features"], 5, 20, 50256, 50256, 50256, 6, 8)
+    assert torch.equal(ids.cpu(), ref["sequences"])
+    assert torch.equal(info["beam_indices"].cpu(), ref["beam_indices"])
+    torch.testing.assert_close(info["sequences_scores"].cpu(), ref["sequences_scores"], rtol=1e-4, atol=1e-4)
