@@ -26,6 +26,31 @@ import torch.distributed as dist  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
 FLOP_PER_IMAGE = 120.7e9  # config-3 fwd+bwd algorithmic FLOPs per image
+FLOP_PER_CAPTION = 54e9   # beam-5 caption (ViT fwd + memory K/V + 19 KV-cached steps x 5 beams)
+
+
+def beam_bench(model, batch, reps, device, rank):
+    """Beam-5 captions/s (second half of BASELINE's metric): encoder forward + KV-cached
+    beam-5 decode, max_length 20 (InferenceConfig), HF beam semantics, bf16, batch images
+    resident in HBM.  Random-init weights never emit EOS early, so every batch runs the
+    full 19 decode steps (worst case)."""
+    from capk import ops
+    model.eval()
+    g = torch.Generator(device=device).manual_seed(7 + 1000 * rank)
+    images = torch.randn(batch, 3, 224, 224, device=device, generator=g)
+    with torch.no_grad():
+        model.generate(images=images, max_length=20, num_beams=5)
+        torch.cuda.synchronize()
+        ops.GEMM_TIMER.start()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            ids, info = model.generate(images=images, max_length=20, num_beams=5)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        ops.GEMM_TIMER.stop()
+    gem = ops.GEMM_TIMER.summary()
+    model.train()
+    return dt, gem, int(ids.shape[1])
 
 
 def build(batch, device):
@@ -57,6 +82,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=4)
     ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--beam-batch", type=int, default=256, help="images per beam-5 batch (0 = skip)")
+    ap.add_argument("--beam-reps", type=int, default=3)
+    ap.add_argument("--cpu-beam-images", type=int, default=4)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -116,6 +144,14 @@ def main():
         elapsed = float(t)
     gem = ops.GEMM_TIMER.summary()
     final_loss = float(loss)
+    beam = None
+    if args.beam_batch > 0:
+        bdt, bgem, blen = beam_bench(model, args.beam_batch, args.beam_reps, device, rank)
+        if world > 1:
+            t = torch.tensor([bdt], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            bdt = float(t)
+        beam = (bdt, bgem, blen)
 
     if rank == 0:
         ms = elapsed / args.steps * 1e3
@@ -147,6 +183,29 @@ def main():
                             "frac_of_peak": round(FLOP_PER_IMAGE * value / world / 1e12 / PEAK_BF16_TFLOPS, 4)},
             "final_loss": round(final_loss, 4),
         }
+        if beam is not None:
+            bdt, bgem, blen = beam
+            cps = args.beam_batch * world * args.beam_reps / bdt
+            bach = bgem["flops"] / (bgem["total_ms"] * 1e-3) / 1e12 if bgem["launches"] else 0.0
+            rec["beam5"] = {"metric": "beam-5 captions/sec", "value": round(cps, 2), "unit": "captions/s",
+                            "per_gpu_batch": args.beam_batch, "reps": args.beam_reps,
+                            "ms_per_batch": round(bdt / args.beam_reps * 1e3, 3), "num_beams": 5, "max_length": 20,
+                            "output_length": blen, "dtype": "bf16",
+                            "workload": "ViT-B/16 encoder fwd + KV-cached Transformer beam-5 decode (HF semantics)",
+                            "roofline": {"bound": "mfma", "kernel": "gemm_bf16_kernel (all GEMM launches)",
+                                         "achieved": round(bach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                                         "frac": round(bach / PEAK_BF16_TFLOPS, 4),
+                                         "gemm_share": round(bgem["total_ms"] / (bdt * 1e3), 3)},
+                            "model_flops": {"per_caption": FLOP_PER_CAPTION,
+                                            "tflops": round(FLOP_PER_CAPTION * cps / world / 1e12, 1)}}
+            if world == 1 and not args.no_cpu_baseline:
+                from oracle.step import time_cpu_beam
+                threads = min(16, os.cpu_count() or 1)
+                cps_cpu, cdt = time_cpu_beam(cpu_sd, images=args.cpu_beam_images, threads=threads)
+                rec["beam5"]["cpu_baseline"] = {
+                    "value": round(cps_cpu, 3), "unit": "captions/s", "cores": threads, "kind": "port",
+                    "sample": f"oracle fp32 CPU: ViT fwd + beam-5 (oracle/beam.py) re-running the decoder on each "
+                              f"prefix, {args.cpu_beam_images} images, max_length 20 ({cdt:.1f} s)"}
         if world == 1 and not args.no_cpu_baseline:
             from oracle.step import time_cpu_baseline
             threads = min(16, os.cpu_count() or 1)

@@ -90,8 +90,31 @@ class ViTLayer(CapkModule):
         self.layernorm_after = nn.LayerNorm(d, eps=self.eps)
         self.mlp = _MLP(d, a["intermediate_size"])
 
+    act = ACT_GELU_ERF  # ViTIntermediate: hidden_act "gelu" (exact erf)
+
+    # role accessors shared with the CLIP layer (clip.py), which has other names
+    @property
+    def ln1(self):
+        return self.layernorm_before
+
+    @property
+    def ln2(self):
+        return self.layernorm_after
+
+    @property
+    def attn(self):
+        return self.attention
+
+    @property
+    def fc1(self):
+        return self.mlp.fc1
+
+    @property
+    def fc2(self):
+        return self.mlp.fc2
+
     def forward(self, x, B, N):
-        return _ViTLayerFn.apply(x, self.attention.o_proj.weight, self, B, N)
+        return _ViTLayerFn.apply(x, self.attn.o_proj.weight, self, B, N)
 
 
 class _Pooler(nn.Module):
@@ -176,7 +199,9 @@ class _ViTEmbedFn(torch.autograd.Function):
 
 
 class _ViTLayerFn(torch.autograd.Function):
-    """ViTLayer.forward (modeling_vit.py:266-286), pre-LN."""
+    """Pre-LN encoder layer: ViTLayer.forward (modeling_vit.py:266-286) and, with the
+    CLIP layer's accessors and quick_gelu, CLIPEncoderLayer.forward
+    (modeling_clip.py:355-395)."""
 
     @staticmethod
     def forward(ctx, x, anchor, L, B, N):
@@ -184,8 +209,8 @@ class _ViTLayerFn(torch.autograd.Function):
         D = x.shape[1]
         H = L.num_heads
         hd = D // H
-        at, mlp = L.attention, L.mlp
-        ln1, ln2 = L.layernorm_before, L.layernorm_after
+        at, fc1, fc2, act = L.attn, L.fc1, L.fc2, L.act
+        ln1, ln2 = L.ln1, L.ln2
         h1, mu1, rs1 = ops.layernorm_fwd(x, ln1.weight.detach(), ln1.bias.detach(), L.eps)
         qkv = ops.linear(h1, at.qkv_w.w(dt), at.qkv_b.master)
         o = torch.empty(x.shape[0], D, dtype=x.dtype, device=x.device)
@@ -193,10 +218,10 @@ class _ViTLayerFn(torch.autograd.Function):
                                    heads(o, 0, B, N), B, H, N, N, hd, 1.0 / math.sqrt(hd))
         x1 = ops.linear(o, W(at.o_proj.weight, dt), at.o_proj.bias.detach(), residual=x)
         h2, mu2, rs2 = ops.layernorm_fwd(x1, ln2.weight.detach(), ln2.bias.detach(), L.eps)
-        I = mlp.fc1.weight.shape[0]
+        I = fc1.weight.shape[0]
         f_pre = torch.empty(x.shape[0], I, dtype=x.dtype, device=x.device)
-        f = ops.linear(h2, W(mlp.fc1.weight, dt), mlp.fc1.bias.detach(), act=ACT_GELU_ERF, preact=f_pre)
-        y = ops.linear(f, W(mlp.fc2.weight, dt), mlp.fc2.bias.detach(), residual=x1)
+        f = ops.linear(h2, W(fc1.weight, dt), fc1.bias.detach(), act=act, preact=f_pre)
+        y = ops.linear(f, W(fc2.weight, dt), fc2.bias.detach(), residual=x1)
         ctx.L, ctx.B, ctx.N = L, B, N
         ctx.saved = (x, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, f_pre, f)
         return y
@@ -211,10 +236,10 @@ class _ViTLayerFn(torch.autograd.Function):
         D = x.shape[1]
         H = L.num_heads
         hd = D // H
-        at, mlp = L.attention, L.mlp
-        ln1, ln2 = L.layernorm_before, L.layernorm_after
-        dfp = linear_bwd(dy, f, mlp.fc2.weight, mlp.fc2.bias, dt, act_bwd=ACT_GELU_ERF, aux=f_pre)
-        dh2 = linear_bwd(dfp, h2, mlp.fc1.weight, mlp.fc1.bias, dt)
+        at, fc1, fc2, act = L.attn, L.fc1, L.fc2, L.act
+        ln1, ln2 = L.ln1, L.ln2
+        dfp = linear_bwd(dy, f, fc2.weight, fc2.bias, dt, act_bwd=act, aux=f_pre)
+        dh2 = linear_bwd(dfp, h2, fc1.weight, fc1.bias, dt)
         dx1 = ops.layernorm_bwd(dh2, x1, ln2.weight.detach(), mu2, rs2, G(ln2.weight), G(ln2.bias), dres=dy)
         do = linear_bwd(dx1, o, at.o_proj.weight, at.o_proj.bias, dt)
         dqkv = torch.empty_like(qkv)

@@ -506,6 +506,132 @@ static int launch_dyn(K kernel, dim3 grid, dim3 block, size_t shm, hipStream_t s
   return CAPK_OK;
 }
 
+
+// ------------------------------------------------------------ decode (small Nq) ---
+// Incremental-decode attention (KV-cached beam / greedy steps): Nq <= 8 queries per
+// (batch, head) — one new token per beam for self-attention, or the k beams of one
+// image against its shared memory keys for cross-attention.  HBM-bound on the K/V
+// stream, so VALU (fp32) instead of MFMA: 16 lanes own one key row (8 dims each,
+// 16-B loads, a 192-B contiguous row segment at hd 96), 4 keys per wave, 16 per
+// block iteration; scores go to LDS, softmax per query by one wave, then P·V with
+// the same key ownership and a cross-wave LDS reduction.  No dropout / causal
+// (decode never needs either); key padding honoured.
+template <int NQ>
+__global__ __launch_bounds__(256) void attn_decode_bf16(AttnArgs a) {
+  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, grp = lane >> 4, c = lane & 15;
+  const bool act = c * 8 < a.hd;
+  const int hoff = h * a.hd + c * 8;
+  __shared__ float sc[NQ][257];
+  __shared__ float red[4][NQ][128];
+  __shared__ float inv_l[NQ];
+  const float qs = a.scale * kLog2e;
+  float qv[NQ][8];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    bf16x8 t = (act && q < a.Nq) ? ld8((const bf16*)a.q + (int64_t)b * a.q_bs + (int64_t)q * a.q_rs + hoff) : zero8();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) qv[q][i] = (float)t[i] * qs;
+  }
+  const bf16* kb = (const bf16*)a.k + (int64_t)b * a.k_bs + hoff;
+  const bf16* vb = (const bf16*)a.v + (int64_t)b * a.v_bs + hoff;
+  // phase 1: scores (log2 domain).  Every K and V row segment this lane will touch is
+  // requested up front (<= 16 keys per lane at Nk <= 256) so the whole block's K/V
+  // stream is in flight at once instead of one dependent load per loop trip.
+  constexpr int KIT = 16;
+  bf16x8 kr[KIT], vr[KIT];
+  const int j0 = w * 4 + grp;
+#pragma unroll
+  for (int it = 0; it < KIT; ++it) {
+    const int j = j0 + 16 * it;
+    kr[it] = (act && j < a.Nk) ? ld8(kb + (int64_t)j * a.k_rs) : zero8();
+  }
+#pragma unroll
+  for (int it = 0; it < KIT; ++it) {
+    const int j = j0 + 16 * it;
+    vr[it] = (act && j < a.Nk) ? ld8(vb + (int64_t)j * a.v_rs) : zero8();
+  }
+#pragma unroll
+  for (int it = 0; it < KIT; ++it) {
+    const int j = j0 + 16 * it;
+    if (16 * it >= a.Nk) break;
+    float kf[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) kf[i] = (float)kr[it][i];
+    const bool ok = j < a.Nk && (!a.key_pad || !a.key_pad[(int64_t)b * a.Nk + j]);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      float d = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d = fmaf(qv[q][i], kf[i], d);
+      d += __shfl_xor(d, 8, 64);
+      d += __shfl_xor(d, 4, 64);
+      d += __shfl_xor(d, 2, 64);
+      d += __shfl_xor(d, 1, 64);
+      if (c == 0 && j < a.Nk) sc[q][j] = ok ? d : -INFINITY;
+    }
+  }
+  __syncthreads();
+  // phase 2: softmax per query (wave w owns queries w, w+4)
+  for (int q = w; q < a.Nq; q += 4) {
+    float m = -INFINITY;
+    for (int j = lane; j < a.Nk; j += 64) m = fmaxf(m, sc[q][j]);
+    m = wave_max(m);
+    float l = 0.f;
+    for (int j = lane; j < a.Nk; j += 64) {
+      const float p = (m == -INFINITY) ? 0.f : exp2f(sc[q][j] - m);
+      sc[q][j] = p;
+      l += p;
+    }
+    l = wave_sum(l);
+    if (lane == 0) {
+      inv_l[q] = l > 0.f ? 1.f / l : 0.f;
+      a.lse[((int64_t)b * a.H + h) * a.Nq + q] = l > 0.f ? (m + __log2f(l)) * kLn2 : -INFINITY;
+    }
+  }
+  __syncthreads();
+  // phase 3: O = P V
+  float acc[NQ][8];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[q][i] = 0.f;
+#pragma unroll
+  for (int it = 0; it < KIT; ++it) {
+    const int j = j0 + 16 * it;
+    if (16 * it >= a.Nk) break;
+    if (j < a.Nk) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const float p = sc[q][j];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[q][i] = fmaf(p, (float)vr[it][i], acc[q][i]);
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float x = acc[q][i];
+      x += __shfl_xor(x, 16, 64);
+      x += __shfl_xor(x, 32, 64);
+      acc[q][i] = x;
+    }
+  if (grp == 0 && act) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) red[w][q][c * 8 + i] = acc[q][i];
+  }
+  __syncthreads();
+  for (int e = tid; e < a.Nq * a.hd; e += 256) {
+    const int q = e / a.hd, d = e % a.hd;
+    const float o = (red[0][q][d] + red[1][q][d] + red[2][q][d] + red[3][q][d]) * inv_l[q];
+    ((bf16*)a.out)[(int64_t)b * a.out_bs + (int64_t)q * a.out_rs + h * a.hd + d] = (bf16)o;
+  }
+}
+
 static int hdp_of(int hd) { return hd <= 32 ? 32 : hd <= 64 ? 64 : hd <= 96 ? 96 : 128; }
 
 static int check_common(int dtype, int B, int H, int Nq, int Nk, int hd) {
@@ -553,6 +679,21 @@ extern "C" int capk_attention_fwd(int dtype, int B, int H, int Nq, int Nk, int h
   CAPK_CHECK_ARG(q_rs % 8 == 0 && k_rs % 8 == 0 && v_rs % 8 == 0 && o_rs % 4 == 0 && q_bs % 8 == 0 &&
                      k_bs % 8 == 0 && v_bs % 8 == 0,
                  "capk_attention_fwd(bf16): strides must allow 16-B vector access");
+  if (Nq <= 8 && !causal && !(drop_p > 0.f)) {
+    const dim3 g(B * H), blk(256);
+    switch (Nq) {
+      case 1: hipLaunchKernelGGL(attn_decode_bf16<1>, g, blk, 0, st, a); break;
+      case 2: hipLaunchKernelGGL(attn_decode_bf16<2>, g, blk, 0, st, a); break;
+      case 3: hipLaunchKernelGGL(attn_decode_bf16<3>, g, blk, 0, st, a); break;
+      case 4: hipLaunchKernelGGL(attn_decode_bf16<4>, g, blk, 0, st, a); break;
+      case 5: hipLaunchKernelGGL(attn_decode_bf16<5>, g, blk, 0, st, a); break;
+      case 6: hipLaunchKernelGGL(attn_decode_bf16<6>, g, blk, 0, st, a); break;
+      case 7: hipLaunchKernelGGL(attn_decode_bf16<7>, g, blk, 0, st, a); break;
+      default: hipLaunchKernelGGL(attn_decode_bf16<8>, g, blk, 0, st, a); break;
+    }
+    CAPK_LAUNCH_CHECK("attn_decode_bf16");
+    return CAPK_OK;
+  }
   const int hdp = hdp_of(hd);
   const size_t shm = fwd_smem(Nk, hdp);
   const dim3 grid(B * H), block(512);

@@ -104,6 +104,36 @@ __device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2
   else s += s2 * __expf(m2 - m);
 }
 
+// Per-wave candidate filter: a wave streams 512 contiguous logits per iteration (8 per
+// lane, 16-B loads); an element enters the wave's LDS candidate buffer only if its
+// (value, -index) key is >= the wave threshold (the K2-th best key seen so far), which
+// makes appends rare after the first chunk; the buffer is compacted to its K2 best
+// (rank counting) when it could overflow.  All control flow on the filter is
+// wave-uniform (ballots), so there is no per-lane insertion divergence.
+static constexpr int WAVE_CAP = 128;
+
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l), hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// keep the K2 best of wb[0..cnt) in wb[0..K2) sorted descending; returns new count
+__device__ __forceinline__ int wave_compact(uint64_t* wb, int cnt, int K2, int lane) {
+  const uint64_t a0 = lane < cnt ? wb[lane] : 0, a1 = lane + 64 < cnt ? wb[lane + 64] : 0;
+  int r0 = 0, r1 = 0;
+  for (int e = 0; e < cnt; ++e) {
+    const uint64_t x = wb[e];
+    r0 += x > a0;
+    r1 += x > a1;
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (a0 && r0 < K2) wb[r0] = a0;
+  if (a1 && r1 < K2) wb[r1] = a1;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  return cnt < K2 ? cnt : K2;
+}
+
 template <typename T>
 __global__ __launch_bounds__(ROWS_THREADS) void beam_rows_kernel(const T* __restrict__ logits, int64_t ld, int V,
                                                                  int K2, int* flags, float* cand_val, int* cand_tok,
@@ -111,70 +141,89 @@ __global__ __launch_bounds__(ROWS_THREADS) void beam_rows_kernel(const T* __rest
   const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (r == 0 && tid < 4) flags[tid] = 0;
   const T* x = logits + (int64_t)r * ld;
-  uint64_t keys[BEAM_K2MAX];
-#pragma unroll
-  for (int j = 0; j < BEAM_K2MAX; ++j) keys[j] = 0;
+  __shared__ uint64_t wbuf[4][WAVE_CAP];
+  __shared__ float sm[4], ss[4];
+  uint64_t* wb = wbuf[w];
   float m = -INFINITY, s = 0.f;
-  auto insert = [&](uint64_t key) {
-    if (key <= keys[BEAM_K2MAX - 1]) return;
-#pragma unroll
-    for (int j = BEAM_K2MAX - 1; j > 0; --j) {
-      const uint64_t a = keys[j - 1], b = keys[j];
-      keys[j] = key > a ? a : (key > b ? key : b);
+  uint64_t thr = 0;
+  int cnt = 0;
+  auto offer = [&](uint64_t key) {  // wave-uniform call
+    bool p = key != 0 && key >= thr;
+    uint64_t mask = __ballot(p);
+    if (!mask) return;
+    if (cnt + 64 > WAVE_CAP) {
+      cnt = wave_compact(wb, cnt, K2, lane);
+      if (cnt == K2) thr = wb[K2 - 1];
+      p = key != 0 && key >= thr;
+      mask = __ballot(p);
+      if (!mask) return;
     }
-    keys[0] = key > keys[0] ? key : keys[0];
+    if (p) wb[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0))] = key;
+    cnt += __popcll(mask);
   };
   const int V8 = V & ~7;
-  for (int i = tid * 8; i < V8; i += ROWS_THREADS * 8) {
+  bool first = true;
+  for (int c0 = w * 512; c0 < V8; c0 += 4 * 512) {
+    const int i = c0 + lane * 8;
+    const bool valid = i < V8;
     float v[8];
-    Vec8<T>::load(x + i, v);
+    if (valid) Vec8<T>::load(x + i, v);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = -INFINITY;
+    }
     float cm = v[0];
 #pragma unroll
     for (int j = 1; j < 8; ++j) cm = fmaxf(cm, v[j]);
-    if (cm > m) { s = (m == -INFINITY) ? 0.f : s * __expf(m - cm); m = cm; }
+    if (valid) {
+      if (cm > m) { s = (m == -INFINITY) ? 0.f : s * __expf(m - cm); m = cm; }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      s += __expf(v[j] - m);
-      insert(ckey(v[j], i + j));
+      for (int j = 0; j < 8; ++j) s += __expf(v[j] - m);
     }
+    if (first) {  // threshold from the K2-th best lane maximum of the first chunk
+      first = false;
+      uint64_t km = 0;
+      if (valid) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { const uint64_t kk = ckey(v[j], i + j); km = kk > km ? kk : km; }
+      }
+      int rank = 0;
+      for (int o = 0; o < 64; ++o) rank += readlane_u64(km, o) > km;
+      const uint64_t ball = __ballot(km != 0 && rank == K2 - 1);
+      thr = ball ? readlane_u64(km, __builtin_ctzll(ball)) : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) offer(valid ? ckey(v[j], i + j) : 0);
   }
-  for (int i = V8 + tid; i < V; i += ROWS_THREADS) {
-    const float v = to_f32(x[i]);
-    if (v > m) { s = (m == -INFINITY) ? 0.f : s * __expf(m - v); m = v; }
-    s += __expf(v - m);
-    insert(ckey(v, i));
+  for (int t0 = V8 + w * 64; t0 < V; t0 += 256) {  // tail (< 8 elements, one wave-uniform pass)
+    const int i = t0 + lane;
+    uint64_t key = 0;
+    if (i < V) {
+      const float v = to_f32(x[i]);
+      if (v > m) { s = (m == -INFINITY) ? 0.f : s * __expf(m - v); m = v; }
+      s += __expf(v - m);
+      key = ckey(v, i);
+    }
+    offer(key);
   }
+  cnt = wave_compact(wb, cnt, K2, lane);
+  for (int j = cnt + lane; j < K2; j += 64) wb[j] = 0;
   // log-sum-exp statistics: wave, then block
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
     lse_merge(m, s, m2, s2);
   }
-  __shared__ float sm[4], ss[4];
-  __shared__ uint64_t wk[4][BEAM_K2MAX];
   if (lane == 0) { sm[w] = m; ss[w] = s; }
-  // wave top-K2: K2 rounds of wave argmax over each lane's sorted list head
-  for (int j = 0; j < K2; ++j) {
-    const uint64_t best = wave_max_u64(keys[0]);
-    if (keys[0] == best && best != 0) {
-#pragma unroll
-      for (int t = 0; t < BEAM_K2MAX - 1; ++t) keys[t] = keys[t + 1];
-      keys[BEAM_K2MAX - 1] = 0;
-    }
-    if (lane == 0) wk[w][j] = best;
-  }
   __syncthreads();
   if (w == 0) {
     float M = sm[0], Ssum = ss[0];
     for (int q = 1; q < 4; ++q) lse_merge(M, Ssum, sm[q], ss[q]);
     // final top-K2 of the 4*K2 wave candidates by rank counting
     const int nc = 4 * K2;
-    uint64_t mine = lane < nc ? wk[lane / K2][lane % K2] : 0;
+    uint64_t mine = lane < nc ? wbuf[lane / K2][lane % K2] : 0;
     int rank = 0;
-    for (int c = 0; c < nc; ++c) {
-      const uint64_t o = wk[c / K2][c % K2];
-      rank += (o > mine) ? 1 : 0;
-    }
+    for (int c = 0; c < nc; ++c) rank += wbuf[c / K2][c % K2] > mine;
     if (lane < nc && rank < K2 && mine != 0) {
       cand_val[(int64_t)r * K2 + rank] = funkey((uint32_t)(mine >> 32));
       cand_tok[(int64_t)r * K2 + rank] = (int)(0xFFFFFFFFu - (uint32_t)mine);

@@ -99,3 +99,43 @@ def transformer_last_logits(p, mem, ids, num_layers, num_heads):
     for i in range(num_layers):
         x = decoder_layer(p, i, x, mem, num_heads, None)
     return F.linear(x[:, -1], p["output_layer.weight"], p["output_layer.bias"])
+
+
+def _gelu_new(x):
+    return 0.5 * x * (1.0 + torch.tanh(math.sqrt(2.0 / math.pi) * (x + 0.044715 * torch.pow(x, 3.0))))
+
+
+def gpt2_decoder(p, pooled, captions, num_layers, num_heads, pad_token_id, prefix_len=10, eps=1e-5):
+    """GPT2Decoder.forward (src/models/decoders.py:554-595) with the SURVEY D7
+    restatement: prefix P = image_to_prefix(pooled).view(B,10,D); every layer's past
+    K = V = P split into heads (decoders.py:597-617 intent); attention mask =
+    cat(ones(B,10), captions != pad); caption positions 10..10+T-1
+    (modeling_gpt2.py:569-574).  GPT2Block (246-300): x += c_proj(attn(ln_1 x));
+    x += mlp(ln_2 x) with Conv1D (y = x W + b, W [in, out]) and gelu_new; ln_f;
+    LM head tied to wte (698).  Parameter names: the GPT2Decoder state dict minus
+    ``decoder.``."""
+    B, T = captions.shape
+    D = p["model.transformer.wte.weight"].shape[1]
+    H, hd = num_heads, D // num_heads
+    P = F.linear(pooled, p["image_to_prefix.weight"], p["image_to_prefix.bias"]).view(B, prefix_len, D)
+    pk = P.view(B, prefix_len, H, hd).transpose(1, 2)
+    x = p["model.transformer.wte.weight"][captions] + p["model.transformer.wpe.weight"][prefix_len:prefix_len + T][None]
+    keep = torch.cat([torch.ones(B, prefix_len, dtype=torch.bool), captions != pad_token_id], 1)
+    causal = torch.ones(T, prefix_len + T, dtype=torch.bool).tril(prefix_len)
+    allowed = keep[:, None, None, :] & causal[None, None]
+    for i in range(num_layers):
+        pre = f"model.transformer.h.{i}."
+        h = F.layer_norm(x, (D,), p[pre + "ln_1.weight"], p[pre + "ln_1.bias"], eps)
+        qkv = h @ p[pre + "attn.c_attn.weight"] + p[pre + "attn.c_attn.bias"]
+        q, k, v = (t.view(B, T, H, hd).transpose(1, 2) for t in qkv.split(D, dim=2))
+        k = torch.cat([pk, k], 2)
+        v = torch.cat([pk, v], 2)
+        s = torch.matmul(q, k.transpose(-1, -2)) / math.sqrt(hd)
+        s = s.masked_fill(~allowed, float("-inf"))
+        o = torch.matmul(torch.softmax(s, -1), v).transpose(1, 2).reshape(B, T, D)
+        x = x + o @ p[pre + "attn.c_proj.weight"] + p[pre + "attn.c_proj.bias"]
+        h = F.layer_norm(x, (D,), p[pre + "ln_2.weight"], p[pre + "ln_2.bias"], eps)
+        h = _gelu_new(h @ p[pre + "mlp.c_fc.weight"] + p[pre + "mlp.c_fc.bias"])
+        x = x + h @ p[pre + "mlp.c_proj.weight"] + p[pre + "mlp.c_proj.bias"]
+    x = F.layer_norm(x, (D,), p["model.transformer.ln_f.weight"], p["model.transformer.ln_f.bias"], eps)
+    return x @ p["model.transformer.wte.weight"].t()

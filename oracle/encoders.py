@@ -78,3 +78,37 @@ def vit_encoder(p, images, num_layers, num_heads, patch_size, eps=1e-12):
     (130-131; restated as None = no key padding)."""
     seq, pooled = vit_model(p, images, num_layers, num_heads, patch_size, eps)
     return {"features": seq[:, 1:], "pooled_features": pooled, "attention_mask": None}
+
+
+def clip_vision(p, images, num_layers, num_heads, patch_size, eps=1e-5):
+    """CLIPVisionModel.forward (transformers 5.15 modeling_clip.py): embeddings
+    (179-196: bias-free Conv2d patch, class_embedding, position_embedding) ->
+    pre_layrnorm (642) -> pre-LN layers (355-395: quick_gelu MLP) -> last_hidden_state;
+    pooled = post_layernorm(last_hidden_state[:, 0]) (650-651).  Parameter names are
+    the (flattened) CLIPVisionModel state dict."""
+    x = F.conv2d(images, p["embeddings.patch_embedding.weight"], None, stride=patch_size)
+    x = x.flatten(2).transpose(1, 2)
+    B, _, D = x.shape
+    cls = p["embeddings.class_embedding"].expand(B, 1, -1)
+    x = torch.cat([cls, x], 1) + p["embeddings.position_embedding.weight"][None]
+    x = F.layer_norm(x, (D,), p["pre_layrnorm.weight"], p["pre_layrnorm.bias"], eps)
+    for i in range(num_layers):
+        pre = f"encoder.layers.{i}."
+        h = F.layer_norm(x, (D,), p[pre + "layer_norm1.weight"], p[pre + "layer_norm1.bias"], eps)
+        a = pre + "self_attn."
+        x = x + mha_self(h, p[a + "q_proj.weight"], p[a + "q_proj.bias"], p[a + "k_proj.weight"],
+                         p[a + "k_proj.bias"], p[a + "v_proj.weight"], p[a + "v_proj.bias"],
+                         p[a + "out_proj.weight"], p[a + "out_proj.bias"], num_heads)
+        h = F.layer_norm(x, (D,), p[pre + "layer_norm2.weight"], p[pre + "layer_norm2.bias"], eps)
+        h = F.linear(h, p[pre + "mlp.fc1.weight"], p[pre + "mlp.fc1.bias"])
+        h = h * torch.sigmoid(1.702 * h)  # quick_gelu
+        x = x + F.linear(h, p[pre + "mlp.fc2.weight"], p[pre + "mlp.fc2.bias"])
+    pooled = F.layer_norm(x[:, 0], (D,), p["post_layernorm.weight"], p["post_layernorm.bias"], eps)
+    return x, pooled
+
+
+def clip_encoder(p, images, num_layers, num_heads, patch_size, eps=1e-5):
+    """CLIPEncoder.forward (src/models/encoders.py:209-230): features =
+    last_hidden_state[:, 1:] (no post-LN), pooled = pooler_output, proj = Identity."""
+    seq, pooled = clip_vision(p, images, num_layers, num_heads, patch_size, eps)
+    return {"features": seq[:, 1:], "pooled_features": pooled, "attention_mask": None}

@@ -138,7 +138,90 @@ def case_vit_transformer(R):
     return arrs
 
 
-CASES = {"vit_transformer_step": case_vit_transformer}
+def _d7_wrap(R, dec, prefix_len=10):
+    """SURVEY D7 restatement applied around the reference GPT2Decoder: the prefix
+    becomes a per-layer K = V = image_prefix.view(B,10,H,hd).transpose(1,2) cache
+    (the "simplified placeholder" intent of decoders.py:597-617) and the attention
+    mask gains the 10 always-visible prefix slots."""
+    from transformers import DynamicCache
+    cfg = dec.model.config
+    H = cfg.n_head
+
+    def prefix_cache(prefix_embeds):
+        B, P, D = prefix_embeds.shape
+        kv = prefix_embeds.view(B, P, H, D // H).transpose(1, 2)
+        cache = DynamicCache()
+        for layer in range(cfg.n_layer):
+            cache.update(kv, kv, layer)
+        return cache
+
+    dec._create_prefix_past_key_values = prefix_cache
+    inner = dec.model.forward
+
+    def fwd(*a, **kw):
+        ids, am = kw.get("input_ids"), kw.get("attention_mask")
+        if am is not None and ids is not None and am.shape[1] == ids.shape[1]:
+            kw["attention_mask"] = torch.cat([torch.ones(am.shape[0], prefix_len, dtype=am.dtype), am], 1)
+        return inner(*a, **kw)
+
+    dec.model.forward = fwd
+
+
+def case_clip_gpt2(R):
+    """Config 4 path (CLIP-ViT + GPT2Decoder; AoA inert, D15): CE train step through
+    the reference's ImageCaptioningModel.forward (CLIPEncoder, GPT2Decoder with the D7
+    prefix restatement), CombinedLoss and backward; eval mode (dropout off)."""
+    from transformers import CLIPVisionConfig, CLIPVisionModel
+    torch.manual_seed(4321)
+    D, Le, He, Ld, Hd, V = 64, 2, 2, 2, 2, 61
+    pad = V - 1
+    ccfg = CLIPVisionConfig(hidden_size=D, num_hidden_layers=Le, num_attention_heads=He, intermediate_size=2 * D,
+                            image_size=64, patch_size=32, num_channels=3)
+    enc = R.enc.CLIPEncoder.__new__(R.enc.CLIPEncoder)
+    nn.Module.__init__(enc)
+    enc.model = CLIPVisionModel(ccfg)
+    enc.feature_dim = D
+    enc.proj = nn.Identity()
+    dcfg = R.config.DecoderConfig(decoder_type=R.config.DecoderType.GPT2, pretrained_model_name=None, hidden_dim=D,
+                                  num_layers=Ld, num_heads=Hd, dropout=0.1, max_length=40)
+    dec = R.dec.GPT2Decoder(dcfg, vocab_size=V, pad_token_id=pad, bos_token_id=pad, eos_token_id=pad)
+    _d7_wrap(R, dec)
+    cfg = R.config.Config.__new__(R.config.Config)
+    model = R.cap.ImageCaptioningModel.__new__(R.cap.ImageCaptioningModel)
+    nn.Module.__init__(model)
+    model.config = cfg
+    model.encoder = enc
+    model.decoder = dec
+    orig_fwd = enc.forward
+    enc.forward = lambda images: {**orig_fwd(images), "attention_mask": None}
+    model.eval()
+
+    B, T = 3, 7
+    images = torch.randn(B, 3, 64, 64)
+    captions = torch.randint(0, V - 1, (B, T))
+    captions[0, 0] = pad  # bos
+    captions[1, 5:] = pad
+    captions[2, 6] = pad
+    params0 = {n: p.detach().clone() for n, p in model.named_parameters()}
+    out = model(images=images, captions=captions, caption_lengths=None)
+    logits = out["logits"]
+    loss = R.loss.CombinedLoss(pad_token_id=pad)(logits=logits, targets=captions)["total_loss"]
+    loss.backward()
+    feats = enc(images)
+    arrs = {
+        "meta/dims": np.array([D, Le, He, Ld, Hd, V, pad, 32, 64], dtype=np.int64),
+        "in/images": _np(images), "in/captions": _np(captions),
+        "out/logits": _np(logits), "out/loss": _np(loss.reshape(1)),
+        "out/features": _np(feats["features"]), "out/pooled": _np(feats["pooled_features"]),
+    }
+    for n, p in model.named_parameters():
+        arrs["p0/" + n] = _np(params0[n])
+        if p.grad is not None:
+            arrs["grad/" + n] = _np(p.grad)
+    return arrs
+
+
+CASES = {"vit_transformer_step": case_vit_transformer, "clip_gpt2_step": case_clip_gpt2}
 
 
 def main(names=None):

@@ -55,3 +55,24 @@ def time_cpu_baseline(state_dict, batch=4, steps=2, warmup=1, pad=50256, threads
         train_step(params, opt_state, images, caps, pad, warmup + i + 1, 5e-5)
     dt = time.perf_counter() - t0
     return batch * steps / dt, dt
+
+
+def time_cpu_beam(state_dict, images=2, num_beams=5, max_length=20, threads=None, eos=50256):
+    """Captions/s of the oracle CPU beam-5 path (ViT forward + oracle/beam.py over the
+    decoder re-run on each prefix, as the reference's generate does) on a bounded sample."""
+    import torch.nn.functional as F
+    from .beam import beam_search
+    if threads:
+        torch.set_num_threads(threads)
+    p = {k: v.detach().float() for k, v in state_dict.items()}
+    dec = _sub(p, "decoder.")
+    img = torch.randn(images, 3, 224, 224, generator=torch.Generator().manual_seed(7))
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        feats = oenc.vit_encoder(_sub(p, "encoder.model."), img, 12, 12, 16)["features"]
+        mem = F.linear(feats, dec["visual_projection.weight"], dec["visual_projection.bias"])
+        mem = mem.repeat_interleave(num_beams, 0)
+        beam_search(lambda s: odec.transformer_last_logits(dec, mem, s, 6, 8), images, num_beams, max_length,
+                    bos=eos, eos=eos, pad=eos)
+    dt = time.perf_counter() - t0
+    return images / dt, dt

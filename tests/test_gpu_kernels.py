@@ -194,6 +194,57 @@ def test_attention_fwd_bwd(ops, dtype, case):
         assert float(gap_rows.abs().max()) == 0.0
 
 
+@cuda
+@pytest.mark.parametrize("case", ["self_step", "cross_beams", "pad", "hd64_q8"])
+def test_attention_decode_bf16(ops, case):
+    """Small-Nq decode path (attn_decode_bf16, chosen automatically for Nq <= 8): KV-cache
+    self-attention (one query, strided cache rows) and beam cross-attention (k beam
+    queries of one image against shared memory keys with a CLS gap row)."""
+    from capk.ops import HeadView
+    g = torch.Generator(device="cuda").manual_seed(11)
+    pad = None
+    if case == "self_step":
+        B, H, Nq, Nk, hd, gap, Lm = 40, 8, 1, 13, 96, 0, 20
+    elif case == "cross_beams":
+        B, H, Nq, Nk, hd, gap, Lm = 6, 8, 5, 196, 96, 1, 0
+    elif case == "pad":
+        B, H, Nq, Nk, hd, gap, Lm = 4, 4, 3, 37, 32, 0, 0
+        pad = torch.zeros(B, Nk, dtype=torch.bool, device="cuda")
+        pad[1, 30:] = True
+        pad[2, 0] = True
+    else:
+        B, H, Nq, Nk, hd, gap, Lm = 5, 12, 8, 256, 64, 0, 0
+    D = H * hd
+    dtype = torch.bfloat16
+    if Lm:  # [B, Lm, 3D] cache; query = row Nk-1's q slot
+        cache = torch.randn(B, Lm, 3 * D, device="cuda", generator=g).to(dtype)
+        qv = HeadView(cache, (Nk - 1) * 3 * D, Lm * 3 * D, 3 * D)
+        kview = HeadView(cache, D, Lm * 3 * D, 3 * D)
+        vview = HeadView(cache, 2 * D, Lm * 3 * D, 3 * D)
+        qr = cache[:, Nk - 1:Nk, :D].float()
+        kr, vr = cache[:, :Nk, D:2 * D].float(), cache[:, :Nk, 2 * D:].float()
+    else:
+        q = torch.randn(B * Nq, D, device="cuda", generator=g).to(dtype)
+        kv = torch.randn((B - 1) * (Nk + gap) + Nk, 2 * D, device="cuda", generator=g).to(dtype)
+        qv = HeadView(q, 0, Nq * D, D)
+        kview = HeadView(kv, 0, (Nk + gap) * 2 * D, 2 * D)
+        vview = HeadView(kv, D, (Nk + gap) * 2 * D, 2 * D)
+        qr = q.float().view(B, Nq, D)
+        kr = torch.stack([kv[b * (Nk + gap):b * (Nk + gap) + Nk, :D] for b in range(B)]).float()
+        vr = torch.stack([kv[b * (Nk + gap):b * (Nk + gap) + Nk, D:] for b in range(B)]).float()
+    o = torch.empty(B * Nq, D, device="cuda", dtype=dtype)
+    scale = 1.0 / math.sqrt(hd)
+    lse, _ = ops.attention_fwd(qv, kview, vview, HeadView(o, 0, Nq * D, D), B, H, Nq, Nk, hd, scale, key_pad=pad)
+    sp = lambda t, n: t.reshape(B, n, H, hd).transpose(1, 2)  # noqa: E731
+    ref = _attn_ref(sp(qr, Nq), sp(kr, Nk), sp(vr, Nk), scale, False, pad)
+    got = o.float().view(B, Nq, H, hd).transpose(1, 2)
+    assert _rel(got, ref) < 1e-2
+    s = torch.einsum("bhqd,bhkd->bhqk", sp(qr, Nq), sp(kr, Nk)) * scale
+    if pad is not None:
+        s = s.masked_fill(pad[:, None, None, :], float("-inf"))
+    torch.testing.assert_close(lse, torch.logsumexp(s, -1), rtol=1e-4, atol=1e-4)
+
+
 # ------------------------------------------------------ CE / embeddings -----
 @cuda
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

@@ -98,3 +98,39 @@ def test_greedy_generate_matches_reference(vt):
         enc = oenc.vit_encoder(_sub(p, "encoder.model."), images, Le, He, patch)
         ids = odec.transformer_greedy(_sub(p, "decoder."), enc["features"], 6, Ld, Hd, pad, pad)
     np.testing.assert_array_equal(ids.numpy(), vt["out/greedy_ids"])
+
+
+# ------------------------------------------------ config 4: CLIP + GPT-2 (D7) --
+@pytest.fixture(scope="module")
+def cg(golden_dir):
+    return _load(golden_dir, "clip_gpt2_step")
+
+
+def _forward_cg(p, z):
+    D, Le, He, Ld, Hd, V, pad, patch, img = [int(x) for x in z["meta/dims"]]
+    images = torch.from_numpy(z["in/images"])
+    caps = torch.from_numpy(z["in/captions"])
+    enc = oenc.clip_encoder(_sub(p, "encoder.model."), images, Le, He, patch)
+    logits = odec.gpt2_decoder(_sub(p, "decoder."), enc["pooled_features"], caps, Ld, Hd, pad)
+    return enc, logits, otrain.shifted_ce(logits, caps, pad)
+
+
+def test_clip_gpt2_forward_matches_reference(cg):
+    enc, logits, loss = _forward_cg(_params(cg, "p0"), cg)
+    np.testing.assert_allclose(enc["features"].detach().numpy(), cg["out/features"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(enc["pooled_features"].detach().numpy(), cg["out/pooled"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(logits.detach().numpy(), cg["out/logits"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(loss.item(), cg["out/loss"][0], rtol=1e-6)
+
+
+def test_clip_gpt2_grads_match_reference(cg):
+    p = {k: v.requires_grad_(True) for k, v in _params(cg, "p0").items()}
+    _, _, loss = _forward_cg(p, cg)
+    loss.backward()
+    ref = _params(cg, "grad")
+    for n, t in p.items():
+        if n in ref:
+            assert t.grad is not None, n
+            np.testing.assert_allclose(t.grad.numpy(), ref[n].numpy(), rtol=1e-4, atol=1e-6, err_msg=n)
+        else:  # image_prefix / visual_projection: unused by the reference forward (grad None)
+            assert t.grad is None or float(t.grad.abs().max()) == 0.0, n
