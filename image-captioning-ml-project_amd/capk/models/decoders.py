@@ -11,6 +11,7 @@ import torch
 import torch.nn as nn
 
 from ..config import AttentionConfig, DecoderConfig, DecoderType
+from .gpt2 import GPT2DecoderCore
 from .transformer import TransformerDecoderCore
 
 
@@ -78,6 +79,44 @@ class TransformerDecoder(TransformerDecoderCore, CaptionDecoder):
         return ids, {}
 
 
+class GPT2Decoder(GPT2DecoderCore, CaptionDecoder):
+    """decoders.py:495-656 on libcapk kernels with the D7 prefix restatement.
+    Conditions on ``pooled_features`` only (patch features unused, as in the reference)."""
+
+    def __init__(self, config: DecoderConfig, vocab_size: int = None, pad_token_id: int = None,
+                 bos_token_id: int = None, eos_token_id: int = None):
+        GPT2DecoderCore.__init__(self, config, vocab_size, pad_token_id, bos_token_id, eos_token_id)
+
+    def forward(self, encoder_features, captions=None, caption_lengths=None, **kwargs):
+        if captions is None:
+            return self.generate(encoder_features, 50)  # decoders.py:562-564
+        logits = self.forward_logits(encoder_features["pooled_features"], captions)
+        # HF's labels=captions LM loss (mean over every shifted token, ignore_index -100; decoders.py:583-589);
+        # the trainer uses CombinedLoss on the logits instead (SURVEY A12)
+        from ..train.losses import shifted_cross_entropy
+        return {"logits": logits, "loss": shifted_cross_entropy(logits, captions, -100)}
+
+    @torch.no_grad()
+    def generate(self, encoder_features, max_length, num_beams=4, length_penalty=1.0, early_stopping=False,
+                 **kwargs):
+        """decoders.py:619-656: HF generate(num_beams, max_length, bos/eos/pad) from a
+        one-token bos prompt with the image prefix as cache (D7) -> HF beam search
+        semantics on the KV-cached decoder.  Returns (sequences, info)."""
+        if num_beams < 2:
+            raise NotImplementedError("capk GPT2Decoder.generate: greedy (num_beams=1) is not on the hot path; "
+                                      "the reference always beam-searches (decoders.py:623)")
+        from ..beam import beam_search
+        from .gpt2 import GPT2KVRunner
+        pooled = encoder_features["pooled_features"]
+        B = pooled.shape[0]
+        runner = GPT2KVRunner(self, pooled, num_beams, max_length)
+        prompt = torch.full((B,), self.bos_token_id, dtype=torch.long, device=pooled.device)
+        out = beam_search(runner.step, B, num_beams, max_length, prompt, self.eos_token_id,
+                          pad_token_id=self.pad_token_id, length_penalty=length_penalty,
+                          early_stopping=early_stopping, vocab_size=self.vocab_size)
+        return out["sequences"], {"sequences_scores": out["sequences_scores"], "beam_indices": out["beam_indices"]}
+
+
 def build_decoder(config: DecoderConfig, attention_config: AttentionConfig, vocab_size: int, pad_token_id: int,
                   bos_token_id: int, eos_token_id: int) -> CaptionDecoder:
     """decoders.py:659-692 (with D2: string types accepted; D3: attention hidden_dim filled)."""
@@ -85,6 +124,8 @@ def build_decoder(config: DecoderConfig, attention_config: AttentionConfig, voca
     attention_config.hidden_dim = config.hidden_dim
     if dt == DecoderType.TRANSFORMER:
         return TransformerDecoder(config, vocab_size, pad_token_id, bos_token_id, eos_token_id)
-    if dt in (DecoderType.LSTM, DecoderType.GPT2):
+    if dt == DecoderType.GPT2:
+        return GPT2Decoder(config, vocab_size, pad_token_id, bos_token_id, eos_token_id)
+    if dt == DecoderType.LSTM:
         raise NotImplementedError(f"capk: decoder '{dt.value}' is scheduled after the Transformer hot path")
     raise ValueError(f"Unsupported decoder type: {config.decoder_type}")

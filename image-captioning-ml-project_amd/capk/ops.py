@@ -305,3 +305,54 @@ def adamw(param, grad, m, v, param_bf16, lr, wd, beta1, beta2, eps, step):
     bc2 = 1.0 - beta2 ** step
     check(lib().capk_adamw(param.numel(), _p(param), _p(grad), _p(m), _p(v), _p(param_bf16), float(lr), float(wd),
                            float(beta1), float(beta2), float(eps), float(bc1), float(bc2), _stream()), "capk_adamw")
+
+
+# ---------------------------------------------------------- Conv1D (GPT-2) ---
+def conv1d(x, w, b=None, *, out=None, residual=None, act=0, preact=None, drop=NO_DROP):
+    """HF Conv1D: y = dropout(act(x @ W + b)) + residual with W [in, out] row-major
+    (transformers/pytorch_utils.py Conv1D; GPT-2 c_attn/c_proj/c_fc): the weight is
+    the GEMM's N-major B operand, so no transpose is materialised."""
+    M, K = x.shape
+    N = w.shape[1]
+    if out is None:
+        out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    gemm(x, True, w, False, M, N, K, out, lda=x.stride(0), ldb=w.stride(0), ldc=out.stride(0), bias=b,
+         residual=residual, ldr=residual.stride(0) if residual is not None else 0, act=act, preact=preact,
+         ldx=preact.stride(0) if preact is not None else 0, drop=drop)
+    return out
+
+
+def conv1d_dx(dy, w, *, out=None, act_bwd=0, aux=None, beta=0.0):
+    """dX[M, in] = dY[M, out] @ W[in, out]^T (optionally * act'(aux))."""
+    M, N = dy.shape
+    K = w.shape[0]
+    if out is None:
+        out = torch.empty(M, K, dtype=dy.dtype, device=dy.device)
+    gemm(dy, True, w, True, M, K, N, out, lda=dy.stride(0), ldb=w.stride(0), ldc=out.stride(0), beta=beta,
+         act=(ACT_BWD | act_bwd) if act_bwd else 0, aux=aux, ldx=aux.stride(0) if aux is not None else 0)
+    return out
+
+
+def gather_rows(x, idx, y, groups, rows, cols, ldx, gsx, ldy, gsy, x_off=0, y_off=0):
+    """y[g][r] = x[g][idx[r]] (element offsets x_off / y_off into x / y)."""
+    check(lib().capk_gather_rows(dtype_code(x), groups, rows, cols, idx.data_ptr(),
+                                 x.data_ptr() + x_off * x.element_size(), ldx, gsx,
+                                 y.data_ptr() + y_off * y.element_size(), ldy, gsy, _stream()), "capk_gather_rows")
+
+
+def dropout_apply(x, drop, out=None):
+    """x * mask (GEMM-epilogue mask convention, index r*cols + c)."""
+    if drop[0] <= 0:
+        return x
+    rows, cols = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    check(lib().capk_dropout_apply(dtype_code(x), rows, cols, _p(x), x.stride(0), float(drop[0]),
+                                   int(drop[1]) & 0xFFFFFFFF, _p(out), out.stride(0), _stream()),
+          "capk_dropout_apply")
+    return out
+
+
+def add_rows(x, y, groups, rows, cols, gsx, ldx, nseg, seg, gsy, ldy, accumulate, x_off=0):
+    check(lib().capk_add_rows(dtype_code(x), groups, rows, cols, x.data_ptr() + x_off * x.element_size(), gsx, ldx,
+                              nseg, seg, _p(y), gsy, ldy, int(accumulate), _stream()), "capk_add_rows")

@@ -40,7 +40,7 @@ __device__ __forceinline__ float pdrop(const AttnArgs& a, int b, int h, int q, i
 
 __device__ __forceinline__ bool key_ok(const AttnArgs& a, int b, int key, int q) {
   if (key >= a.Nk) return false;
-  if (a.causal && key > q) return false;
+  if (a.causal && key > q + (a.Nk - a.Nq)) return false;  // bottom-right aligned (prefix / KV cache)
   if (a.key_pad && a.key_pad[(int64_t)b * a.Nk + key]) return false;
   return true;
 }

@@ -280,6 +280,44 @@ __global__ __launch_bounds__(256) void copy_rows_kernel(int rows, int cols, cons
   }
 }
 
+
+// y = x * keep(seed, r*cols + c) / (1-p): the GEMM-epilogue dropout mask of an [rows, cols]
+// output re-applied to its gradient (pre-LN residual branches: GPT-2 resid dropout).
+template <typename T>
+__global__ __launch_bounds__(256) void dropout_apply_kernel(int rows, int cols, const T* __restrict__ x, int64_t ldx,
+                                                            T* __restrict__ y, int64_t ldy, Drop d) {
+  const int ch = cols / 8;
+  const int64_t total = (int64_t)rows * ch;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / ch;
+    const int c = (int)(i % ch) * 8;
+    float v[8];
+    Vec8<T>::load(x + r * ldx + c, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] *= d.mul((uint64_t)r * cols + c + j);
+    Vec8<T>::store(y + r * ldy + c, v);
+  }
+}
+
+// y[g][r][c] (+)= sum_s x[g][r][s*seg + c]   (fp32 out): e.g. the GPT-2 prefix gradient
+// dP = dK[:, :10] + dV[:, :10] summed over layers (K = V = prefix).
+template <typename T>
+__global__ __launch_bounds__(256) void add_rows_kernel(int G, int rows, int cols, const T* __restrict__ x, int64_t gsx,
+                                                       int64_t ldx, int nseg, int64_t seg, float* __restrict__ y,
+                                                       int64_t gsy, int64_t ldy, int accumulate) {
+  const int64_t total = (int64_t)G * rows * cols;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % cols);
+    const int64_t gr = i / cols;
+    const int r = (int)(gr % rows), g = (int)(gr / rows);
+    const T* xp = x + g * gsx + (int64_t)r * ldx + c;
+    float acc = 0.f;
+    for (int sgi = 0; sgi < nseg; ++sgi) acc += to_f32(xp[sgi * seg]);
+    float* yp = y + g * gsy + (int64_t)r * ldy + c;
+    *yp = accumulate ? *yp + acc : acc;
+  }
+}
+
 // ------------------------------------------------------------ AdamW --------
 __global__ __launch_bounds__(256) void adamw_kernel(int64_t n, float* __restrict__ p, const float* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v,
@@ -472,6 +510,30 @@ extern "C" int capk_copy_rows(int dtype, int rows, int cols, const void* x, int6
   DT_DISPATCH(dtype, L, 0)
 #undef L
   CAPK_LAUNCH_CHECK("copy_rows_kernel");
+  return CAPK_OK;
+}
+
+
+extern "C" int capk_dropout_apply(int dtype, int rows, int cols, const void* x, int64_t ldx, float p, uint32_t seed,
+                                  void* y, int64_t ldy, void* stream) {
+  CAPK_CHECK_ARG(rows > 0 && cols % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0, "capk_dropout_apply: need multiples of 8");
+  const int64_t work = (int64_t)rows * cols / 8;
+#define L(T, _) hipLaunchKernelGGL(dropout_apply_kernel<T>, dim3(grid_for(work)), dim3(256), 0, S(stream), rows, cols, (const T*)x, ldx, (T*)y, ldy, make_drop(p, seed))
+  DT_DISPATCH(dtype, L, 0)
+#undef L
+  CAPK_LAUNCH_CHECK("dropout_apply_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_add_rows(int dtype, int groups, int rows, int cols, const void* x, int64_t gsx, int64_t ldx,
+                             int nseg, int64_t seg_stride, float* y, int64_t gsy, int64_t ldy, int accumulate,
+                             void* stream) {
+  CAPK_CHECK_ARG(groups > 0 && rows > 0 && cols > 0 && nseg > 0, "capk_add_rows: sizes");
+  const int64_t work = (int64_t)groups * rows * cols;
+#define L(T, _) hipLaunchKernelGGL(add_rows_kernel<T>, dim3(grid_for(work)), dim3(256), 0, S(stream), groups, rows, cols, (const T*)x, gsx, ldx, nseg, seg_stride, y, gsy, ldy, accumulate)
+  DT_DISPATCH(dtype, L, 0)
+#undef L
+  CAPK_LAUNCH_CHECK("add_rows_kernel");
   return CAPK_OK;
 }
 

@@ -104,10 +104,15 @@ int capk_layernorm_bwd(int dtype, int rows, int cols, const void* dy, int64_t ld
  * workgroup, Q/K/V/dO staged in LDS, softmax by wavefront shuffles.
  * Token t of batch b, head h lives at  X + b*x_bs + t*x_rs + h*hd.
  * key_pad (optional, [B, Nk] uint8, 1 = padded key) and causal masks follow
- * nn.MultiheadAttention (-inf).  lse (fp32 [B,H,Nq]) is saved for backward.
- * Nk <= 256, Nq <= 256, hd in {16, 32, 64, 96, 128} (hd % 16 == 0).
- * Replaces ViT SDPA (modeling_vit.py:164-189,219-235) and the self/cross
- * attention of nn.TransformerDecoderLayer (transformer.py _sa_block/_mha_block). */
+ * nn.MultiheadAttention (-inf).  The causal mask is bottom-right aligned: key j is
+ * visible to query i iff j <= i + (Nk - Nq) (square: j <= i; GPT-2 with a 10-slot
+ * prefix cache: the prefix is always visible, modeling_gpt2.py causal mask with
+ * past_key_values).  lse (fp32 [B,H,Nq]) is saved for backward.
+ * Nk <= 256, Nq <= 256, hd % 8 == 0, hd <= 128 (fp32 path: hd in {8,16,32,64,96,128}).
+ * Nq <= 8 without causal/dropout (decode steps) runs a VALU kernel streaming K/V once.
+ * Replaces ViT/CLIP SDPA (modeling_vit.py:164-189,219-235), the self/cross
+ * attention of nn.TransformerDecoderLayer (transformer.py _sa_block/_mha_block)
+ * and GPT2Attention (modeling_gpt2.py:144-226). */
 int capk_attention_fwd(int dtype, int B, int H, int Nq, int Nk, int hd, float scale, int causal,
                        const void* q, int64_t q_bs, int64_t q_rs,
                        const void* k, int64_t k_bs, int64_t k_rs,
@@ -176,6 +181,17 @@ int capk_colsum(int dtype, int M, int N, const void* dy, int64_t ldy, float* db,
 /* elementwise casts / copies */
 int capk_cast(int in_dtype, int out_dtype, int64_t n, const void* x, void* y, void* stream);
 int capk_copy_rows(int dtype, int rows, int cols, const void* x, int64_t ldx, void* y, int64_t ldy, void* stream);
+
+/* y = x * dropout-mask(p, seed, index r*cols + c) — the GEMM-epilogue mask of an
+ * [rows, cols] output re-applied to its gradient (GPT-2 resid_dropout backward,
+ * modeling_gpt2.py:224,243). */
+int capk_dropout_apply(int dtype, int rows, int cols, const void* x, int64_t ldx, float p, uint32_t seed,
+                       void* y, int64_t ldy, void* stream);
+/* y[g][r][c] (+)= sum_{s<nseg} x[g][r][s*seg_stride + c]   (y fp32): e.g. the GPT-2
+ * prefix gradient dP = sum over layers of dK + dV of the 10 prefix slots (K = V =
+ * prefix; decoders.py:597-617). */
+int capk_add_rows(int dtype, int groups, int rows, int cols, const void* x, int64_t gsx, int64_t ldx, int nseg,
+                  int64_t seg_stride, float* y, int64_t gsy, int64_t ldy, int accumulate, void* stream);
 
 /* out = dy * act'(aux) elementwise (activation backward outside a GEMM, e.g. the
  * ViT pooler tanh, modeling_vit.py:295-301). */

@@ -105,7 +105,8 @@ def _gelu_new(x):
     return 0.5 * x * (1.0 + torch.tanh(math.sqrt(2.0 / math.pi) * (x + 0.044715 * torch.pow(x, 3.0))))
 
 
-def gpt2_decoder(p, pooled, captions, num_layers, num_heads, pad_token_id, prefix_len=10, eps=1e-5):
+def gpt2_decoder(p, pooled, captions, num_layers, num_heads, pad_token_id, prefix_len=10, eps=1e-5,
+                 use_pad_mask=True):
     """GPT2Decoder.forward (src/models/decoders.py:554-595) with the SURVEY D7
     restatement: prefix P = image_to_prefix(pooled).view(B,10,D); every layer's past
     K = V = P split into heads (decoders.py:597-617 intent); attention mask =
@@ -121,6 +122,8 @@ def gpt2_decoder(p, pooled, captions, num_layers, num_heads, pad_token_id, prefi
     pk = P.view(B, prefix_len, H, hd).transpose(1, 2)
     x = p["model.transformer.wte.weight"][captions] + p["model.transformer.wpe.weight"][prefix_len:prefix_len + T][None]
     keep = torch.cat([torch.ones(B, prefix_len, dtype=torch.bool), captions != pad_token_id], 1)
+    if not use_pad_mask:  # generate(): HF's mask is all ones for the prompt and every generated token
+        keep = torch.ones_like(keep)
     causal = torch.ones(T, prefix_len + T, dtype=torch.bool).tril(prefix_len)
     allowed = keep[:, None, None, :] & causal[None, None]
     for i in range(num_layers):

@@ -87,6 +87,31 @@ def test_factories_and_state_dict_names_match_reference():
         build_encoder(C.EncoderConfig(encoder_type="convnext"))
 
 
+def test_config4_factories_and_state_dict_names():
+    """CLIP-ViT-B/32 + GPT-2 (config 4): reference state-dict names (transformers 5.15
+    flattened CLIPVisionModel, GPT2LMHeadModel with tied lm_head) and 218.4 M params."""
+    from capk import config as C
+    from capk.models import captioning_model as cm
+    cfg = C.Config()
+    cfg.model.encoder = C.EncoderConfig(encoder_type="clip", pretrained_model_name="openai/clip-vit-base-patch32")
+    cfg.model.decoder = C.DecoderConfig(decoder_type="gpt2", pretrained_model_name="gpt2", num_layers=12,
+                                        num_heads=12)
+    cfg.model.vocab_size, cfg.model.pad_token_id = 50257, 50256
+    m = cm.ImageCaptioningModel(cfg)
+    keys = set(m.state_dict())
+    for k in ("encoder.model.embeddings.class_embedding", "encoder.model.embeddings.patch_embedding.weight",
+              "encoder.model.pre_layrnorm.weight", "encoder.model.encoder.layers.11.self_attn.out_proj.bias",
+              "encoder.model.encoder.layers.0.mlp.fc1.weight", "encoder.model.post_layernorm.bias",
+              "decoder.model.transformer.wte.weight", "decoder.model.transformer.h.11.attn.c_attn.weight",
+              "decoder.model.transformer.h.0.mlp.c_proj.bias", "decoder.model.lm_head.weight",
+              "decoder.image_to_prefix.weight", "decoder.image_prefix", "decoder.visual_projection.weight"):
+        assert k in keys, k
+    assert "encoder.model.embeddings.patch_embedding.bias" not in keys  # CLIP patch conv has no bias
+    assert m.decoder.model.lm_head.weight is m.decoder.model.transformer.wte.weight
+    assert m.decoder.model.transformer.h[0].attn.c_attn.weight.shape == (768, 2304)  # Conv1D [in, out]
+    assert abs(sum(p.numel() for p in m.parameters()) / 1e6 - 218.4) < 0.1
+
+
 def test_param_store_layout_cpu():
     """Flat buffers: AdamW groups by the reference name rule, fused QKV adjacency,
     padded vocab rows, optional pooler at the tail (CPU tensors; no kernels)."""
