@@ -63,6 +63,12 @@ SIGNATURES = {
     "capk_adamw": (_i, [_i64, _c_p, _c_p, _c_p, _c_p, _c_p, _f, _f, _f, _f, _f, _f, _f, _c_p]),
     "capk_dropout_apply": (_i, [_i, _i, _i, _c_p, _i64, _f, _u32, _c_p, _i64, _c_p]),
     "capk_add_rows": (_i, [_i, _i, _i, _i, _c_p, _i64, _i64, _i, _i64, _c_p, _i64, _i64, _i, _c_p]),
+    "capk_lstm_cell_fwd": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _c_p, _c_p, _i64, _c_p, _i64, _c_p, _f, _u32, _c_p]),
+    "capk_lstm_cell_bwd": (_i, [_i, _i, _i, _c_p, _c_p, _c_p, _i64, _c_p, _c_p, _c_p]),
+    "capk_soft_attn_fwd": (_i, [_i, _i, _i, _i, _c_p, _i64, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _c_p, _f, _c_p,
+                                _c_p, _i64, _c_p, _c_p]),
+    "capk_soft_attn_bwd": (_i, [_i, _i, _i, _i, _c_p, _i64, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _f, _c_p, _c_p,
+                                _i64, _c_p, _i64, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "capk_beam_state_bytes": (_sz, [_i, _i, _i]),
     "capk_beam_init": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _sz, _c_p]),
     "capk_beam_step": (_i, [_i, _i, _i, _i, _i, _i64, _c_p, _i, _i64, _f, _f, _i, _c_p, _sz, _c_p, _c_p, _c_p]),

@@ -1,0 +1,248 @@
+// LSTM decoder step kernels.
+//
+// The recurrent GEMMs (gates = x W_ih^T + b_ih + h W_hh^T + b_hh) run on the MFMA
+// GEMM; these kernels are the per-step elementwise / reduction parts:
+//   lstm_cell_fwd / lstm_cell_bwd  torch nn.LSTM cell (aten lstm_cell: gate order
+//                                  i, f, g, o; c' = f c + i g; h' = o tanh(c')), cell
+//                                  state kept in fp32, inter-layer dropout fused on
+//                                  the copy of h' that feeds the next layer.
+//   soft_attn_fwd / soft_attn_bwd  SoftAttention (src/models/attention.py:57-118):
+//                                  e = energy(tanh(q_proj(q) + key_proj(k))) / T,
+//                                  masked_fill(-1e9), softmax over S, ctx = w @ v.
+//                                  key_proj(k) is hoisted out of the decode loop by
+//                                  the caller (same values every step).
+// One workgroup per image for the attention kernels (S <= 256, D <= 1024).
+#include "common.h"
+
+namespace capk {
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+
+template <typename T>
+__global__ __launch_bounds__(256) void lstm_cell_fwd_kernel(int B, int D, const T* __restrict__ gates, int64_t ldg,
+                                                            const float* __restrict__ c_prev, float* __restrict__ c_out,
+                                                            T* __restrict__ h_out, int64_t ldh, T* __restrict__ h_drop,
+                                                            int64_t ldhd, T* __restrict__ act, Drop drop) {
+  const int64_t n = (int64_t)B * D;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int b = (int)(e / D), d = (int)(e % D);
+    const T* g = gates + (int64_t)b * ldg;
+    const float i = sigm(to_f32(g[d])), f = sigm(to_f32(g[D + d]));
+    const float gg = tanhf(to_f32(g[2 * D + d])), o = sigm(to_f32(g[3 * D + d]));
+    const float c = f * c_prev[e] + i * gg;
+    const float h = o * tanhf(c);
+    c_out[e] = c;
+    h_out[(int64_t)b * ldh + d] = from_f32<T>(h);
+    if (h_drop) h_drop[(int64_t)b * ldhd + d] = from_f32<T>(drop.on() ? h * drop.mul((uint64_t)e) : h);
+    T* a = act + (int64_t)b * 4 * D;
+    a[d] = from_f32<T>(i);
+    a[D + d] = from_f32<T>(f);
+    a[2 * D + d] = from_f32<T>(gg);
+    a[3 * D + d] = from_f32<T>(o);
+  }
+}
+
+// dh: total gradient w.r.t. h' (T), dc: in = grad w.r.t. c', out = grad w.r.t. c_prev (fp32, in place)
+template <typename T>
+__global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(int B, int D, const T* __restrict__ act,
+                                                            const float* __restrict__ c_prev, const T* __restrict__ dh,
+                                                            int64_t lddh, float* __restrict__ dc,
+                                                            T* __restrict__ dgates) {
+  const int64_t n = (int64_t)B * D;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int b = (int)(e / D), d = (int)(e % D);
+    const T* a = act + (int64_t)b * 4 * D;
+    const float i = to_f32(a[d]), f = to_f32(a[D + d]), g = to_f32(a[2 * D + d]), o = to_f32(a[3 * D + d]);
+    const float cp = c_prev[e];
+    const float c = f * cp + i * g;
+    const float tc = tanhf(c);
+    const float gh = to_f32(dh[(int64_t)b * lddh + d]);
+    const float dct = dc[e] + gh * o * (1.f - tc * tc);
+    T* dg = dgates + (int64_t)b * 4 * D;
+    dg[d] = from_f32<T>(dct * g * i * (1.f - i));
+    dg[D + d] = from_f32<T>(dct * cp * f * (1.f - f));
+    dg[2 * D + d] = from_f32<T>(dct * i * (1.f - g * g));
+    dg[3 * D + d] = from_f32<T>(gh * tc * o * (1.f - o));
+    dc[e] = dct * f;
+  }
+}
+
+// ------------------------------------------------------------ soft attention --
+static constexpr int SA_MAXS = 256;
+
+template <typename T>
+__global__ __launch_bounds__(256) void soft_attn_fwd_kernel(int S, int D, const T* __restrict__ qp, int64_t ldq,
+                                                            const T* __restrict__ kp, int64_t kp_bs, int64_t kp_rs,
+                                                            const T* __restrict__ v, int64_t v_bs, int64_t v_rs,
+                                                            const float* __restrict__ we, const float* __restrict__ be,
+                                                            float inv_temp, const uint8_t* __restrict__ key_pad,
+                                                            T* __restrict__ ctx, int64_t ldc, float* __restrict__ wout) {
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  __shared__ float sc[SA_MAXS];
+  __shared__ float red[4];
+  const T* q = qp + (int64_t)b * ldq;
+  const T* kb = kp + (int64_t)b * kp_bs;
+  for (int s = w; s < S; s += 4) {
+    const T* k = kb + (int64_t)s * kp_rs;
+    float acc = 0.f;
+    for (int d = lane; d < D; d += 64) acc += we[d] * tanhf(to_f32(q[d]) + to_f32(k[d]));
+    acc = wave_sum(acc);
+    if (lane == 0) {
+      float e = (acc + be[0]) * inv_temp;
+      if (key_pad && key_pad[(int64_t)b * S + s]) e = -1e9f;
+      sc[s] = e;
+    }
+  }
+  __syncthreads();
+  if (w == 0) {
+    float m = -INFINITY;
+    for (int s = lane; s < S; s += 64) m = fmaxf(m, sc[s]);
+    m = wave_max(m);
+    float l = 0.f;
+    for (int s = lane; s < S; s += 64) {
+      const float p = __expf(sc[s] - m);
+      sc[s] = p;
+      l += p;
+    }
+    l = wave_sum(l);
+    if (lane == 0) red[0] = 1.f / l;
+  }
+  __syncthreads();
+  const float inv = red[0];
+  for (int s = tid; s < S; s += 256) {
+    sc[s] *= inv;
+    wout[(int64_t)b * S + s] = sc[s];
+  }
+  __syncthreads();
+  const T* vb = v + (int64_t)b * v_bs;
+  for (int d = tid; d < D; d += 256) {
+    float acc = 0.f;
+    for (int s = 0; s < S; ++s) acc += sc[s] * to_f32(vb[(int64_t)s * v_rs + d]);
+    ctx[(int64_t)b * ldc + d] = from_f32<T>(acc);
+  }
+}
+
+// Gradients of one step; the key/value/energy gradients ACCUMULATE (fp32) over the
+// decode steps: dkp [B,S,D], dv [B,S,D], dwe_part [B,D], dbe_part [B].
+template <typename T>
+__global__ __launch_bounds__(256) void soft_attn_bwd_kernel(int S, int D, const T* __restrict__ qp, int64_t ldq,
+                                                            const T* __restrict__ kp, int64_t kp_bs, int64_t kp_rs,
+                                                            const T* __restrict__ v, int64_t v_bs, int64_t v_rs,
+                                                            const float* __restrict__ we, float inv_temp,
+                                                            const float* __restrict__ wsave, const T* __restrict__ dctx,
+                                                            int64_t lddc, T* __restrict__ dqp, int64_t lddq,
+                                                            float* __restrict__ dkp, float* __restrict__ dv,
+                                                            float* __restrict__ dwe_part, float* __restrict__ dbe_part) {
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  __shared__ float ws[SA_MAXS], de[SA_MAXS];
+  __shared__ float red[4];
+  const T* g = dctx + (int64_t)b * lddc;
+  const T* vb = v + (int64_t)b * v_bs;
+  for (int s = tid; s < S; s += 256) ws[s] = wsave[(int64_t)b * S + s];
+  __syncthreads();
+  // dw[s] = dctx . v[s]
+  for (int s = w; s < S; s += 4) {
+    const T* vr = vb + (int64_t)s * v_rs;
+    float acc = 0.f;
+    for (int d = lane; d < D; d += 64) acc += to_f32(g[d]) * to_f32(vr[d]);
+    acc = wave_sum(acc);
+    if (lane == 0) de[s] = acc;
+  }
+  __syncthreads();
+  if (w == 0) {
+    float dot = 0.f;
+    for (int s = lane; s < S; s += 64) dot += ws[s] * de[s];
+    dot = wave_sum(dot);
+    if (lane == 0) red[0] = dot;
+  }
+  __syncthreads();
+  const float dot = red[0];
+  for (int s = tid; s < S; s += 256) de[s] = ws[s] * (de[s] - dot) * inv_temp;
+  __syncthreads();
+  const T* q = qp + (int64_t)b * ldq;
+  const T* kb = kp + (int64_t)b * kp_bs;
+  float* dkb = dkp + (int64_t)b * S * D;
+  float* dvb = dv + (int64_t)b * S * D;
+  float dbe = 0.f;
+  for (int s = tid; s < S; s += 256) dbe += de[s];
+  for (int d = tid; d < D; d += 256) {
+    const float qd = to_f32(q[d]), wd = we[d], gd = to_f32(g[d]);
+    float dq = 0.f, dw = 0.f;
+    for (int s = 0; s < S; ++s) {
+      const float a = tanhf(qd + to_f32(kb[(int64_t)s * kp_rs + d]));
+      const float gr = de[s] * wd * (1.f - a * a);
+      dq += gr;
+      dw += de[s] * a;
+      dkb[(int64_t)s * D + d] += gr;
+      dvb[(int64_t)s * D + d] += ws[s] * gd;
+    }
+    dqp[(int64_t)b * lddq + d] = from_f32<T>(dq);
+    dwe_part[(int64_t)b * D + d] += dw;
+  }
+  dbe = wave_sum(dbe);
+  if (lane == 0) red[w] = dbe;
+  __syncthreads();
+  if (tid == 0) dbe_part[b] += red[0] + red[1] + red[2] + red[3];
+}
+
+static int grid_n(int64_t n) {
+  int64_t g = (n + 255) / 256;
+  return (int)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
+}
+
+}  // namespace capk
+
+using namespace capk;
+
+#define DT2(dtype, KERNEL_T, ...)                                                 \
+  do {                                                                           \
+    if ((dtype) == CAPK_F32) { KERNEL_T(float, __VA_ARGS__); }                    \
+    else if ((dtype) == CAPK_BF16) { KERNEL_T(bf16, __VA_ARGS__); }               \
+    else { set_error("capk lstm: dtype"); return CAPK_EINVAL; }                   \
+  } while (0)
+
+extern "C" int capk_lstm_cell_fwd(int dtype, int B, int D, const void* gates, int64_t ldg, const float* c_prev,
+                                  float* c_out, void* h_out, int64_t ldh, void* h_drop, int64_t ldhd, void* act,
+                                  float drop_p, uint32_t drop_seed, void* stream) {
+  CAPK_CHECK_ARG(B > 0 && D > 0 && ldg >= 4 * D && ldh >= D, "capk_lstm_cell_fwd: bad sizes");
+#define K(T, _) hipLaunchKernelGGL(lstm_cell_fwd_kernel<T>, dim3(grid_n((int64_t)B * D)), dim3(256), 0, S(stream), B, D, (const T*)gates, ldg, c_prev, c_out, (T*)h_out, ldh, (T*)h_drop, ldhd, (T*)act, make_drop(drop_p, drop_seed))
+  DT2(dtype, K, 0);
+#undef K
+  CAPK_LAUNCH_CHECK("lstm_cell_fwd_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_lstm_cell_bwd(int dtype, int B, int D, const void* act, const float* c_prev, const void* dh,
+                                  int64_t lddh, float* dc, void* dgates, void* stream) {
+  CAPK_CHECK_ARG(B > 0 && D > 0 && lddh >= D, "capk_lstm_cell_bwd: bad sizes");
+#define K(T, _) hipLaunchKernelGGL(lstm_cell_bwd_kernel<T>, dim3(grid_n((int64_t)B * D)), dim3(256), 0, S(stream), B, D, (const T*)act, c_prev, (const T*)dh, lddh, dc, (T*)dgates)
+  DT2(dtype, K, 0);
+#undef K
+  CAPK_LAUNCH_CHECK("lstm_cell_bwd_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_soft_attn_fwd(int dtype, int B, int S, int D, const void* qp, int64_t ldq, const void* kp,
+                                  int64_t kp_bs, int64_t kp_rs, const void* v, int64_t v_bs, int64_t v_rs,
+                                  const float* we, const float* be, float inv_temp, const uint8_t* key_pad, void* ctx,
+                                  int64_t ldc, float* w_out, void* stream) {
+  CAPK_CHECK_ARG(B > 0 && S > 0 && S <= SA_MAXS && D > 0, "capk_soft_attn_fwd: need 0 < S <= %d", SA_MAXS);
+#define K(T, _) hipLaunchKernelGGL(soft_attn_fwd_kernel<T>, dim3(B), dim3(256), 0, capk::S(stream), S, D, (const T*)qp, ldq, (const T*)kp, kp_bs, kp_rs, (const T*)v, v_bs, v_rs, we, be, inv_temp, key_pad, (T*)ctx, ldc, w_out)
+  DT2(dtype, K, 0);
+#undef K
+  CAPK_LAUNCH_CHECK("soft_attn_fwd_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_soft_attn_bwd(int dtype, int B, int S, int D, const void* qp, int64_t ldq, const void* kp,
+                                  int64_t kp_bs, int64_t kp_rs, const void* v, int64_t v_bs, int64_t v_rs,
+                                  const float* we, float inv_temp, const float* w, const void* dctx, int64_t lddc,
+                                  void* dqp, int64_t lddq, float* dkp, float* dv, float* dwe_part, float* dbe_part,
+                                  void* stream) {
+  CAPK_CHECK_ARG(B > 0 && S > 0 && S <= SA_MAXS && D > 0, "capk_soft_attn_bwd: need 0 < S <= %d", SA_MAXS);
+#define K(T, _) hipLaunchKernelGGL(soft_attn_bwd_kernel<T>, dim3(B), dim3(256), 0, capk::S(stream), S, D, (const T*)qp, ldq, (const T*)kp, kp_bs, kp_rs, (const T*)v, v_bs, v_rs, we, inv_temp, w, (const T*)dctx, lddc, (T*)dqp, lddq, dkp, dv, dwe_part, dbe_part)
+  DT2(dtype, K, 0);
+#undef K
+  CAPK_LAUNCH_CHECK("soft_attn_bwd_kernel");
+  return CAPK_OK;
+}

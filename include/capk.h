@@ -239,6 +239,32 @@ int capk_beam_finalize(int B, int num_beams, int max_length, const void* state, 
 int capk_gather_rows(int dtype, int groups, int rows, int cols, const int32_t* idx, const void* x, int64_t ldx,
                      int64_t gsx, void* y, int64_t ldy, int64_t gsy, void* stream);
 
+/* --------------------------------------------------- LSTM decoder (A6/A7) ---
+ * nn.LSTM cell (gate order i, f, g, o; aten lstm_cell) on pre-activation gates
+ * [B, 4D] (= x W_ih^T + b_ih + h W_hh^T + b_hh from two GEMMs).  Cell state fp32.
+ * h_drop (optional) receives dropout(h') (inter-layer dropout of nn.LSTM, index
+ * b*D + d) for the next layer's input; act [B, 4D] saves i, f, g, o for backward.
+ * capk_lstm_cell_bwd: dh = total grad w.r.t. h'; dc in = grad w.r.t. c', out = grad
+ * w.r.t. c_prev (in place); dgates = pre-activation gate gradients [B, 4D].
+ * Replaces torch.nn.LSTM (decoders.py:97-103, 199) one step at a time. */
+int capk_lstm_cell_fwd(int dtype, int B, int D, const void* gates, int64_t ldg, const float* c_prev, float* c_out,
+                       void* h_out, int64_t ldh, void* h_drop, int64_t ldhd, void* act, float drop_p,
+                       uint32_t drop_seed, void* stream);
+int capk_lstm_cell_bwd(int dtype, int B, int D, const void* act, const float* c_prev, const void* dh, int64_t lddh,
+                       float* dc, void* dgates, void* stream);
+/* SoftAttention (src/models/attention.py:57-118) for one decode step, one query per
+ * image: e[b,s] = (sum_d we[d] tanh(qp[b,d] + kp[b,s,d]) + be) * inv_temp, key_pad ->
+ * -1e9, w = softmax_s(e), ctx[b] = sum_s w[b,s] v[b,s] (w_out fp32 [B,S]).  kp is the
+ * hoisted key_proj(keys).  Backward ACCUMULATES (fp32) dkp, dv [B,S,D], dwe_part [B,D],
+ * dbe_part [B] over steps and writes dqp.  S <= 256. */
+int capk_soft_attn_fwd(int dtype, int B, int S, int D, const void* qp, int64_t ldq, const void* kp, int64_t kp_bs,
+                       int64_t kp_rs, const void* v, int64_t v_bs, int64_t v_rs, const float* we, const float* be,
+                       float inv_temp, const uint8_t* key_pad, void* ctx, int64_t ldc, float* w_out, void* stream);
+int capk_soft_attn_bwd(int dtype, int B, int S, int D, const void* qp, int64_t ldq, const void* kp, int64_t kp_bs,
+                       int64_t kp_rs, const void* v, int64_t v_bs, int64_t v_rs, const float* we, float inv_temp,
+                       const float* w, const void* dctx, int64_t lddc, void* dqp, int64_t lddq, float* dkp, float* dv,
+                       float* dwe_part, float* dbe_part, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

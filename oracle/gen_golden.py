@@ -221,7 +221,56 @@ def case_clip_gpt2(R):
     return arrs
 
 
-CASES = {"vit_transformer_step": case_vit_transformer, "clip_gpt2_step": case_clip_gpt2}
+def case_lstm_attention(R):
+    """LSTMDecoder (decoders.py:70-314) with each attention type of attention.py
+    (soft with temperature 0.7, multi_head, aoa, adaptive; heads 4): teacher-forced
+    forward (caption_lengths=None, D10), CombinedLoss, backward (eval mode).  Encoder
+    features are plain leaf tensors so their gradients are recorded too.  D3: the
+    AttentionConfig receives hidden_dim as build_decoder's restatement does."""
+    torch.manual_seed(777)
+    D, L, V, B, T, S = 64, 2, 53, 3, 6, 7
+    pad = V - 1
+    arrs = {"meta/dims": np.array([D, L, V, B, T, S, pad], dtype=np.int64)}
+    feats = torch.randn(B, S, D)
+    pooled = torch.randn(B, D)
+    caps = torch.randint(0, V - 1, (B, T))
+    caps[1, 4:] = pad
+    arrs["in/features"], arrs["in/pooled"], arrs["in/captions"] = _np(feats), _np(pooled), _np(caps)
+    variants = [("soft", R.config.AttentionType.SOFT, 1, 0.7), ("multi_head", R.config.AttentionType.MULTI_HEAD, 4, 1.0),
+                ("aoa", R.config.AttentionType.AOA, 4, 1.0), ("adaptive", R.config.AttentionType.ADAPTIVE, 4, 1.0),
+                ("adaptive_soft", R.config.AttentionType.ADAPTIVE, 1, 1.0)]
+    for name, at, heads, temp in variants:
+        torch.manual_seed(1000 + len(name))
+        dcfg = R.config.DecoderConfig(decoder_type=R.config.DecoderType.LSTM, hidden_dim=D, num_layers=L,
+                                      num_heads=heads, dropout=0.1, max_length=50)
+        acfg = R.config.AttentionConfig(attention_type=at, num_heads=heads, temperature=temp)
+        acfg.hidden_dim = D  # D3
+        dec = R.dec.LSTMDecoder(dcfg, acfg, vocab_size=V, pad_token_id=pad)
+        dec.eval()
+        f = feats.clone().requires_grad_(True)
+        pl = pooled.clone().requires_grad_(True)
+        out = dec({"features": f, "pooled_features": pl, "attention_mask": None}, caps, None)
+        loss = R.loss.CombinedLoss(pad_token_id=pad)(logits=out["logits"], targets=caps)["total_loss"]
+        loss.backward()
+        pre = name + "/"
+        arrs[pre + "logits"] = _np(out["logits"])
+        arrs[pre + "attention_weights"] = _np(out["attention_weights"])
+        arrs[pre + "loss"] = _np(loss.reshape(1))
+        arrs[pre + "dfeatures"] = _np(f.grad)
+        arrs[pre + "dpooled"] = _np(pl.grad)
+        with torch.no_grad():
+            ids, info = dec.generate({"features": feats, "pooled_features": pooled, "attention_mask": None}, 6,
+                                     start_token_id=pad)
+        arrs[pre + "greedy_ids"] = _np(ids)
+        for n, p in dec.named_parameters():
+            arrs[pre + "p0/" + n] = _np(p)
+            if p.grad is not None:
+                arrs[pre + "grad/" + n] = _np(p.grad)
+    return arrs
+
+
+CASES = {"vit_transformer_step": case_vit_transformer, "clip_gpt2_step": case_clip_gpt2,
+         "lstm_attention": case_lstm_attention}
 
 
 def main(names=None):

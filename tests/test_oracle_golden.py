@@ -134,3 +134,38 @@ def test_clip_gpt2_grads_match_reference(cg):
             np.testing.assert_allclose(t.grad.numpy(), ref[n].numpy(), rtol=1e-4, atol=1e-6, err_msg=n)
         else:  # image_prefix / visual_projection: unused by the reference forward (grad None)
             assert t.grad is None or float(t.grad.abs().max()) == 0.0, n
+
+
+# ------------------------------------------- LSTM decoder + attention types --
+LSTM_VARIANTS = [("soft", "soft", 1, 0.7), ("multi_head", "multi_head", 4, 1.0), ("aoa", "aoa", 4, 1.0),
+                 ("adaptive", "adaptive", 4, 1.0), ("adaptive_soft", "adaptive", 1, 1.0)]
+
+
+@pytest.mark.parametrize("name,kind,heads,temp", LSTM_VARIANTS)
+def test_lstm_attention_matches_reference(golden_dir, name, kind, heads, temp):
+    from oracle import lstm as olstm
+    z = _load(golden_dir, "lstm_attention")
+    D, L, V, B, T, S, pad = [int(x) for x in z["meta/dims"]]
+    p = {k[len(name) + 4:]: torch.from_numpy(z[k].copy()).requires_grad_(True) for k in z.files
+         if k.startswith(name + "/p0/")}
+    feats = torch.from_numpy(z["in/features"]).requires_grad_(True)
+    pooled = torch.from_numpy(z["in/pooled"]).requires_grad_(True)
+    caps = torch.from_numpy(z["in/captions"])
+    logits, w = olstm.lstm_decoder(p, feats, pooled, caps, L, kind, heads, temp)
+    np.testing.assert_allclose(logits.detach().numpy(), z[name + "/logits"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(w.detach().numpy(), z[name + "/attention_weights"], rtol=1e-5, atol=1e-6)
+    loss = otrain.shifted_ce(logits, caps, pad)
+    np.testing.assert_allclose(loss.item(), z[name + "/loss"][0], rtol=1e-6)
+    loss.backward()
+    np.testing.assert_allclose(feats.grad.numpy(), z[name + "/dfeatures"], rtol=1e-4, atol=1e-7)
+    np.testing.assert_allclose(pooled.grad.numpy(), z[name + "/dpooled"], rtol=1e-4, atol=1e-7)
+    for n, t in p.items():
+        key = name + "/grad/" + n
+        if key in z.files:
+            np.testing.assert_allclose(t.grad.numpy(), z[key], rtol=1e-4, atol=1e-7, err_msg=n)
+        else:
+            assert t.grad is None or float(t.grad.abs().max()) == 0.0, n
+    with torch.no_grad():
+        ids = olstm.lstm_greedy({k: v.detach() for k, v in p.items()}, feats.detach(), pooled.detach(), 6, L, kind,
+                                pad, heads, temp)
+    np.testing.assert_array_equal(ids.numpy(), z[name + "/greedy_ids"])
