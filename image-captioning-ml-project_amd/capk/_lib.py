@@ -74,6 +74,7 @@ SIGNATURES = {
     "capk_beam_step": (_i, [_i, _i, _i, _i, _i, _i64, _c_p, _i, _i64, _f, _f, _i, _c_p, _sz, _c_p, _c_p, _c_p]),
     "capk_beam_flags": (_i, [_c_p, _c_p, _c_p]),
     "capk_beam_finalize": (_i, [_i, _i, _i, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "capk_argmax_rows": (_i, [_i, _i, _i, _i64, _c_p, _c_p, _i64, _c_p]),
     "capk_gather_rows": (_i, [_i, _i, _i, _i, _c_p, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p]),
 }
 

@@ -12,6 +12,7 @@ import torch.nn as nn
 
 from ..config import AttentionConfig, DecoderConfig, DecoderType
 from .gpt2 import GPT2DecoderCore
+from .lstm import LSTMDecoderCore, lstm_greedy
 from .transformer import TransformerDecoderCore
 
 
@@ -79,6 +80,29 @@ class TransformerDecoder(TransformerDecoderCore, CaptionDecoder):
         return ids, {}
 
 
+class LSTMDecoder(LSTMDecoderCore, CaptionDecoder):
+    """decoders.py:70-314 on libcapk kernels (SURVEY A6 + the attention module of A7-A10)."""
+
+    def __init__(self, config: DecoderConfig, attention_config: AttentionConfig, vocab_size: int, pad_token_id: int,
+                 embedding_dim: int = None):
+        LSTMDecoderCore.__init__(self, config, attention_config, vocab_size, pad_token_id, embedding_dim)
+        self.max_length = config.max_length
+
+    def forward(self, encoder_features, captions=None, caption_lengths=None, **kwargs):
+        if captions is None:  # decoders.py:145-148 (D11: `config` restated as the decoder's own max_length)
+            return self.generate(encoder_features, self.max_length)
+        # caption_lengths: the reference sorts by length and unsorts afterwards (decoders.py:157-169) but builds
+        # h0/c0 from the unsorted pooled features (D10); the trainer passes None (SURVEY A6) -> no sort here
+        logits, weights = self.forward_logits(encoder_features["features"], encoder_features["pooled_features"],
+                                              captions)
+        return {"logits": logits, "attention_weights": weights}
+
+    @torch.no_grad()
+    def generate(self, encoder_features, max_length, start_token_id=1, **kwargs):
+        return lstm_greedy(self, encoder_features["features"], encoder_features["pooled_features"], max_length,
+                           start_token_id)
+
+
 class GPT2Decoder(GPT2DecoderCore, CaptionDecoder):
     """decoders.py:495-656 on libcapk kernels with the D7 prefix restatement.
     Conditions on ``pooled_features`` only (patch features unused, as in the reference)."""
@@ -127,5 +151,5 @@ def build_decoder(config: DecoderConfig, attention_config: AttentionConfig, voca
     if dt == DecoderType.GPT2:
         return GPT2Decoder(config, vocab_size, pad_token_id, bos_token_id, eos_token_id)
     if dt == DecoderType.LSTM:
-        raise NotImplementedError(f"capk: decoder '{dt.value}' is scheduled after the Transformer hot path")
+        return LSTMDecoder(config, attention_config, vocab_size, pad_token_id)
     raise ValueError(f"Unsupported decoder type: {config.decoder_type}")

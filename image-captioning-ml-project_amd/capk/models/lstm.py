@@ -1,0 +1,280 @@
+"""LSTM caption decoder on libcapk kernels (with A7-A10 attention).
+
+Restates src/models/decoders.py:70-314 (LSTMDecoder).  Parameter names match the
+reference (``embedding``, ``lstm.weight_ih_l{k}`` / ``weight_hh_l{k}`` / ``bias_*``,
+``attention.*``, ``output_layer``, ``init_h``, ``init_c``).
+
+Teacher-forced pass = one autograd Function over the whole caption:
+  * h0/c0 = init_h/init_c(pooled) (GEMMs; c kept fp32);
+  * embeddings of all steps and their layer-0 input projection are ONE GEMM before the
+    loop (x_t W_ih0[:, :E]^T); per step only the recurrent GEMMs remain:
+      layer 0: gates = pre_t + ctx_{t-1} W_ih0[:, E:]^T + h W_hh0^T + b_hh0
+      layer l: gates = h_{l-1}' W_ih_l^T + b_ih_l + h_l W_hh_l^T + b_hh_l
+    then the fused cell kernel (fp32 cell state; inter-layer dropout on the copy that
+    feeds the next layer);
+  * attention step (query = top h, memory/cell = h[-1]/c[-1]) — key/value projections
+    of the image features hoisted out of the loop;
+  * logits = output_layer(dropout(ctx)) for all steps as ONE GEMM after the loop.
+Backward runs the recurrence in reverse with per-step GEMMs for the state/input
+gradients and batches every weight gradient into one GEMM over all steps.  Step
+buffers are t-major ([T, B, ...]); the LM head works on b-major rows so the logits are
+the [B, T, V] view the CE kernel consumes.
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .common import G, CapkModule, W, next_seed
+from .transformer import _pad64, _pad_bias, _pad_bias_grad, _padded_grad
+from .attention import build_attention
+
+
+class _LSTMParams(nn.Module):
+    """nn.LSTM's parameters (names + uniform(-1/sqrt(H), 1/sqrt(H)) init) without its cuDNN state."""
+
+    def __init__(self, input_size, hidden_size, num_layers):
+        super().__init__()
+        self.input_size, self.hidden_size, self.num_layers = input_size, hidden_size, num_layers
+        k = 1.0 / math.sqrt(hidden_size)
+        for layer in range(num_layers):
+            inp = input_size if layer == 0 else hidden_size
+            for name, shape in ((f"weight_ih_l{layer}", (4 * hidden_size, inp)),
+                                (f"weight_hh_l{layer}", (4 * hidden_size, hidden_size)),
+                                (f"bias_ih_l{layer}", (4 * hidden_size,)), (f"bias_hh_l{layer}", (4 * hidden_size,))):
+                p = nn.Parameter(torch.empty(shape))
+                nn.init.uniform_(p, -k, k)
+                self.register_parameter(name, p)
+
+    def w(self, kind, layer):
+        return getattr(self, f"{kind}_l{layer}")
+
+
+class LSTMDecoderCore(CapkModule):
+    def __init__(self, config, attention_config, vocab_size, pad_token_id, embedding_dim=None):
+        super().__init__()
+        self.hidden_dim = config.hidden_dim
+        self.embedding_dim = embedding_dim or config.hidden_dim
+        self.num_layers = config.num_layers
+        self.vocab_size = vocab_size
+        self.vocab_pad = _pad64(vocab_size)
+        self.dropout_p = config.dropout
+        self.pad_token_id = pad_token_id
+        self.embedding = nn.Embedding(vocab_size, self.embedding_dim, padding_idx=pad_token_id)
+        self.lstm = _LSTMParams(self.embedding_dim + self.hidden_dim, self.hidden_dim, self.num_layers)
+        self.attention = build_attention(attention_config)
+        self.output_layer = nn.Linear(self.hidden_dim, vocab_size)
+        self.output_layer.weight._capk_pad_rows = self.vocab_pad
+        self.output_layer.bias._capk_pad_rows = self.vocab_pad
+        self.init_h = nn.Linear(self.hidden_dim, self.hidden_dim * self.num_layers)
+        self.init_c = nn.Linear(self.hidden_dim, self.hidden_dim * self.num_layers)
+        self.dropout = nn.Dropout(self.dropout_p)
+
+    def forward_logits(self, features, pooled, captions):
+        """-> (logits [B,T,V] view, attention_weights [B,T,S] view)."""
+        return _LSTMFn.apply(features, pooled, captions, self.output_layer.weight, self)
+
+
+class _LSTMFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, features, pooled, captions, anchor, m):
+        ctx.set_materialize_grads(False)
+        dt = m.cdtype
+        dev = captions.device
+        B, T = captions.shape
+        D, E, L = m.hidden_dim, m.embedding_dim, m.num_layers
+        V, Vp = m.vocab_size, m.vocab_pad
+        lstm, att = m.lstm, m.attention
+        if features.dtype != dt or pooled.dtype != dt:
+            raise TypeError(f"capk LSTMDecoder: feature dtype {features.dtype}/{pooled.dtype} != compute dtype {dt}")
+        p = m.dropout_p if m.training else 0.0
+        drop = (lambda: (p, next_seed())) if p > 0 else (lambda: ops.NO_DROP)
+        pooled = pooled.contiguous()
+        # initial states (decoders.py:122-135): layer l = columns [l*D, (l+1)*D)
+        h0 = ops.linear(pooled, W(m.init_h.weight, dt), m.init_h.bias.detach())
+        c0 = ops.linear(pooled, W(m.init_c.weight, dt), m.init_c.bias.detach(), out_dtype=torch.float32)
+        Hs = [torch.empty(T + 1, B, D, dtype=dt, device=dev) for _ in range(L)]
+        Cs = [torch.empty(T + 1, B, D, dtype=torch.float32, device=dev) for _ in range(L)]
+        for layer in range(L):
+            ops.copy_rows(h0[:, layer * D:(layer + 1) * D], Hs[layer][0])
+            ops.copy_rows(c0[:, layer * D:(layer + 1) * D], Cs[layer][0])
+        # embeddings, t-major rows (t*B + b), dropout (decoders.py:172-173)
+        ids_t = captions.t().contiguous()
+        d_emb = drop()
+        emb = ops.embedding_fwd(ids_t, m.embedding.weight.detach(), None, 0, dt, drop=d_emb)  # [T*B, E]
+        w_ih0 = W(lstm.weight_ih_l0, dt)
+        pre0 = ops.linear(emb, w_ih0[:, :E], lstm.bias_ih_l0.detach())  # [T*B, 4D]
+        CtxT = torch.zeros(T + 1, B, D, dtype=dt, device=dev)  # ctx_{t-1} feeds step t; row 0 = zeros
+        H = att.hoist(features, features, None, T)
+        acts = [torch.empty(T, B, 4 * D, dtype=dt, device=dev) for _ in range(L)]
+        Hd = [torch.empty(T, B, D, dtype=dt, device=dev) for _ in range(L - 1)] if p > 0 else None
+        drops = [[drop() for _ in range(L - 1)] for _ in range(T)]
+        gates = torch.empty(B, 4 * D, dtype=dt, device=dev)
+        for t in range(T):
+            for layer in range(L):
+                if layer == 0:
+                    ops.gemm(CtxT[t], True, w_ih0[:, E:], True, B, 4 * D, D, gates, lda=D, ldb=E + D, ldc=4 * D,
+                             residual=pre0[t * B:(t + 1) * B], ldr=4 * D)
+                else:
+                    xin = Hd[layer - 1][t] if Hd is not None else Hs[layer - 1][t + 1]
+                    ops.linear(xin, W(lstm.w("weight_ih", layer), dt), lstm.w("bias_ih", layer).detach(), out=gates)
+                ops.gemm(Hs[layer][t], True, W(lstm.w("weight_hh", layer), dt), True, B, 4 * D, D, gates, lda=D,
+                         ldb=D, ldc=4 * D, beta=1.0, bias=lstm.w("bias_hh", layer).detach())
+                hd = Hd[layer][t] if (Hd is not None and layer < L - 1) else None
+                ops.lstm_cell_fwd(gates, Cs[layer][t], Cs[layer][t + 1], Hs[layer][t + 1], acts[layer][t], h_drop=hd,
+                                  drop=drops[t][layer] if hd is not None else ops.NO_DROP)
+            att.step_fwd(H, t, Hs[L - 1][t + 1], Hs[L - 1][t + 1], Cs[L - 1][t + 1], CtxT[t + 1])
+        # LM head on b-major rows: ctx [B, T, D] (decoders.py:222-223: output_layer(dropout(context)))
+        Ctxb = torch.empty(B, T, D, dtype=dt, device=dev)
+        idxT = torch.arange(T, dtype=torch.int32, device=dev)
+        ops.gather_rows(CtxT, idxT, Ctxb, B, T, D, B * D, D, D, T * D, x_off=B * D)
+        d_out = drop()
+        ctx_in = ops.dropout_apply(Ctxb.view(B * T, D), d_out) if d_out[0] > 0 else Ctxb.view(B * T, D)
+        ol = m.output_layer
+        wout = ol.weight._capk_pad_bf16 if dt == torch.bfloat16 else ol.weight._capk_pad_master
+        logits_pad = ops.linear(ctx_in, wout, _pad_bias(ol))
+        ctx.m = m
+        ctx.dims = (B, T, D, E, L, V, Vp)
+        ctx.saved = (features, pooled, ids_t, emb, Hs, Cs, CtxT, H, acts, Hd, drops, d_emb, d_out, ctx_in)
+        ctx.logits_pad = logits_pad
+        weights = H.w.permute(1, 0, 2)  # [B, T, S] (decoders.py:226-232)
+        return logits_pad[:, :V].view(B, T, V), weights
+
+    @staticmethod
+    def backward(ctx, dlogits, dweights):
+        m = ctx.m
+        dt = m.cdtype
+        B, T, D, E, L, V, Vp = ctx.dims
+        features, pooled, ids_t, emb, Hs, Cs, CtxT, H, acts, Hd, drops, d_emb, d_out, ctx_in = ctx.saved
+        ctx.saved = None
+        dev = pooled.device
+        lstm, att = m.lstm, m.attention
+        ol = m.output_layer
+        wout = ol.weight._capk_pad_bf16 if dt == torch.bfloat16 else ol.weight._capk_pad_master
+        if dlogits is None:
+            raise RuntimeError("capk LSTMDecoder: backward needs the logits gradient")
+        dl = _padded_grad(dlogits, ctx.logits_pad, B * T, V, Vp)
+        ctx.logits_pad = None
+        ops.linear_dw(dl, ctx_in, ol.weight._capk_pad_grad)
+        ops.colsum(dl, _pad_bias_grad(ol))
+        dctx_b = ops.linear_dx(dl, wout)  # [B*T, D]
+        if d_out[0] > 0:
+            dctx_b = ops.dropout_apply(dctx_b, d_out)
+        idxT = torch.arange(T, dtype=torch.int32, device=dev)
+        idxB = torch.arange(B, dtype=torch.int32, device=dev)
+        dCtxT = torch.empty(T, B, D, dtype=dt, device=dev)  # t-major copy of the output gradient
+        ops.gather_rows(dctx_b, idxB, dCtxT, T, B, D, T * D, D, D, B * D)
+        att.begin_bwd(H)
+        dh = [torch.zeros(B, D, dtype=dt, device=dev) for _ in range(L)]
+        dc = [torch.zeros(B, D, dtype=torch.float32, device=dev) for _ in range(L)]
+        dG = [torch.empty(T, B, 4 * D, dtype=dt, device=dev) for _ in range(L)]
+        dEmb = torch.empty(T, B, E, dtype=dt, device=dev)
+        dctx_carry = torch.empty(B, D, dtype=dt, device=dev)
+        dh_tot = torch.empty(B, D, dtype=dt, device=dev)
+        w_ih0 = W(lstm.weight_ih_l0, dt)
+        for t in range(T - 1, -1, -1):
+            dctx_t = dCtxT[t] if t == T - 1 else dctx_carry
+            # attention: d(query) + recurrent grad of the top layer
+            att.step_bwd(H, t, dctx_t, dh_tot, dq_residual=dh[L - 1], dc_mem_out=dc[L - 1])
+            for layer in range(L - 1, -1, -1):
+                src = dh_tot if layer == L - 1 else dh_below
+                ops.lstm_cell_bwd(acts[layer][t], Cs[layer][t], src, dc[layer], dG[layer][t])
+                # recurrent state gradient for step t-1
+                dnext = torch.empty(B, D, dtype=dt, device=dev)
+                ops.linear_dx(dG[layer][t], W(lstm.w("weight_hh", layer), dt), out=dnext)
+                if layer > 0:
+                    # input gradient -> layer below's output at step t (dropout mask of the forward copy)
+                    dh_below = torch.empty(B, D, dtype=dt, device=dev)
+                    ops.gemm(dG[layer][t], True, W(lstm.w("weight_ih", layer), dt), False, B, D, 4 * D, dh_below,
+                             lda=4 * D, ldb=D, ldc=D, residual=dh[layer - 1], ldr=D,
+                             drop=drops[t][layer - 1] if Hd is not None else ops.NO_DROP)
+                else:
+                    ops.gemm(dG[0][t], True, w_ih0[:, :E], False, B, E, 4 * D, dEmb[t], lda=4 * D, ldb=E + D, ldc=E)
+                    if t > 0:
+                        ops.gemm(dG[0][t], True, w_ih0[:, E:], False, B, D, 4 * D, dctx_carry, lda=4 * D,
+                                 ldb=E + D, ldc=D, residual=dCtxT[t - 1], ldr=D)
+                dh[layer] = dnext
+        # batched weight gradients over all steps
+        for layer in range(L):
+            g = dG[layer].view(T * B, 4 * D)
+            ops.linear_dw(g, Hs[layer][:T].reshape(T * B, D), G(lstm.w("weight_hh", layer)))
+            ops.colsum(g, G(lstm.w("bias_hh", layer)))
+            ops.colsum(g, G(lstm.w("bias_ih", layer)))
+            if layer == 0:
+                gw = G(lstm.weight_ih_l0)
+                ops.gemm(g, False, emb, False, 4 * D, E, T * B, gw, lda=4 * D, ldb=E, ldc=E + D)
+                ops.gemm(g, False, CtxT[:T].reshape(T * B, D), False, 4 * D, D, T * B, gw[:, E:], lda=4 * D, ldb=D,
+                         ldc=E + D)
+            else:
+                xin = Hd[layer - 1] if Hd is not None else Hs[layer - 1][1:]
+                ops.linear_dw(g, xin.reshape(T * B, D), G(lstm.w("weight_ih", layer)))
+        dfeat, _ = att.finish_bwd(H, Hs[L - 1][1:].reshape(T * B, D))
+        # embeddings (padding_idx row excluded, decoders.py:92-94)
+        ops.zero_(G(m.embedding.weight))
+        ops.embedding_bwd(ids_t, dEmb.view(T * B, E), m.pad_token_id, G(m.embedding.weight), None, 0, drop=d_emb)
+        # initial states -> init_h / init_c -> pooled
+        dh0 = torch.empty(B, L * D, dtype=dt, device=dev)
+        dc0 = torch.empty(B, L * D, dtype=dt, device=dev)
+        for layer in range(L):
+            ops.copy_rows(dh[layer], dh0[:, layer * D:(layer + 1) * D])
+            if dt == torch.float32:
+                ops.copy_rows(dc[layer], dc0[:, layer * D:(layer + 1) * D])
+            else:
+                tmp = torch.empty(B, D, dtype=dt, device=dev)
+                ops.cast(dc[layer], tmp)
+                ops.copy_rows(tmp, dc0[:, layer * D:(layer + 1) * D])
+        ops.linear_dw(dh0, pooled, G(m.init_h.weight))
+        ops.colsum(dh0, G(m.init_h.bias))
+        ops.linear_dw(dc0, pooled, G(m.init_c.weight))
+        ops.colsum(dc0, G(m.init_c.bias))
+        dpooled = ops.linear_dx(dh0, W(m.init_h.weight, dt))
+        ops.linear_dx(dc0, W(m.init_c.weight, dt), out=dpooled, beta=1.0)
+        return dfeat, dpooled, None, None, None
+
+
+@torch.no_grad()
+def lstm_greedy(m, features, pooled, max_length, start_token_id):
+    """LSTMDecoder.generate (decoders.py:236-314): ids[:, t] = current token (starting
+    at start_token_id), next = argmax(output_layer(ctx)); no EOS stop, no dropout."""
+    dt = m.cdtype
+    dev = pooled.device
+    B = pooled.shape[0]
+    D, E, L, V = m.hidden_dim, m.embedding_dim, m.num_layers, m.vocab_size
+    lstm, att = m.lstm, m.attention
+    pooled = pooled.contiguous()
+    h0 = ops.linear(pooled, W(m.init_h.weight, dt), m.init_h.bias.detach())
+    c0 = ops.linear(pooled, W(m.init_c.weight, dt), m.init_c.bias.detach(), out_dtype=torch.float32)
+    hs = [[torch.empty(B, D, dtype=dt, device=dev) for _ in range(2)] for _ in range(L)]
+    cs = [[torch.empty(B, D, dtype=torch.float32, device=dev) for _ in range(2)] for _ in range(L)]
+    for layer in range(L):
+        ops.copy_rows(h0[:, layer * D:(layer + 1) * D], hs[layer][0])
+        ops.copy_rows(c0[:, layer * D:(layer + 1) * D], cs[layer][0])
+    H = att.hoist(features, features, None, max_length)
+    ids = torch.zeros(B, max_length, dtype=torch.long, device=dev)
+    cur = torch.full((B,), start_token_id, dtype=torch.long, device=dev)
+    ctx = [torch.zeros(B, D, dtype=dt, device=dev), torch.empty(B, D, dtype=dt, device=dev)]
+    gates = torch.empty(B, 4 * D, dtype=dt, device=dev)
+    act = torch.empty(B, 4 * D, dtype=dt, device=dev)
+    w_ih0 = W(lstm.weight_ih_l0, dt)
+    ol = m.output_layer
+    wout = ol.weight._capk_pad_bf16 if dt == torch.bfloat16 else ol.weight._capk_pad_master
+    for t in range(max_length):
+        ids[:, t].copy_(cur)
+        a, b = t % 2, (t + 1) % 2
+        emb = ops.embedding_fwd(cur.view(B, 1), m.embedding.weight.detach(), None, 0, dt)
+        for layer in range(L):
+            if layer == 0:
+                ops.linear(emb, w_ih0[:, :E], lstm.bias_ih_l0.detach(), out=gates)
+                ops.gemm(ctx[a], True, w_ih0[:, E:], True, B, 4 * D, D, gates, lda=D, ldb=E + D, ldc=4 * D,
+                         beta=1.0)
+            else:
+                ops.linear(hs[layer - 1][b], W(lstm.w("weight_ih", layer), dt), lstm.w("bias_ih", layer).detach(),
+                           out=gates)
+            ops.gemm(hs[layer][a], True, W(lstm.w("weight_hh", layer), dt), True, B, 4 * D, D, gates, lda=D, ldb=D,
+                     ldc=4 * D, beta=1.0, bias=lstm.w("bias_hh", layer).detach())
+            ops.lstm_cell_fwd(gates, cs[layer][a], cs[layer][b], hs[layer][b], act)
+        att.step_fwd(H, t, hs[L - 1][b], hs[L - 1][b], cs[L - 1][b], ctx[b])
+        logits = ops.linear(ctx[b], wout, _pad_bias(ol))
+        ops.argmax_rows(logits, V, cur)
+    return ids, {"attention_weights": H.w.permute(1, 0, 2)}

@@ -356,3 +356,40 @@ def dropout_apply(x, drop, out=None):
 def add_rows(x, y, groups, rows, cols, gsx, ldx, nseg, seg, gsy, ldy, accumulate, x_off=0):
     check(lib().capk_add_rows(dtype_code(x), groups, rows, cols, x.data_ptr() + x_off * x.element_size(), gsx, ldx,
                               nseg, seg, _p(y), gsy, ldy, int(accumulate), _stream()), "capk_add_rows")
+
+
+# ------------------------------------------------------------ LSTM decoder ---
+def lstm_cell_fwd(gates, c_prev, c_out, h_out, act, h_drop=None, drop=NO_DROP):
+    B, D = c_prev.shape
+    check(lib().capk_lstm_cell_fwd(dtype_code(gates), B, D, _p(gates), gates.stride(0), _p(c_prev), _p(c_out),
+                                   _p(h_out), h_out.stride(0), _p(h_drop), h_drop.stride(0) if h_drop is not None else 0,
+                                   _p(act), float(drop[0]), int(drop[1]) & 0xFFFFFFFF, _stream()), "capk_lstm_cell_fwd")
+
+
+def lstm_cell_bwd(act, c_prev, dh, dc, dgates):
+    B, D = c_prev.shape
+    check(lib().capk_lstm_cell_bwd(dtype_code(act), B, D, _p(act), _p(c_prev), _p(dh), dh.stride(0), _p(dc),
+                                   _p(dgates), _stream()), "capk_lstm_cell_bwd")
+
+
+def soft_attn_fwd(qp, kp, v, we, be, inv_temp, ctx, w_out, key_pad=None):
+    """qp [B,D]; kp, v: [B,S,D] views (row strides free); ctx [B,D] view; w_out fp32 [B,S]."""
+    B, S, D = kp.shape
+    check(lib().capk_soft_attn_fwd(dtype_code(qp), B, S, D, _p(qp), qp.stride(0), _p(kp), kp.stride(0), kp.stride(1),
+                                   _p(v), v.stride(0), v.stride(1), _p(we), _p(be), float(inv_temp), _p(key_pad),
+                                   _p(ctx), ctx.stride(0), _p(w_out), _stream()), "capk_soft_attn_fwd")
+
+
+def soft_attn_bwd(qp, kp, v, we, inv_temp, w, dctx, dqp, dkp, dv, dwe_part, dbe_part):
+    B, S, D = kp.shape
+    check(lib().capk_soft_attn_bwd(dtype_code(qp), B, S, D, _p(qp), qp.stride(0), _p(kp), kp.stride(0), kp.stride(1),
+                                   _p(v), v.stride(0), v.stride(1), _p(we), float(inv_temp), _p(w), _p(dctx),
+                                   dctx.stride(0), _p(dqp), dqp.stride(0), _p(dkp), _p(dv), _p(dwe_part),
+                                   _p(dbe_part), _stream()), "capk_soft_attn_bwd")
+
+
+def argmax_rows(x, V, out):
+    """out[r] (int64 view, any stride) = argmax(x[r, :V])."""
+    check(lib().capk_argmax_rows(dtype_code(x), x.shape[0], V, x.stride(0), _p(x), _p(out), out.stride(0), _stream()),
+          "capk_argmax_rows")
+    return out

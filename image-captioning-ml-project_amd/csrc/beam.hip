@@ -439,6 +439,30 @@ __global__ void gather_rows_kernel(int G, int R, int cols, const int* __restrict
   }
 }
 
+
+// Row-wise argmax over the V valid columns of a padded row (greedy decoding:
+// logits.argmax(dim=-1), first index on ties like torch).
+template <typename T>
+__global__ __launch_bounds__(256) void argmax_rows_kernel(const T* __restrict__ x, int64_t ld, int V,
+                                                          int64_t* __restrict__ out, int64_t out_stride) {
+  const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const T* row = x + (int64_t)r * ld;
+  uint64_t best = 0;
+  for (int i = tid; i < V; i += 256) {
+    const uint64_t k = ckey(to_f32(row[i]), i);
+    best = k > best ? k : best;
+  }
+  best = wave_max_u64(best);
+  __shared__ uint64_t sb[4];
+  if (lane == 0) sb[w] = best;
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t b = sb[0];
+    for (int q = 1; q < 4; ++q) b = sb[q] > b ? sb[q] : b;
+    out[(int64_t)r * out_stride] = (int64_t)(0xFFFFFFFFu - (uint32_t)b);
+  }
+}
+
 static int grid_of(int64_t work) {
   int64_t g = (work + 255) / 256;
   return (int)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
@@ -538,5 +562,19 @@ extern "C" int capk_gather_rows(int dtype, int groups, int rows, int cols, const
                        idx, (const bf16*)x, ldx, gsx, (bf16*)y, ldy, gsy);
   else CAPK_CHECK_ARG(false, "capk_gather_rows: dtype");
   CAPK_LAUNCH_CHECK("gather_rows_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_argmax_rows(int dtype, int rows, int V, int64_t ld, const void* x, int64_t* out, int64_t out_stride,
+                                void* stream) {
+  CAPK_CHECK_ARG(rows > 0 && V > 0 && ld >= V, "capk_argmax_rows: bad sizes");
+  if (dtype == CAPK_F32)
+    hipLaunchKernelGGL(argmax_rows_kernel<float>, dim3(rows), dim3(256), 0, S(stream), (const float*)x, ld, V, out,
+                       out_stride);
+  else if (dtype == CAPK_BF16)
+    hipLaunchKernelGGL(argmax_rows_kernel<bf16>, dim3(rows), dim3(256), 0, S(stream), (const bf16*)x, ld, V, out,
+                       out_stride);
+  else CAPK_CHECK_ARG(false, "capk_argmax_rows: dtype");
+  CAPK_LAUNCH_CHECK("argmax_rows_kernel");
   return CAPK_OK;
 }

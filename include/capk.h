@@ -234,6 +234,10 @@ int capk_beam_step(int dtype, int B, int num_beams, int max_length, int V, int64
 int capk_beam_flags(const void* state, int32_t* flags_out, void* stream);
 int capk_beam_finalize(int B, int num_beams, int max_length, const void* state, int64_t* sequences,
                        float* scores, int32_t* beam_indices, void* stream);
+/* out[r * out_stride] = argmax over the V valid columns of row r (first index on ties,
+ * torch.argmax): greedy decoding (decoders.py:308-309, 480). */
+int capk_argmax_rows(int dtype, int rows, int V, int64_t ld, const void* x, int64_t* out, int64_t out_stride,
+                     void* stream);
 /* y[g][r] = x[g][idx[r]] row gather over G groups (KV-cache reorder after a beam
  * step, all layers in one launch; HF Cache.reorder_cache = index_select on dim 0). */
 int capk_gather_rows(int dtype, int groups, int rows, int cols, const int32_t* idx, const void* x, int64_t ldx,

@@ -1,0 +1,89 @@
+"""LSTM decoder (A6) with the attention modules (A7-A10) on the GPU vs the reference's
+own outputs (tests/golden/lstm_attention.npz, oracle/gen_golden.py): logits, attention
+weights, loss, every parameter gradient, d(features), d(pooled) and greedy ids (fp32);
+bf16 logits within 3e-2; bf16 train-mode steps reduce the loss."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+cuda = pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "lstm_attention.npz")
+VARIANTS = {"soft": ("soft", 1, 0.7)}
+
+
+def _decoder(name, precision):
+    import capk
+    from capk import config as C
+    from capk.models.decoders import build_decoder
+    z = np.load(GOLD, allow_pickle=False)
+    D, L, V, B, T, S, pad = [int(x) for x in z["meta/dims"]]
+    kind, heads, temp = VARIANTS[name]
+    dec = build_decoder(C.DecoderConfig(decoder_type="lstm", hidden_dim=D, num_layers=L, num_heads=heads, dropout=0.1),
+                        C.AttentionConfig(attention_type=kind, num_heads=heads, temperature=temp), V, pad, pad, pad)
+    pre = name + "/p0/"
+    sd = {k[len(pre):]: torch.from_numpy(z[k].copy()) for k in z.files if k.startswith(pre)}
+    dec.load_state_dict(sd, strict=True)
+    capk.prepare(dec, "cuda", precision)
+    dec.eval()
+    return z, dec
+
+
+@cuda
+@pytest.mark.parametrize("name", sorted(VARIANTS))
+def test_lstm_golden_fp32(name):
+    from capk.train import CombinedLoss
+    z, dec = _decoder(name, "fp32")
+    D, L, V, B, T, S, pad = [int(x) for x in z["meta/dims"]]
+    feats = torch.from_numpy(z["in/features"]).cuda().requires_grad_(True)
+    pooled = torch.from_numpy(z["in/pooled"]).cuda().requires_grad_(True)
+    caps = torch.from_numpy(z["in/captions"]).cuda()
+    out = dec({"features": feats, "pooled_features": pooled, "attention_mask": None}, caps)
+    np.testing.assert_allclose(out["logits"].detach().cpu().numpy(), z[name + "/logits"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(out["attention_weights"].detach().cpu().numpy(), z[name + "/attention_weights"],
+                               rtol=1e-4, atol=1e-6)
+    loss = CombinedLoss(pad)(logits=out["logits"], targets=caps)["total_loss"]
+    np.testing.assert_allclose(float(loss), float(z[name + "/loss"][0]), rtol=1e-5)
+    loss.backward()
+    for ref_key, got in ((name + "/dfeatures", feats.grad), (name + "/dpooled", pooled.grad)):
+        ref = z[ref_key]
+        np.testing.assert_allclose(got.cpu().numpy(), ref, rtol=2e-4, atol=2e-4 * float(np.abs(ref).max()),
+                                   err_msg=ref_key)
+    for n, p in dec.named_parameters():
+        key = name + "/grad/" + n
+        ref = z[key]
+        np.testing.assert_allclose(p._capk_grad.cpu().numpy(), ref, rtol=2e-4,
+                                   atol=2e-4 * float(np.abs(ref).max()) + 1e-8, err_msg=n)
+    with torch.no_grad():
+        ids, info = dec.generate({"features": feats.detach(), "pooled_features": pooled.detach()}, 6,
+                                 start_token_id=pad)
+    np.testing.assert_array_equal(ids.cpu().numpy(), z[name + "/greedy_ids"])
+
+
+@cuda
+@pytest.mark.parametrize("name", sorted(VARIANTS))
+def test_lstm_bf16_close_and_trains(name):
+    from capk.train import CapkAdamW, CombinedLoss
+    z, dec = _decoder(name, "bf16")
+    D, L, V, B, T, S, pad = [int(x) for x in z["meta/dims"]]
+    feats = torch.from_numpy(z["in/features"]).cuda().bfloat16()
+    pooled = torch.from_numpy(z["in/pooled"]).cuda().bfloat16()
+    caps = torch.from_numpy(z["in/captions"]).cuda()
+    enc = {"features": feats, "pooled_features": pooled, "attention_mask": None}
+    with torch.no_grad():
+        got = dec(enc, caps)["logits"].float().cpu()
+    ref = torch.from_numpy(z[name + "/logits"])
+    assert float((got - ref).norm() / ref.norm()) < 3e-2
+    dec.train()
+    store = next(iter(dec.parameters()))._capk_store_ref
+    opt = CapkAdamW(store, lr=3e-3, weight_decay=0.01)
+    lf = CombinedLoss(pad)
+    losses = []
+    for _ in range(8):
+        loss = lf(logits=dec(enc, caps)["logits"], targets=caps)["total_loss"]
+        loss.backward()
+        opt.step(lr=3e-3)
+        losses.append(float(loss))
+    assert all(np.isfinite(losses)) and losses[-1] < losses[0] * 0.9, losses
