@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(_HERE, "libcapk.so")
 F32 = 0
 BF16 = 1
 
-ACT_NONE, ACT_GELU_ERF, ACT_GELU_TANH, ACT_QUICK_GELU, ACT_TANH, ACT_RELU = 0, 1, 2, 3, 4, 5
+ACT_NONE, ACT_GELU_ERF, ACT_GELU_TANH, ACT_QUICK_GELU, ACT_TANH, ACT_RELU, ACT_SIGMOID = 0, 1, 2, 3, 4, 5, 6
 ACT_BWD = 16
 
 _c_p = ctypes.c_void_p
@@ -68,7 +68,15 @@ SIGNATURES = {
     "capk_soft_attn_fwd": (_i, [_i, _i, _i, _i, _c_p, _i64, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _c_p, _f, _c_p,
                                 _c_p, _i64, _c_p, _c_p]),
     "capk_soft_attn_bwd": (_i, [_i, _i, _i, _i, _c_p, _i64, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _f, _c_p, _c_p,
-                                _i64, _c_p, _i64, _c_p, _c_p, _c_p, _c_p, _c_p]),
+                                _i64, _c_p, _c_p, _i64, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "capk_ew_mul": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p, _i64, _c_p]),
+    "capk_tanh_gate_fwd": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p, _i64, _c_p]),
+    "capk_tanh_gate_bwd": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p, _i64, _c_p, _i64, _c_p, _i64, _c_p]),
+    "capk_gate_mix_fwd": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p, _c_p, _c_p, _c_p, _i64, _c_p]),
+    "capk_gate_mix_bwd": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p, _c_p, _c_p, _i64, _c_p, _i64, _c_p, _i64,
+                               _c_p, _c_p, _c_p]),
+    "capk_attention_probs_mean": (_i, [_i, _i, _i, _i, _i, _i, _f, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _c_p,
+                                       _c_p, _c_p]),
     "capk_beam_state_bytes": (_sz, [_i, _i, _i]),
     "capk_beam_init": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _sz, _c_p]),
     "capk_beam_step": (_i, [_i, _i, _i, _i, _i, _i64, _c_p, _i, _i64, _f, _f, _i, _c_p, _sz, _c_p, _c_p, _c_p]),

@@ -19,9 +19,15 @@ contract (one query per image) via the same protocol.
 import torch
 import torch.nn as nn
 
+from .. import _lib as ops_act_lib
 from .. import ops
 from ..config import AttentionConfig, AttentionType
 from .common import G, CapkModule, W
+
+
+class ops_act:  # activation codes of the GEMM epilogue / act_bwd
+    TANH = ops_act_lib.ACT_TANH
+    SIGMOID = ops_act_lib.ACT_SIGMOID
 
 
 class AttentionMechanism(nn.Module):
@@ -87,11 +93,12 @@ class SoftAttention(AttentionMechanism, CapkModule):
         H.dbe = torch.zeros(B, dtype=torch.float32, device=dev)
         H.dqp = torch.empty_like(H.qp)
 
-    def step_bwd(self, H, t, dctx, dq_out, dq_residual=None, dc_mem_out=None):
-        """Writes dq_out = d(query) (+ dq_residual).  Soft attention does not read the LSTM states."""
+    def step_bwd(self, H, t, dctx, dq_out, dq_residual=None, dc_mem_out=None, dw=None):
+        """Writes dq_out = d(query) (+ dq_residual).  Soft attention does not read the LSTM states.
+        dw: optional gradient on the returned weights (fp32 [B, S])."""
         dt = self.cdtype
         ops.soft_attn_bwd(H.qp[t], H.kp.view(H.B, H.S, H.D), self._v(H), self.energy.weight.detach().view(-1),
-                          1.0 / self.temperature, H.w[t], dctx, H.dqp[t], H.dkp, H.dv, H.dwe, H.dbe)
+                          1.0 / self.temperature, H.w[t], dctx, H.dqp[t], H.dkp, H.dv, H.dwe, H.dbe, dw_in=dw)
         ops.gemm(H.dqp[t], True, W(self.query_proj.weight, dt), False, H.B, H.D, H.D, dq_out, lda=H.D,
                  ldb=H.D, ldc=dq_out.stride(0), residual=dq_residual,
                  ldr=dq_residual.stride(0) if dq_residual is not None else 0)
@@ -153,14 +160,24 @@ class _StandaloneFn(torch.autograd.Function):
         w = mod.step_fwd(H, 0, q, h_mem, c_mem, out)
         ctx_.mod, ctx_.H, ctx_.q, ctx_.same = mod, H, q, same
         ctx_.shapes = (key.shape, value.shape)
-        return out, w.clone()
+        w = w.clone()
+        if not isinstance(mod, SoftAttention):
+            ctx_.mark_non_differentiable(w)
+        return out, w
 
     @staticmethod
     def backward(ctx_, dout, dw):
         mod, H, q = ctx_.mod, ctx_.H, ctx_.q
         mod.begin_bwd(H)
         dq = torch.empty_like(q)
-        mod.step_bwd(H, 0, dout.contiguous(), dq)
+        if dout is None:
+            dout = torch.zeros_like(q)
+        if isinstance(mod, SoftAttention):
+            mod.step_bwd(H, 0, dout.contiguous(), dq, dw=dw.float().contiguous() if dw is not None else None)
+        else:
+            # MultiHeadAttention / AoA return head-averaged weights for inspection; like the LSTM decoder's
+            # use of them, they carry no gradient here (a loss on them needs the soft module)
+            mod.step_bwd(H, 0, dout.contiguous(), dq)
         dk, dv = mod.finish_bwd(H, q)
         if ctx_.same:
             return dq, dk, None, None, None, None, None, None
@@ -168,7 +185,9 @@ class _StandaloneFn(torch.autograd.Function):
 
 
 class MultiHeadAttention(AttentionMechanism, CapkModule):
-    """attention.py:121-218 (parameters; the LSTM step path is row A8)."""
+    """attention.py:121-218: q/k/v/o projections, softmax(q k^T / (T sqrt(hd))),
+    masked_fill(-1e9) (the fused kernel uses -inf: identical unless every key of an image
+    is padded), returned weights = mean over heads."""
 
     def __init__(self, config: AttentionConfig):
         super().__init__()
@@ -182,15 +201,99 @@ class MultiHeadAttention(AttentionMechanism, CapkModule):
         self.value_proj = nn.Linear(self.hidden_dim, self.hidden_dim)
         self.output_proj = nn.Linear(self.hidden_dim, self.hidden_dim)
 
-    def hoist(self, *a, **k):
-        raise NotImplementedError("capk: MultiHeadAttention inside the LSTM decoder (SURVEY A8) is next")
+    def hoist(self, keys, values, key_pad, steps):
+        dt = self.cdtype
+        H = _Hoist()
+        H.keys = _compact(keys)
+        H.values = _compact(values) if values is not keys else None
+        B, S, D = H.keys.shape
+        H.B, H.S, H.D, H.key_pad, H.kpu = B, S, D, key_pad, None
+        dev = keys.device
+        H.kh = ops.linear(H.keys.view(B * S, D), W(self.key_proj.weight, dt), self.key_proj.bias.detach())
+        vals = (H.values if H.values is not None else H.keys).view(B * S, D)
+        H.vh = ops.linear(vals, W(self.value_proj.weight, dt), self.value_proj.bias.detach())
+        H.qh = torch.empty(steps, B, D, dtype=dt, device=dev)
+        H.o = torch.empty(steps, B, D, dtype=dt, device=dev)
+        H.w = torch.empty(steps, B, S, dtype=torch.float32, device=dev)
+        H.lse = [None] * steps
+        H.scale = 1.0 / (self.temperature * self.head_dim ** 0.5)
+        return H
+
+    def _views(self, H, t):
+        B, S, D = H.B, H.S, H.D
+        return (ops.HeadView(H.qh[t], 0, D, D), ops.HeadView(H.kh, 0, S * D, D), ops.HeadView(H.vh, 0, S * D, D),
+                ops.HeadView(H.o[t], 0, D, D))
+
+    def step_fwd(self, H, t, q, h_mem, c_mem, ctx_out):
+        dt = self.cdtype
+        ops.linear(q, W(self.query_proj.weight, dt), self.query_proj.bias.detach(), out=H.qh[t])
+        qv, kv, vv, ov = self._views(H, t)
+        H.lse[t], H.kpu = ops.attention_fwd(qv, kv, vv, ov, H.B, self.num_heads, 1, H.S, self.head_dim, H.scale,
+                                            key_pad=H.key_pad)
+        ops.attention_probs_mean(qv, kv, H.lse[t], H.B, self.num_heads, 1, H.S, self.head_dim, H.scale, H.w[t],
+                                 key_pad=H.kpu)
+        ops.linear(H.o[t], W(self.output_proj.weight, dt), self.output_proj.bias.detach(), out=ctx_out)
+        return H.w[t]
+
+    def begin_bwd(self, H):
+        B, S, D, dev, dt = H.B, H.S, H.D, H.kh.device, self.cdtype
+        H.dK = torch.zeros(B * S, D, dtype=torch.float32, device=dev)
+        H.dV = torch.zeros(B * S, D, dtype=torch.float32, device=dev)
+        H.sk = torch.empty(B * S, D, dtype=dt, device=dev)
+        H.sv = torch.empty(B * S, D, dtype=dt, device=dev)
+        H.dqh = torch.empty_like(H.qh)
+        H.dctx = torch.empty_like(H.o)
+        H.do = torch.empty(B, D, dtype=dt, device=dev)
+
+    def step_bwd(self, H, t, dctx, dq_out, dq_residual=None, dc_mem_out=None):
+        dt = self.cdtype
+        B, S, D = H.B, H.S, H.D
+        ops.copy_rows(dctx, H.dctx[t])
+        ops.linear_dx(dctx, W(self.output_proj.weight, dt), out=H.do)
+        qv, kv, vv, ov = self._views(H, t)
+        ops.attention_bwd(qv, kv, vv, ov, ops.HeadView(H.do, 0, D, D), H.lse[t], ops.HeadView(H.dqh[t], 0, D, D),
+                          ops.HeadView(H.sk, 0, S * D, D), ops.HeadView(H.sv, 0, S * D, D), B, self.num_heads, 1, S,
+                          self.head_dim, H.scale, key_pad_u8=H.kpu)
+        ops.add_rows(H.sk, H.dK, 1, B * S, D, 0, D, 1, 0, 0, D, True)
+        ops.add_rows(H.sv, H.dV, 1, B * S, D, 0, D, 1, 0, 0, D, True)
+        ops.gemm(H.dqh[t], True, W(self.query_proj.weight, dt), False, B, D, D, dq_out, lda=D, ldb=D,
+                 ldc=dq_out.stride(0), residual=dq_residual,
+                 ldr=dq_residual.stride(0) if dq_residual is not None else 0)
+        return False
+
+    def finish_bwd(self, H, Q):
+        dt = self.cdtype
+        B, S, D = H.B, H.S, H.D
+        steps = H.qh.shape[0]
+        dctx = H.dctx.view(steps * B, D)
+        ops.linear_dw(dctx, H.o.view(steps * B, D), G(self.output_proj.weight))
+        ops.colsum(dctx, G(self.output_proj.bias))
+        dqh = H.dqh.view(steps * B, D)
+        ops.linear_dw(dqh, Q, G(self.query_proj.weight))
+        ops.colsum(dqh, G(self.query_proj.bias))
+        outs = []
+        for acc, proj, x in ((H.dK, self.key_proj, H.keys), (H.dV, self.value_proj,
+                                                              H.values if H.values is not None else H.keys)):
+            g = acc
+            if dt != torch.float32:
+                g = torch.empty(B * S, D, dtype=dt, device=acc.device)
+                ops.cast(acc, g)
+            ops.linear_dw(g, x.view(B * S, D), G(proj.weight))
+            ops.colsum(g, G(proj.bias))
+            outs.append(g)
+        dkeys = ops.linear_dx(outs[0], W(self.key_proj.weight, dt))
+        if H.values is None:
+            ops.linear_dx(outs[1], W(self.value_proj.weight, dt), out=dkeys, beta=1.0)
+            return dkeys.view(B, S, D), None
+        return dkeys.view(B, S, D), ops.linear_dx(outs[1], W(self.value_proj.weight, dt)).view(B, S, D)
 
     def forward(self, query, key, value, key_padding_mask=None, **kwargs):
-        raise NotImplementedError("capk: MultiHeadAttention module (SURVEY A8) is next")
+        return _standalone(self, query, key, value, key_padding_mask, kwargs)
 
 
 class AdaptiveAttention(AttentionMechanism, CapkModule):
-    """attention.py:221-294 (parameters; the step path is row A10)."""
+    """attention.py:221-294: visual sentinel s = W_p(sigmoid(W_s [q; h]) * tanh(c)),
+    base attention ctx, beta = sigmoid(W_a [ctx; s]), out = beta ctx + (1 - beta) s."""
 
     def __init__(self, config: AttentionConfig):
         super().__init__()
@@ -200,17 +303,88 @@ class AdaptiveAttention(AttentionMechanism, CapkModule):
         self.sentinel_proj = nn.Linear(self.hidden_dim, self.hidden_dim)
         self.adaptive_weight = nn.Linear(self.hidden_dim * 2, 1)
 
-    def hoist(self, *a, **k):
-        raise NotImplementedError("capk: AdaptiveAttention (SURVEY A10) is next")
+    def hoist(self, keys, values, key_pad, steps):
+        dt = self.cdtype
+        H = _Hoist()
+        H.base = self.base_attention.hoist(keys, values, key_pad, steps)
+        B, D, dev = H.base.B, H.base.D, keys.device
+        H.B, H.D = B, D
+        H.cat1 = torch.empty(steps, B, 2 * D, dtype=dt, device=dev)
+        H.sgpre = torch.empty(steps, B, D, dtype=dt, device=dev)
+        H.sg = torch.empty(steps, B, D, dtype=dt, device=dev)
+        H.sin = torch.empty(steps, B, D, dtype=dt, device=dev)
+        H.cat2 = torch.empty(steps, B, 2 * D, dtype=dt, device=dev)
+        H.beta = torch.empty(steps, B, dtype=torch.float32, device=dev)
+        H.c = [None] * steps
+        return H
+
+    def step_fwd(self, H, t, q, h_mem, c_mem, ctx_out):
+        dt = self.cdtype
+        D = H.D
+        ops.copy_rows(q, H.cat1[t][:, :D])
+        ops.copy_rows(h_mem, H.cat1[t][:, D:])
+        ops.linear(H.cat1[t], W(self.sentinel_gate.weight, dt), self.sentinel_gate.bias.detach(),
+                   act=ops_act.SIGMOID, preact=H.sgpre[t], out=H.sg[t])
+        ops.tanh_gate_fwd(c_mem, H.sg[t], H.sin[t])
+        ops.linear(H.sin[t], W(self.sentinel_proj.weight, dt), self.sentinel_proj.bias.detach(), out=H.cat2[t][:, D:])
+        w = self.base_attention.step_fwd(H.base, t, q, h_mem, c_mem, H.cat2[t][:, :D])
+        ops.gate_mix_fwd(H.cat2[t][:, :D], H.cat2[t][:, D:], self.adaptive_weight.weight.detach().view(-1),
+                         self.adaptive_weight.bias.detach(), H.beta[t], ctx_out)
+        H.c[t] = c_mem
+        H.w = H.base.w
+        return w
+
+    def begin_bwd(self, H):
+        dt, B, D, dev = self.cdtype, H.B, H.D, H.cat1.device
+        self.base_attention.begin_bwd(H.base)
+        steps = H.cat1.shape[0]
+        H.dwa = torch.zeros(2 * D, dtype=torch.float32, device=dev)
+        H.dba = torch.zeros(1, dtype=torch.float32, device=dev)
+        H.dctxb = torch.empty(B, D, dtype=dt, device=dev)
+        H.dsp = torch.empty(steps, B, D, dtype=dt, device=dev)
+        H.dsgpre = torch.empty(steps, B, D, dtype=dt, device=dev)
+        H.dsg = torch.empty(B, D, dtype=dt, device=dev)
+
+    def step_bwd(self, H, t, dctx, dq_out, dq_residual=None, dc_mem_out=None):
+        dt = self.cdtype
+        B, D = H.B, H.D
+        ops.gate_mix_bwd(H.cat2[t][:, :D], H.cat2[t][:, D:], self.adaptive_weight.weight.detach().view(-1),
+                         H.beta[t], dctx, H.dctxb, H.dsp[t], H.dwa, H.dba)
+        dsin = ops.linear_dx(H.dsp[t], W(self.sentinel_proj.weight, dt))
+        if dc_mem_out is None:
+            raise RuntimeError("AdaptiveAttention needs the cell-state gradient buffer")
+        ops.tanh_gate_bwd(H.c[t], H.sg[t], dsin, H.dsg, dc_mem_out)
+        ops.act_bwd(H.dsg, H.sgpre[t], ops_act.SIGMOID, out=H.dsgpre[t])
+        self.base_attention.step_bwd(H.base, t, H.dctxb, dq_out, dq_residual)
+        wsg = W(self.sentinel_gate.weight, dt)  # [D, 2D]: query half and memory-state half both feed h_top
+        for half in (wsg[:, :D], wsg[:, D:]):
+            ops.gemm(H.dsgpre[t], True, half, False, B, D, D, dq_out, lda=D, ldb=2 * D, ldc=dq_out.stride(0),
+                     beta=1.0)
+        return True
+
+    def finish_bwd(self, H, Q):
+        B, D = H.B, H.D
+        steps = H.cat1.shape[0]
+        g = H.dsgpre.view(steps * B, D)
+        ops.linear_dw(g, H.cat1.view(steps * B, 2 * D), G(self.sentinel_gate.weight))
+        ops.colsum(g, G(self.sentinel_gate.bias))
+        g = H.dsp.view(steps * B, D)
+        ops.linear_dw(g, H.sin.view(steps * B, D), G(self.sentinel_proj.weight))
+        ops.colsum(g, G(self.sentinel_proj.bias))
+        ops.copy_rows(H.dwa.view(1, 2 * D), G(self.adaptive_weight.weight))
+        ops.add_rows(H.dba, G(self.adaptive_weight.bias), 1, 1, 1, 0, 0, 1, 1, 0, 0, False)
+        return self.base_attention.finish_bwd(H.base, Q)
 
     def forward(self, query, key, value, key_padding_mask=None, memory_state=None, cell_state=None, **kwargs):
         assert memory_state is not None and cell_state is not None, \
             "AdaptiveAttention requires memory_state and cell_state"
-        raise NotImplementedError("capk: AdaptiveAttention (SURVEY A10) is next")
+        raise NotImplementedError("capk AdaptiveAttention: standalone use outside the LSTM decoder is not supported; "
+                                  "the decoder path runs the step protocol")
 
 
 class AttentionOnAttention(AttentionMechanism, CapkModule):
-    """attention.py:297-360 (parameters; the step path is row A9)."""
+    """attention.py:297-360: ctx = base(q, k, v); cat = [ctx; W_q q];
+    out = tanh(W_i cat + b_i) * sigmoid(W_g cat + b_g)."""
 
     def __init__(self, config: AttentionConfig):
         super().__init__()
@@ -220,11 +394,70 @@ class AttentionOnAttention(AttentionMechanism, CapkModule):
         self.info_vector_proj = nn.Sequential(nn.Linear(self.hidden_dim * 2, self.hidden_dim), nn.Tanh())
         self.info_gate_proj = nn.Sequential(nn.Linear(self.hidden_dim * 2, self.hidden_dim), nn.Sigmoid())
 
-    def hoist(self, *a, **k):
-        raise NotImplementedError("capk: AttentionOnAttention (SURVEY A9) is next")
+    def hoist(self, keys, values, key_pad, steps):
+        dt = self.cdtype
+        H = _Hoist()
+        H.base = self.base_attention.hoist(keys, values, key_pad, steps)
+        B, D, dev = H.base.B, H.base.D, keys.device
+        H.B, H.D = B, D
+        mk = lambda n: torch.empty(steps, B, n, dtype=dt, device=dev)  # noqa: E731
+        H.cat, H.ipre, H.info, H.gpre, H.gate = mk(2 * D), mk(D), mk(D), mk(D), mk(D)
+        return H
+
+    def step_fwd(self, H, t, q, h_mem, c_mem, ctx_out):
+        dt = self.cdtype
+        D = H.D
+        w = self.base_attention.step_fwd(H.base, t, q, h_mem, c_mem, H.cat[t][:, :D])
+        ops.linear(q, W(self.query_proj.weight, dt), self.query_proj.bias.detach(), out=H.cat[t][:, D:])
+        iv, ig = self.info_vector_proj[0], self.info_gate_proj[0]
+        ops.linear(H.cat[t], W(iv.weight, dt), iv.bias.detach(), act=ops_act.TANH, preact=H.ipre[t], out=H.info[t])
+        ops.linear(H.cat[t], W(ig.weight, dt), ig.bias.detach(), act=ops_act.SIGMOID, preact=H.gpre[t],
+                   out=H.gate[t])
+        ops.ew_mul(H.info[t], H.gate[t], ctx_out)
+        H.w = H.base.w
+        return w
+
+    def begin_bwd(self, H):
+        dt, B, D, dev = self.cdtype, H.B, H.D, H.cat.device
+        self.base_attention.begin_bwd(H.base)
+        steps = H.cat.shape[0]
+        H.dipre = torch.empty(steps, B, D, dtype=dt, device=dev)
+        H.dgpre = torch.empty(steps, B, D, dtype=dt, device=dev)
+        H.dqa = torch.empty(steps, B, D, dtype=dt, device=dev)
+        H.tmp = torch.empty(B, D, dtype=dt, device=dev)
+        H.dcat = torch.empty(B, 2 * D, dtype=dt, device=dev)
+
+    def step_bwd(self, H, t, dctx, dq_out, dq_residual=None, dc_mem_out=None):
+        dt = self.cdtype
+        B, D = H.B, H.D
+        iv, ig = self.info_vector_proj[0], self.info_gate_proj[0]
+        ops.ew_mul(dctx, H.gate[t], H.tmp)
+        ops.act_bwd(H.tmp, H.ipre[t], ops_act.TANH, out=H.dipre[t])
+        ops.ew_mul(dctx, H.info[t], H.tmp)
+        ops.act_bwd(H.tmp, H.gpre[t], ops_act.SIGMOID, out=H.dgpre[t])
+        ops.linear_dx(H.dipre[t], W(iv.weight, dt), out=H.dcat)
+        ops.linear_dx(H.dgpre[t], W(ig.weight, dt), out=H.dcat, beta=1.0)
+        ops.copy_rows(H.dcat[:, D:], H.dqa[t])
+        self.base_attention.step_bwd(H.base, t, H.dcat[:, :D], dq_out, dq_residual)
+        ops.gemm(H.dqa[t], True, W(self.query_proj.weight, dt), False, B, D, D, dq_out, lda=D, ldb=D,
+                 ldc=dq_out.stride(0), beta=1.0)
+        return False
+
+    def finish_bwd(self, H, Q):
+        B, D = H.B, H.D
+        steps = H.cat.shape[0]
+        cat = H.cat.view(steps * B, 2 * D)
+        for g, lin in ((H.dipre, self.info_vector_proj[0]), (H.dgpre, self.info_gate_proj[0])):
+            g = g.view(steps * B, D)
+            ops.linear_dw(g, cat, G(lin.weight))
+            ops.colsum(g, G(lin.bias))
+        g = H.dqa.view(steps * B, D)
+        ops.linear_dw(g, Q, G(self.query_proj.weight))
+        ops.colsum(g, G(self.query_proj.bias))
+        return self.base_attention.finish_bwd(H.base, Q)
 
     def forward(self, query, key, value, key_padding_mask=None, **kwargs):
-        raise NotImplementedError("capk: AttentionOnAttention (SURVEY A9) is next")
+        return _standalone(self, query, key, value, key_padding_mask, kwargs)
 
 
 def build_attention(config: AttentionConfig) -> AttentionMechanism:

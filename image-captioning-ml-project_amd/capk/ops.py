@@ -380,11 +380,11 @@ def soft_attn_fwd(qp, kp, v, we, be, inv_temp, ctx, w_out, key_pad=None):
                                    _p(ctx), ctx.stride(0), _p(w_out), _stream()), "capk_soft_attn_fwd")
 
 
-def soft_attn_bwd(qp, kp, v, we, inv_temp, w, dctx, dqp, dkp, dv, dwe_part, dbe_part):
+def soft_attn_bwd(qp, kp, v, we, inv_temp, w, dctx, dqp, dkp, dv, dwe_part, dbe_part, dw_in=None):
     B, S, D = kp.shape
     check(lib().capk_soft_attn_bwd(dtype_code(qp), B, S, D, _p(qp), qp.stride(0), _p(kp), kp.stride(0), kp.stride(1),
                                    _p(v), v.stride(0), v.stride(1), _p(we), float(inv_temp), _p(w), _p(dctx),
-                                   dctx.stride(0), _p(dqp), dqp.stride(0), _p(dkp), _p(dv), _p(dwe_part),
+                                   dctx.stride(0), _p(dw_in), _p(dqp), dqp.stride(0), _p(dkp), _p(dv), _p(dwe_part),
                                    _p(dbe_part), _stream()), "capk_soft_attn_bwd")
 
 
@@ -392,4 +392,47 @@ def argmax_rows(x, V, out):
     """out[r] (int64 view, any stride) = argmax(x[r, :V])."""
     check(lib().capk_argmax_rows(dtype_code(x), x.shape[0], V, x.stride(0), _p(x), _p(out), out.stride(0), _stream()),
           "capk_argmax_rows")
+    return out
+
+
+# ------------------------------------------------ attention-module gates ---
+def ew_mul(a, b, out):
+    rows, cols = a.shape
+    check(lib().capk_ew_mul(dtype_code(a), rows, cols, _p(a), a.stride(0), _p(b), b.stride(0), _p(out), out.stride(0),
+                            _stream()), "capk_ew_mul")
+    return out
+
+
+def tanh_gate_fwd(c, g, out):
+    rows, cols = g.shape
+    check(lib().capk_tanh_gate_fwd(dtype_code(g), rows, cols, _p(c), c.stride(0), _p(g), g.stride(0), _p(out),
+                                   out.stride(0), _stream()), "capk_tanh_gate_fwd")
+    return out
+
+
+def tanh_gate_bwd(c, g, dout, dg, dc):
+    rows, cols = g.shape
+    check(lib().capk_tanh_gate_bwd(dtype_code(g), rows, cols, _p(c), c.stride(0), _p(g), g.stride(0), _p(dout),
+                                   dout.stride(0), _p(dg), dg.stride(0), _p(dc), dc.stride(0), _stream()),
+          "capk_tanh_gate_bwd")
+
+
+def gate_mix_fwd(ctx, s, wa, ba, beta, out):
+    B, D = ctx.shape
+    check(lib().capk_gate_mix_fwd(dtype_code(ctx), B, D, _p(ctx), ctx.stride(0), _p(s), s.stride(0), _p(wa), _p(ba),
+                                  _p(beta), _p(out), out.stride(0), _stream()), "capk_gate_mix_fwd")
+    return out
+
+
+def gate_mix_bwd(ctx, s, wa, beta, dout, dctx, ds, dwa, dba):
+    B, D = ctx.shape
+    check(lib().capk_gate_mix_bwd(dtype_code(ctx), B, D, _p(ctx), ctx.stride(0), _p(s), s.stride(0), _p(wa), _p(beta),
+                                  _p(dout), dout.stride(0), _p(dctx), dctx.stride(0), _p(ds), ds.stride(0), _p(dwa),
+                                  _p(dba), _stream()), "capk_gate_mix_bwd")
+
+
+def attention_probs_mean(q, k, lse, B, H, Nq, Nk, hd, scale, out, key_pad=None):
+    check(lib().capk_attention_probs_mean(dtype_code(q.t), B, H, Nq, Nk, hd, float(scale), q.ptr(), q.bs, q.rs,
+                                          k.ptr(), k.bs, k.rs, _p(key_pad), _p(lse), _p(out), _stream()),
+          "capk_attention_probs_mean")
     return out

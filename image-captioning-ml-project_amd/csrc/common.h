@@ -83,6 +83,7 @@ __device__ __forceinline__ float act_fwd(int act, float x) {
     case CAPK_ACT_QUICK_GELU: return x / (1.0f + __expf(-1.702f * x));
     case CAPK_ACT_TANH: return tanhf(x);
     case CAPK_ACT_RELU: return x > 0.f ? x : 0.f;
+    case CAPK_ACT_SIGMOID: return 1.0f / (1.0f + __expf(-x));
     default: return x;
   }
 }
@@ -106,6 +107,7 @@ __device__ __forceinline__ float act_grad(int act, float x) {
     }
     case CAPK_ACT_TANH: { float t = tanhf(x); return 1.0f - t * t; }
     case CAPK_ACT_RELU: return x > 0.f ? 1.f : 0.f;
+    case CAPK_ACT_SIGMOID: { float sg = 1.0f / (1.0f + __expf(-x)); return sg * (1.0f - sg); }
     default: return 1.0f;
   }
 }

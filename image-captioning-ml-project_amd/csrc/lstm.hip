@@ -130,7 +130,8 @@ __global__ __launch_bounds__(256) void soft_attn_bwd_kernel(int S, int D, const 
                                                             const T* __restrict__ v, int64_t v_bs, int64_t v_rs,
                                                             const float* __restrict__ we, float inv_temp,
                                                             const float* __restrict__ wsave, const T* __restrict__ dctx,
-                                                            int64_t lddc, T* __restrict__ dqp, int64_t lddq,
+                                                            int64_t lddc, const float* __restrict__ dw_in,
+                                                            T* __restrict__ dqp, int64_t lddq,
                                                             float* __restrict__ dkp, float* __restrict__ dv,
                                                             float* __restrict__ dwe_part, float* __restrict__ dbe_part) {
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -146,7 +147,7 @@ __global__ __launch_bounds__(256) void soft_attn_bwd_kernel(int S, int D, const 
     float acc = 0.f;
     for (int d = lane; d < D; d += 64) acc += to_f32(g[d]) * to_f32(vr[d]);
     acc = wave_sum(acc);
-    if (lane == 0) de[s] = acc;
+    if (lane == 0) de[s] = acc + (dw_in ? dw_in[(int64_t)b * S + s] : 0.f);
   }
   __syncthreads();
   if (w == 0) {
@@ -237,10 +238,10 @@ extern "C" int capk_soft_attn_fwd(int dtype, int B, int S, int D, const void* qp
 extern "C" int capk_soft_attn_bwd(int dtype, int B, int S, int D, const void* qp, int64_t ldq, const void* kp,
                                   int64_t kp_bs, int64_t kp_rs, const void* v, int64_t v_bs, int64_t v_rs,
                                   const float* we, float inv_temp, const float* w, const void* dctx, int64_t lddc,
-                                  void* dqp, int64_t lddq, float* dkp, float* dv, float* dwe_part, float* dbe_part,
-                                  void* stream) {
+                                  const float* dw_in, void* dqp, int64_t lddq, float* dkp, float* dv, float* dwe_part,
+                                  float* dbe_part, void* stream) {
   CAPK_CHECK_ARG(B > 0 && S > 0 && S <= SA_MAXS && D > 0, "capk_soft_attn_bwd: need 0 < S <= %d", SA_MAXS);
-#define K(T, _) hipLaunchKernelGGL(soft_attn_bwd_kernel<T>, dim3(B), dim3(256), 0, capk::S(stream), S, D, (const T*)qp, ldq, (const T*)kp, kp_bs, kp_rs, (const T*)v, v_bs, v_rs, we, inv_temp, w, (const T*)dctx, lddc, (T*)dqp, lddq, dkp, dv, dwe_part, dbe_part)
+#define K(T, _) hipLaunchKernelGGL(soft_attn_bwd_kernel<T>, dim3(B), dim3(256), 0, capk::S(stream), S, D, (const T*)qp, ldq, (const T*)kp, kp_bs, kp_rs, (const T*)v, v_bs, v_rs, we, inv_temp, w, (const T*)dctx, lddc, dw_in, (T*)dqp, lddq, dkp, dv, dwe_part, dbe_part)
   DT2(dtype, K, 0);
 #undef K
   CAPK_LAUNCH_CHECK("soft_attn_bwd_kernel");

@@ -38,6 +38,7 @@ extern "C" {
 #define CAPK_ACT_QUICK_GELU 3 /* CLIP quick_gelu x*sigmoid(1.702x)                          */
 #define CAPK_ACT_TANH 4       /* ViT pooler                                                 */
 #define CAPK_ACT_RELU 5
+#define CAPK_ACT_SIGMOID 6    /* AoA info gate, adaptive sentinel gate (attention.py:258,318) */
 /* backward forms: out = acc * act'(aux) where aux is the saved pre-activation */
 #define CAPK_ACT_BWD 16
 
@@ -260,14 +261,39 @@ int capk_lstm_cell_bwd(int dtype, int B, int D, const void* act, const float* c_
  * image: e[b,s] = (sum_d we[d] tanh(qp[b,d] + kp[b,s,d]) + be) * inv_temp, key_pad ->
  * -1e9, w = softmax_s(e), ctx[b] = sum_s w[b,s] v[b,s] (w_out fp32 [B,S]).  kp is the
  * hoisted key_proj(keys).  Backward ACCUMULATES (fp32) dkp, dv [B,S,D], dwe_part [B,D],
- * dbe_part [B] over steps and writes dqp.  S <= 256. */
+ * dbe_part [B] over steps and writes dqp; dw_in (optional fp32 [B,S]) is a gradient on
+ * the returned weights.  S <= 256. */
 int capk_soft_attn_fwd(int dtype, int B, int S, int D, const void* qp, int64_t ldq, const void* kp, int64_t kp_bs,
                        int64_t kp_rs, const void* v, int64_t v_bs, int64_t v_rs, const float* we, const float* be,
                        float inv_temp, const uint8_t* key_pad, void* ctx, int64_t ldc, float* w_out, void* stream);
 int capk_soft_attn_bwd(int dtype, int B, int S, int D, const void* qp, int64_t ldq, const void* kp, int64_t kp_bs,
                        int64_t kp_rs, const void* v, int64_t v_bs, int64_t v_rs, const float* we, float inv_temp,
-                       const float* w, const void* dctx, int64_t lddc, void* dqp, int64_t lddq, float* dkp, float* dv,
-                       float* dwe_part, float* dbe_part, void* stream);
+                       const float* w, const void* dctx, int64_t lddc, const float* dw_in, void* dqp, int64_t lddq,
+                       float* dkp, float* dv, float* dwe_part, float* dbe_part, void* stream);
+
+/* ------------------------------------------- attention-module gates (A8-A10) ----
+ * capk_ew_mul: out = a * b (AoA info * gate, attention.py:354).
+ * capk_tanh_gate_fwd/bwd: out = g * tanh(c) with c fp32 (adaptive visual sentinel,
+ * attention.py:258-262); bwd: dg = dout * tanh(c), dc += dout * g * (1 - tanh(c)^2).
+ * capk_gate_mix_fwd/bwd: beta[b] = sigmoid(wa[:D].ctx[b] + wa[D:].s[b] + ba),
+ * out = beta ctx + (1 - beta) s (attention.py:279-285); bwd writes dctx, ds and
+ * ACCUMULATES dwa [2D], dba [1] (fp32 atomics).
+ * capk_attention_probs_mean: out[b,q,s] = mean_h softmax weights rebuilt from the lse
+ * of capk_attention_fwd (MultiHeadAttention's returned weights, attention.py:207-210). */
+int capk_ew_mul(int dtype, int rows, int cols, const void* a, int64_t lda, const void* b, int64_t ldb, void* out,
+                int64_t ldo, void* stream);
+int capk_tanh_gate_fwd(int dtype, int rows, int cols, const float* c, int64_t ldc, const void* g, int64_t ldg,
+                       void* out, int64_t ldo, void* stream);
+int capk_tanh_gate_bwd(int dtype, int rows, int cols, const float* c, int64_t ldc, const void* g, int64_t ldg,
+                       const void* dout, int64_t lddo, void* dg, int64_t lddg, float* dc, int64_t lddc, void* stream);
+int capk_gate_mix_fwd(int dtype, int B, int D, const void* ctx, int64_t ldx, const void* s, int64_t lds,
+                      const float* wa, const float* ba, float* beta, void* out, int64_t ldo, void* stream);
+int capk_gate_mix_bwd(int dtype, int B, int D, const void* ctx, int64_t ldx, const void* s, int64_t lds,
+                      const float* wa, const float* beta, const void* dout, int64_t lddo, void* dctx, int64_t lddx,
+                      void* ds, int64_t ldds, float* dwa, float* dba, void* stream);
+int capk_attention_probs_mean(int dtype, int B, int H, int Nq, int Nk, int hd, float scale, const void* q,
+                              int64_t q_bs, int64_t q_rs, const void* k, int64_t k_bs, int64_t k_rs,
+                              const uint8_t* key_pad, const float* lse, float* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -11,7 +11,8 @@ import torch
 pytestmark = pytest.mark.gpu
 cuda = pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "lstm_attention.npz")
-VARIANTS = {"soft": ("soft", 1, 0.7)}
+VARIANTS = {"soft": ("soft", 1, 0.7), "multi_head": ("multi_head", 4, 1.0), "aoa": ("aoa", 4, 1.0),
+            "adaptive": ("adaptive", 4, 1.0), "adaptive_soft": ("adaptive", 1, 1.0)}
 
 
 def _decoder(name, precision):
@@ -60,6 +61,42 @@ def test_lstm_golden_fp32(name):
         ids, info = dec.generate({"features": feats.detach(), "pooled_features": pooled.detach()}, 6,
                                  start_token_id=pad)
     np.testing.assert_array_equal(ids.cpu().numpy(), z[name + "/greedy_ids"])
+
+
+@cuda
+def test_standalone_attention_modules_fp32():
+    """AttentionMechanism.forward(query, key, value) drop-in contract (attention.py:12-35)
+    for soft / multi_head / aoa against the oracle restatement, with gradients."""
+    import torch.nn.functional as F  # noqa: F401
+    import capk
+    from capk import config as C
+    from capk.models.attention import build_attention
+    from oracle import lstm as olstm
+    torch.manual_seed(3)
+    B, S, D = 3, 9, 64
+    for kind, heads in (("soft", 1), ("multi_head", 4), ("aoa", 4)):
+        cfg = C.AttentionConfig(attention_type=kind, num_heads=heads, temperature=1.3)
+        cfg.hidden_dim = D
+        mod = build_attention(cfg)
+        sd = {k: v.detach().clone() for k, v in mod.state_dict().items()}
+        capk.prepare(mod, "cuda", "fp32")
+        q = torch.randn(B, D).cuda().requires_grad_(True)
+        kv = torch.randn(B, S, D).cuda().requires_grad_(True)
+        ctx, w = mod(q, kv, kv)
+        wl = 1.0 if kind == "soft" else 0.0  # MHA/AoA weights are returned for inspection (no gradient)
+        (ctx.square().sum() + wl * (w * torch.arange(S, device="cuda")).sum()).backward()
+        p = {"attention." + k: v.clone().requires_grad_(True) for k, v in sd.items()}
+        qr = q.detach().cpu().requires_grad_(True)
+        kr = kv.detach().cpu().requires_grad_(True)
+        rc, rw = olstm.attend(kind, p, qr, kr, heads, 1.3, None, None)
+        (rc.square().sum() + wl * (rw * torch.arange(S)).sum()).backward()
+        torch.testing.assert_close(ctx.detach().cpu(), rc.detach(), rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(w.detach().cpu(), rw.detach(), rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(q.grad.cpu(), qr.grad, rtol=1e-3, atol=1e-5)
+        torch.testing.assert_close(kv.grad.cpu(), kr.grad, rtol=1e-3, atol=1e-5)
+        for n, prm in mod.named_parameters():
+            torch.testing.assert_close(prm._capk_grad.cpu(), p["attention." + n].grad, rtol=1e-3, atol=1e-5,
+                                       msg=lambda m: f"{kind} {n}: {m}")
 
 
 @cuda
