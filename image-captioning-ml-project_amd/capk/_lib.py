@@ -54,6 +54,7 @@ SIGNATURES = {
     "capk_embedding_bwd": (_i, [_i, _i, _i, _i, _c_p, _c_p, _i, _c_p, _c_p, _i, _f, _u32, _c_p]),
     "capk_shifted_ce_workspace": (_sz, [_i, _i]),
     "capk_shifted_ce": (_i, [_i, _i, _i, _i, _i64, _c_p, _c_p, _i, _c_p, _c_p, _c_p, _c_p, _sz, _c_p]),
+    "capk_shifted_ce_weighted": (_i, [_i, _i, _i, _i, _i64, _c_p, _c_p, _i, _c_p, _c_p, _c_p, _c_p, _c_p, _sz, _c_p]),
     "capk_zero": (_i, [_c_p, _sz, _c_p]),
     "capk_colsum_workspace": (_sz, [_i, _i]),
     "capk_colsum": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i, _c_p, _sz, _c_p]),
@@ -83,6 +84,7 @@ SIGNATURES = {
     "capk_beam_flags": (_i, [_c_p, _c_p, _c_p]),
     "capk_beam_finalize": (_i, [_i, _i, _i, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "capk_argmax_rows": (_i, [_i, _i, _i, _i64, _c_p, _c_p, _i64, _c_p]),
+    "capk_sample_rows": (_i, [_i, _i, _i, _i64, _c_p, _u32, _i, _c_p, _i64, _c_p, _c_p]),
     "capk_gather_rows": (_i, [_i, _i, _i, _i, _c_p, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p]),
 }
 

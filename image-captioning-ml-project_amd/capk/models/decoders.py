@@ -70,14 +70,25 @@ class TransformerDecoder(TransformerDecoderCore, CaptionDecoder):
                               early_stopping=early_stopping, vocab_size=self.vocab_size)
             return out["sequences"], {"sequences_scores": out["sequences_scores"],
                                       "beam_indices": out["beam_indices"]}
-        ids = torch.full((B, 1), self.bos_token_id, dtype=torch.long, device=feats.device)
-        for _ in range(max_length - 1):
-            logits, _ = self.forward_logits(feats, ids, use_pad_mask=False)
-            nxt = logits[:, -1, :].argmax(dim=-1, keepdim=True)
-            ids = torch.cat([ids, nxt], dim=1)
+        # greedy on the KV-cached decode step: the same per-position arithmetic as the
+        # reference's full re-decode of the prefix (causal attention), argmax kernel
+        from .transformer import KVDecodeRunner
+        from .. import ops
+        runner = KVDecodeRunner(self, feats, 1, max_length)
+        ids = torch.empty(B, max_length, dtype=torch.long, device=feats.device)
+        ids[:, 0] = self.bos_token_id
+        cur = ids[:, 0].contiguous()
+        T = 1
+        for t in range(max_length - 1):
+            logits = runner.step(t + 1, cur, None)
+            nxt = torch.empty(B, dtype=torch.long, device=feats.device)
+            ops.argmax_rows(logits, self.vocab_size, nxt)
+            ids[:, t + 1] = nxt
+            cur = nxt
+            T = t + 2
             if bool((nxt == self.eos_token_id).all()):
                 break
-        return ids, {}
+        return ids[:, :T], {}
 
 
 class LSTMDecoder(LSTMDecoderCore, CaptionDecoder):

@@ -255,16 +255,31 @@ def embedding_bwd(ids, dout, padding_idx, dtable, dpos, pos_offset=0, drop=NO_DR
           "capk_embedding_bwd")
 
 
-def shifted_ce(logits2d, targets, B, T, V, ignore_index, *, want_loss=True, dlogits=None, grad_scale=None):
-    """loss fp32 [2] = (mean, count) if want_loss; fills dlogits (times *grad_scale, a device scalar)."""
+def shifted_ce(logits2d, targets, B, T, V, ignore_index, *, want_loss=True, dlogits=None, grad_scale=None,
+               row_weight=None):
+    """loss fp32 [2] = (mean, count) if want_loss; fills dlogits (times *grad_scale, a device scalar).
+    row_weight (fp32 [B], optional): per-sample weight (SCST advantage)."""
     L = lib()
     loss = torch.empty(2, dtype=torch.float32, device=logits2d.device) if want_loss else None
     wsb = L.capk_shifted_ce_workspace(B, T)
     ws = _ws(wsb, logits2d.device)
-    check(L.capk_shifted_ce(dtype_code(logits2d), B, T, V, logits2d.stride(0), _p(logits2d), _p(targets),
-                            int(ignore_index), _p(grad_scale), _p(loss), _p(dlogits), _p(ws), wsb, _stream()),
-          "capk_shifted_ce")
+    if row_weight is None:
+        check(L.capk_shifted_ce(dtype_code(logits2d), B, T, V, logits2d.stride(0), _p(logits2d), _p(targets),
+                                int(ignore_index), _p(grad_scale), _p(loss), _p(dlogits), _p(ws), wsb, _stream()),
+              "capk_shifted_ce")
+    else:
+        check(L.capk_shifted_ce_weighted(dtype_code(logits2d), B, T, V, logits2d.stride(0), _p(logits2d),
+                                         _p(targets), int(ignore_index), _p(row_weight), _p(grad_scale), _p(loss),
+                                         _p(dlogits), _p(ws), wsb, _stream()), "capk_shifted_ce_weighted")
     return loss
+
+
+def sample_rows(logits, V, seed, step, out, logp=None):
+    """out[r] (int64 view, any stride) ~ Categorical(softmax(logits[r, :V])) with the counter-based uniform."""
+    check(lib().capk_sample_rows(dtype_code(logits), logits.shape[0], V, logits.stride(0), _p(logits),
+                                 int(seed) & 0xFFFFFFFF, int(step), _p(out), out.stride(0), _p(logp), _stream()),
+          "capk_sample_rows")
+    return out
 
 
 def dropout_mask(n, p, seed, offset=0, device="cuda"):

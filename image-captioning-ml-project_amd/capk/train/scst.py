@@ -1,0 +1,210 @@
+"""Self-critical sequence training.
+
+Restates CaptioningTrainer._train_reinforcement_learning / _sample_captions /
+_calculate_rewards (src/train/trainer.py:319-484) with the SURVEY fixes:
+
+* D8  — the advantage is per sample (r_sample - r_baseline) and the loss is the mean of
+        -logp * advantage over the sampled tokens up to and including the first EOS;
+* D9  — the reward is a per-sample CIDEr-D computed here on token ids (pycocoevalcap is
+        absent: parity unpinned, restated from the published metric);
+* sampling — the reference re-runs the full decoder on the prefix every step and keeps the
+        log-prob graph; here the sampler runs the KV-cached decode step without a graph
+        (softmax + inverse-CDF kernel, counter-based uniforms) and ONE teacher-forced
+        forward + backward over the sampled sequence produces the same log-probabilities
+        and gradients.  Sampling and scoring both use generate()'s attention semantics
+        (no key-padding mask inside a generated prefix).
+* baseline — model.generate (greedy for the Transformer decoder, beam-4 for GPT-2), reusing
+        the encoder features of the step instead of re-encoding the images.
+"""
+import math
+from collections import Counter, defaultdict
+
+import numpy as np
+import torch
+
+from .. import ops
+from .losses import _padded_base
+
+PG_IGNORE = -100
+
+
+# --------------------------------------------------------------- CIDEr-D -----
+def _ngrams(tokens, n):
+    return Counter(tuple(tokens[i:i + n]) for i in range(len(tokens) - n + 1))
+
+
+def _cook(tokens, nmax=4):
+    c = Counter()
+    for n in range(1, nmax + 1):
+        c.update(_ngrams(tokens, n))
+    return c
+
+
+def cider_d(candidates, references, n=4, sigma=6.0):
+    """Per-sample CIDEr-D (Vedantam et al. 2015; the pycocoevalcap CiderD scorer):
+    tf-idf n-gram vectors (n = 1..4) with document frequencies over this corpus of
+    references, clipped cosine similarity, Gaussian length penalty (sigma 6), averaged
+    over n and references, x10.  candidates: list of token lists; references: list (per
+    candidate) of lists of token lists."""
+    crefs = [[_cook(r, n) for r in refs] for refs in references]
+    df = defaultdict(float)
+    for refs in crefs:
+        for ng in set(ng for r in refs for ng in r):
+            df[ng] += 1.0
+    ref_len = math.log(float(len(crefs)))
+
+    def vec(cnts):
+        v = [defaultdict(float) for _ in range(n)]
+        norm = [0.0] * n
+        length = 0
+        for ng, tf in cnts.items():
+            k = len(ng) - 1
+            d = math.log(max(1.0, df[ng]))
+            v[k][ng] = float(tf) * (ref_len - d)
+            norm[k] += v[k][ng] ** 2
+            if k == 1:
+                length += tf
+        return v, [math.sqrt(x) for x in norm], length
+
+    def sim(vh, vr, nh, nr, lh, lr):
+        delta = float(lh - lr)
+        val = np.zeros(n)
+        for k in range(n):
+            for ng, c in vh[k].items():
+                val[k] += min(vh[k][ng], vr[k][ng]) * vr[k][ng]
+            if nh[k] != 0 and nr[k] != 0:
+                val[k] /= nh[k] * nr[k]
+            val[k] *= math.e ** (-(delta ** 2) / (2 * sigma ** 2))
+        return val
+
+    scores = np.zeros(len(candidates))
+    for i, (cand, refs) in enumerate(zip(candidates, crefs)):
+        vh, nh, lh = vec(_cook(cand, n))
+        acc = np.zeros(n)
+        for r in refs:
+            vr, nr, lr = vec(r)
+            acc += sim(vh, vr, nh, nr, lh, lr)
+        scores[i] = float(np.mean(acc)) / max(len(refs), 1) * 10.0
+    return scores
+
+
+def strip_special(ids, eos, pad, bos=None):
+    """Token ids of a caption for scoring (tokenizer.decode(skip_special_tokens=True)):
+    drop a leading bos, cut at the first eos, drop pads."""
+    out = []
+    seq = list(ids)
+    if bos is not None and seq and seq[0] == bos:
+        seq = seq[1:]
+    for t in seq:
+        if t == eos:
+            break
+        if t != pad:
+            out.append(int(t))
+    return out
+
+
+# ------------------------------------------------------------- PG loss -------
+class _PGLossFn(torch.autograd.Function):
+    """loss = sum_{b,t counted} w_b * (-log p(target)) / count  (shifted like the CE)."""
+
+    @staticmethod
+    def forward(ctx, logits, targets, weights):
+        B, T, V = logits.shape
+        base = _padded_base(logits)
+        targets = targets.contiguous()
+        w = weights.float().contiguous()
+        loss = ops.shifted_ce(base, targets, B, T, V, PG_IGNORE, want_loss=True, row_weight=w)
+        ctx.save_for_backward(targets, w)
+        ctx.base = base
+        ctx.dims = (B, T, V)
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, dloss):
+        targets, w = ctx.saved_tensors
+        B, T, V = ctx.dims
+        base = ctx.base
+        ctx.base = None
+        dbase = torch.empty_like(base)
+        ops.shifted_ce(base, targets, B, T, V, PG_IGNORE, want_loss=False, dlogits=dbase,
+                       grad_scale=dloss.reshape(1).float().contiguous(), row_weight=w)
+        return dbase[:, :V].view(B, T, V), None, None
+
+
+def pg_targets(sample_ids, eos):
+    """Sampled ids [B, T'] (position 0 = bos) -> CE targets where every token after the first
+    EOS is ignored (the EOS itself is scored) — SURVEY D8 masking."""
+    tgt = sample_ids.clone()
+    is_eos = sample_ids[:, 1:] == eos
+    after = torch.cumsum(is_eos.int(), 1) - is_eos.int() > 0  # strictly after the first eos
+    tgt[:, 1:][after] = PG_IGNORE
+    return tgt
+
+
+def policy_gradient_loss(logits, sample_ids, advantages, eos):
+    return _PGLossFn.apply(logits, pg_targets(sample_ids, eos), advantages)
+
+
+# ------------------------------------------------------------- sampling ------
+@torch.no_grad()
+def sample_captions(decoder, encoder_features, max_length, seed):
+    """_sample_captions (trainer.py:383-438): start from bos, sample from
+    softmax(last logits), stop when every sampled token of a step is EOS.  Returns
+    sampled ids [B, T'+1] (bos first) and the log-probs of the sampled tokens [B, T']."""
+    from ..models.decoders import GPT2Decoder, TransformerDecoder
+    if isinstance(decoder, TransformerDecoder):
+        from ..models.transformer import KVDecodeRunner
+        feats = encoder_features["features"]
+        runner = KVDecodeRunner(decoder, feats, 1, max_length)
+        B, dev = feats.shape[0], feats.device
+    elif isinstance(decoder, GPT2Decoder):
+        from ..models.gpt2 import GPT2KVRunner
+        pooled = encoder_features["pooled_features"]
+        runner = GPT2KVRunner(decoder, pooled, 1, max_length)
+        B, dev = pooled.shape[0], pooled.device
+    else:
+        raise NotImplementedError(f"capk SCST sampler: {type(decoder).__name__} (Transformer / GPT-2 decoders)")
+    ids = torch.empty(B, max_length, dtype=torch.long, device=dev)
+    ids[:, 0] = decoder.bos_token_id
+    logp = torch.empty(max_length - 1, B, dtype=torch.float32, device=dev)
+    cur = ids[:, 0].contiguous()
+    T = 1
+    for t in range(max_length - 1):
+        logits = runner.step(t + 1, cur, None)
+        nxt = torch.empty(B, dtype=torch.long, device=dev)
+        ops.sample_rows(logits, decoder.vocab_size, seed, t, nxt, logp[t])
+        ids[:, t + 1] = nxt
+        cur = nxt
+        T = t + 2
+        if bool((nxt == decoder.eos_token_id).all()):
+            break
+    return ids[:, :T], logp[:T - 1].t()
+
+
+def scst_step(model, images, references, optimizer, lr, max_length=20, seed=0, baseline_kwargs=None):
+    """One SCST update (trainer.py:338-381): encoder forward, sampled captions, baseline
+    captions (model.generate), per-sample CIDEr-D rewards, loss = masked mean of
+    -logp * (r_sample - r_baseline), backward, AdamW step.  references: per image a list
+    of token-id lists.  Returns (loss, mean sample reward, mean baseline reward)."""
+    dec = model.decoder
+    enc = model.encoder(images)
+    enc_nograd = {k: (v.detach() if torch.is_tensor(v) else v) for k, v in enc.items()}
+    ids, _ = sample_captions(dec, enc_nograd, max_length, seed)
+    with torch.no_grad():
+        base_ids, _ = dec.generate(enc_nograd, max_length, **(baseline_kwargs or {}))
+    eos, pad, bos = dec.eos_token_id, dec.pad_token_id, dec.bos_token_id
+    samp = [strip_special(r, eos, pad, bos) for r in ids.cpu().tolist()]
+    base = [strip_special(r, eos, pad, bos) for r in base_ids.cpu().tolist()]
+    refs = [[list(x) for x in rs] for rs in references]
+    r_s, r_b = cider_d(samp, refs), cider_d(base, refs)
+    adv = torch.tensor(r_s - r_b, dtype=torch.float32, device=ids.device)
+    if hasattr(dec, "forward_logits"):
+        from ..models.decoders import GPT2Decoder
+        if isinstance(dec, GPT2Decoder):
+            logits = dec.forward_logits(enc["pooled_features"], ids, use_pad_mask=False)
+        else:
+            logits, _ = dec.forward_logits(enc["features"], ids, use_pad_mask=False)
+    loss = policy_gradient_loss(logits, ids, adv, eos)
+    loss.backward()
+    optimizer.step(lr=lr)
+    return loss.detach(), float(np.mean(r_s)), float(np.mean(r_b))

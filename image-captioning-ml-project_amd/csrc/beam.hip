@@ -463,6 +463,58 @@ __global__ __launch_bounds__(256) void argmax_rows_kernel(const T* __restrict__ 
   }
 }
 
+
+// Categorical sampling from softmax(logits[r, :V]) by inverse CDF with a counter-based
+// uniform u = hash(seed, step<<32 | r) (SCST sampler, trainer.py:383-438 restated: the
+// distribution of torch.distributions.Categorical(softmax(logits)), a reproducible RNG
+// stream instead of torch.multinomial's).  Thread t owns the contiguous columns
+// [t*chunk, (t+1)*chunk); the CDF is the in-order sum of exp(x - max) over threads'
+// chunks (block exclusive scan), so the oracle can restate it exactly.
+__global__ __launch_bounds__(256) void sample_rows_kernel_f32(const float* __restrict__ x0, int64_t ld, int V,
+                                                              uint32_t seed, int step, int64_t* __restrict__ out,
+                                                              int64_t out_stride, float* __restrict__ logp,
+                                                              int is_bf16) {
+  const int r = blockIdx.x, tid = threadIdx.x;
+  const int chunk = (V + 255) / 256;
+  const int lo = tid * chunk, hi = min(V, lo + chunk);
+  const float* xf = x0 + (is_bf16 ? 0 : (int64_t)r * ld);
+  const bf16* xb = (const bf16*)x0 + (is_bf16 ? (int64_t)r * ld : 0);
+  auto X = [&](int i) { return is_bf16 ? (float)xb[i] : xf[i]; };
+  __shared__ float red[4];
+  __shared__ float pre[257];
+  float m = -INFINITY;
+  for (int i = lo; i < hi; ++i) m = fmaxf(m, X(i));
+  m = wave_max(m);
+  if ((tid & 63) == 0) red[tid >> 6] = m;
+  __syncthreads();
+  const float M = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float sl = 0.f;
+  for (int i = lo; i < hi; ++i) sl += __expf(X(i) - M);
+  pre[tid + 1] = sl;
+  __syncthreads();
+  if (tid == 0) {
+    pre[0] = 0.f;
+    for (int t = 1; t <= 256; ++t) pre[t] += pre[t - 1];
+  }
+  __syncthreads();
+  const float S = pre[256];
+  const uint32_t h = drop_hash(seed, ((uint64_t)(uint32_t)step << 32) | (uint32_t)r);
+  const float target = (float)(h >> 8) * (1.0f / 16777216.0f) * S;
+  // the owning thread: pre[t] <= target < pre[t+1]; rounding past the end -> last non-empty chunk
+  const bool own = (pre[tid] <= target && target < pre[tid + 1]) ||
+                   (tid == min(255, (V - 1) / chunk) && target >= pre[tid + 1]);
+  if (own && lo < hi) {
+    float cum = pre[tid];
+    int tok = hi - 1;
+    for (int i = lo; i < hi; ++i) {
+      cum += __expf(X(i) - M);
+      if (cum > target) { tok = i; break; }
+    }
+    out[(int64_t)r * out_stride] = tok;
+    if (logp) logp[r] = (X(tok) - M) - logf(S);
+  }
+}
+
 static int grid_of(int64_t work) {
   int64_t g = (work + 255) / 256;
   return (int)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
@@ -576,5 +628,15 @@ extern "C" int capk_argmax_rows(int dtype, int rows, int V, int64_t ld, const vo
                        out_stride);
   else CAPK_CHECK_ARG(false, "capk_argmax_rows: dtype");
   CAPK_LAUNCH_CHECK("argmax_rows_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_sample_rows(int dtype, int rows, int V, int64_t ld, const void* logits, uint32_t seed, int step,
+                                int64_t* out, int64_t out_stride, float* logp, void* stream) {
+  CAPK_CHECK_ARG(rows > 0 && V > 0 && ld >= V && (dtype == CAPK_F32 || dtype == CAPK_BF16),
+                 "capk_sample_rows: bad arguments");
+  hipLaunchKernelGGL(sample_rows_kernel_f32, dim3(rows), dim3(256), 0, S(stream), (const float*)logits, ld, V, seed,
+                     step, out, out_stride, logp, dtype == CAPK_BF16 ? 1 : 0);
+  CAPK_LAUNCH_CHECK("sample_rows_kernel");
   return CAPK_OK;
 }

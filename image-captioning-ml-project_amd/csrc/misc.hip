@@ -128,7 +128,8 @@ __global__ __launch_bounds__(CE_THREADS) void ce_rows_kernel(int B, int T_, int 
                                                              const T* __restrict__ logits,
                                                              const int64_t* __restrict__ targets, int ignore_index,
                                                              const float* __restrict__ grad_scale, const float* __restrict__ cnt,
-                                                             float* __restrict__ row_loss, T* __restrict__ dlogits) {
+                                                             float* __restrict__ row_loss, T* __restrict__ dlogits,
+                                                             const float* __restrict__ row_weight) {
   __shared__ float red[16];
   const int row = blockIdx.x;
   const int b = row / T_, t = row % T_;
@@ -174,9 +175,10 @@ __global__ __launch_bounds__(CE_THREADS) void ce_rows_kernel(int B, int T_, int 
   }
   s = block_reduce(s, red, false);
   const float lse = mx + __logf(s);
-  if (threadIdx.x == 0 && row_loss) row_loss[row] = lse - tgt_logit;
+  const float rw = row_weight ? row_weight[b] : 1.f;
+  if (threadIdx.x == 0 && row_loss) row_loss[row] = rw * (lse - tgt_logit);
   if (dlogits) {
-    const float scale = (grad_scale ? grad_scale[0] : 1.f) / cnt[0];
+    const float scale = rw * (grad_scale ? grad_scale[0] : 1.f) / cnt[0];
     const float inv = 1.f / s;
 #pragma unroll
     for (int k = 0; k < CE_MAXCH; ++k) {
@@ -466,7 +468,7 @@ extern "C" int capk_embedding_bwd(int dtype, int B, int T, int D, const int64_t*
 
 extern "C" size_t capk_shifted_ce_workspace(int B, int T) { return (size_t)(B * T + 4) * sizeof(float); }
 
-extern "C" int capk_shifted_ce(int dtype, int B, int T, int V, int64_t ld, const void* logits,
+static int shifted_ce_impl(const float* row_weight, int dtype, int B, int T, int V, int64_t ld, const void* logits,
                                const int64_t* targets, int ignore_index, const float* grad_scale, float* loss_out,
                                void* dlogits, void* ws, size_t ws_bytes, void* stream) {
   CAPK_CHECK_ARG(B > 0 && T > 1 && V > 0 && ld >= V && ld % 8 == 0, "capk_shifted_ce: bad shape (ld %% 8)");
@@ -477,7 +479,7 @@ extern "C" int capk_shifted_ce(int dtype, int B, int T, int V, int64_t ld, const
   hipStream_t st = S(stream);
   hipLaunchKernelGGL(ce_count_kernel, dim3(1), dim3(1024), 0, st, B, T, targets, ignore_index, cnt);
   CAPK_LAUNCH_CHECK("ce_count_kernel");
-#define L(T_, _) hipLaunchKernelGGL(ce_rows_kernel<T_>, dim3(B * T), dim3(CE_THREADS), 0, st, B, T, V, ld, (const T_*)logits, targets, ignore_index, grad_scale, cnt, row_loss, (T_*)dlogits)
+#define L(T_, _) hipLaunchKernelGGL(ce_rows_kernel<T_>, dim3(B * T), dim3(CE_THREADS), 0, st, B, T, V, ld, (const T_*)logits, targets, ignore_index, grad_scale, cnt, row_loss, (T_*)dlogits, row_weight)
   DT_DISPATCH(dtype, L, 0)
 #undef L
   CAPK_LAUNCH_CHECK("ce_rows_kernel");
@@ -486,6 +488,22 @@ extern "C" int capk_shifted_ce(int dtype, int B, int T, int V, int64_t ld, const
     CAPK_LAUNCH_CHECK("ce_finish_kernel");
   }
   return CAPK_OK;
+}
+
+extern "C" int capk_shifted_ce(int dtype, int B, int T, int V, int64_t ld, const void* logits,
+                               const int64_t* targets, int ignore_index, const float* grad_scale, float* loss_out,
+                               void* dlogits, void* ws, size_t ws_bytes, void* stream) {
+  return shifted_ce_impl(nullptr, dtype, B, T, V, ld, logits, targets, ignore_index, grad_scale, loss_out, dlogits, ws,
+                         ws_bytes, stream);
+}
+
+extern "C" int capk_shifted_ce_weighted(int dtype, int B, int T, int V, int64_t ld, const void* logits,
+                                        const int64_t* targets, int ignore_index, const float* row_weight,
+                                        const float* grad_scale, float* loss_out, void* dlogits, void* ws,
+                                        size_t ws_bytes, void* stream) {
+  CAPK_CHECK_ARG(row_weight != nullptr, "capk_shifted_ce_weighted: row_weight");
+  return shifted_ce_impl(row_weight, dtype, B, T, V, ld, logits, targets, ignore_index, grad_scale, loss_out, dlogits,
+                         ws, ws_bytes, stream);
 }
 
 extern "C" int capk_cast(int in_dtype, int out_dtype, int64_t n, const void* x, void* y, void* stream) {

@@ -171,6 +171,14 @@ size_t capk_shifted_ce_workspace(int B, int T);
 int capk_shifted_ce(int dtype, int B, int T, int V, int64_t ld, const void* logits,
                     const int64_t* targets, int ignore_index, const float* grad_scale,
                     float* loss_out, void* dlogits, void* ws, size_t ws_bytes, void* stream);
+/* Same with a per-sample weight w[b] on every counted row: loss = sum w_b (-log p) / count,
+ * d logits scaled by w_b — the SCST policy-gradient loss -mean(logp * advantage) over the
+ * unmasked sampled tokens (trainer.py:367-374 with D8: per-sample advantage, masked after
+ * EOS via ignore_index targets). */
+int capk_shifted_ce_weighted(int dtype, int B, int T, int V, int64_t ld, const void* logits,
+                             const int64_t* targets, int ignore_index, const float* row_weight,
+                             const float* grad_scale, float* loss_out, void* dlogits, void* ws, size_t ws_bytes,
+                             void* stream);
 /* hipMemsetAsync(ptr, 0, bytes) on the stream (gradient buffers that are scatter-added). */
 int capk_zero(void* ptr, size_t bytes, void* stream);
 
@@ -239,6 +247,11 @@ int capk_beam_finalize(int B, int num_beams, int max_length, const void* state, 
  * torch.argmax): greedy decoding (decoders.py:308-309, 480). */
 int capk_argmax_rows(int dtype, int rows, int V, int64_t ld, const void* x, int64_t* out, int64_t out_stride,
                      void* stream);
+/* Categorical sample from softmax(logits[r, :V]) by inverse CDF with the counter-based
+ * uniform u = (hash(seed, step<<32 | r) >> 8) / 2^24 (same hash as dropout); out[r*out_stride]
+ * = token, logp[r] (optional) = its log-probability.  SCST sampler (trainer.py:383-438). */
+int capk_sample_rows(int dtype, int rows, int V, int64_t ld, const void* logits, uint32_t seed, int step,
+                     int64_t* out, int64_t out_stride, float* logp, void* stream);
 /* y[g][r] = x[g][idx[r]] row gather over G groups (KV-cache reorder after a beam
  * step, all layers in one launch; HF Cache.reorder_cache = index_select on dim 0). */
 int capk_gather_rows(int dtype, int groups, int rows, int cols, const int32_t* idx, const void* x, int64_t ldx,
