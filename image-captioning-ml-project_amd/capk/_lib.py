@@ -86,6 +86,19 @@ SIGNATURES = {
     "capk_argmax_rows": (_i, [_i, _i, _i, _i64, _c_p, _c_p, _i64, _c_p]),
     "capk_sample_rows": (_i, [_i, _i, _i, _i64, _c_p, _u32, _i, _c_p, _i64, _c_p, _c_p]),
     "capk_gather_rows": (_i, [_i, _i, _i, _i, _c_p, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p]),
+    "capk_im2col": (_i, [_i, _i, _i, _i, _i, _i, _i64, _i64, _i64, _i64, _i, _i, _i, _i, _i, _i, _i, _c_p, _c_p,
+                         _c_p]),
+    "capk_col2im": (_i, [_i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _c_p, _c_p, _f, _c_p]),
+    "capk_bn_workspace": (_sz, [_i, _i]),
+    "capk_bn_stats": (_i, [_i, _i, _i, _c_p, _i64, _f, _f, _c_p, _c_p, _c_p, _c_p, _c_p, _sz, _c_p]),
+    "capk_bn_eval_stats": (_i, [_i, _c_p, _c_p, _f, _c_p, _c_p, _c_p]),
+    "capk_bn_apply": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _c_p, _c_p, _c_p, _c_p, _i64, _i, _c_p, _i64, _c_p]),
+    "capk_bn_bwd": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p, _i64, _c_p, _c_p, _c_p, _c_p, _c_p, _i, _c_p, _i64,
+                         _f, _c_p, _i64, _i, _c_p, _sz, _c_p]),
+    "capk_maxpool_fwd": (_i, [_i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _c_p, _c_p, _c_p, _c_p]),
+    "capk_maxpool_bwd": (_i, [_i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _c_p, _c_p, _c_p, _c_p]),
+    "capk_avgpool_fwd": (_i, [_i, _i, _i, _i, _i, _i, _i, _c_p, _c_p, _i64, _c_p]),
+    "capk_avgpool_bwd": (_i, [_i, _i, _i, _i, _i, _i, _i, _c_p, _i64, _c_p, _f, _c_p]),
 }
 
 _lib = None

@@ -14,6 +14,8 @@ import torch.nn as nn
 
 from ..config import EncoderConfig, EncoderType
 from .clip import CLIP_ARCHS, CapkCLIPVisionModel
+from .common import CapkModule
+from .resnet import RESNET_ARCHS, CapkResNetModel, _ResNetHeadFn
 from .vit import VIT_ARCHS, CapkViTModel
 
 
@@ -85,6 +87,37 @@ class CLIPEncoder(ImageEncoder):
         return {"features": features, "pooled_features": pooled, "attention_mask": mask}
 
 
+class ResNetEncoder(ImageEncoder, CapkModule):
+    """encoders.py:37-91 on libcapk kernels.  Restated per SURVEY §0.1 D6:
+    the reference applies Linear(2048->768) to the NCHW map (shape error) and returns
+    the unprojected pooler output; here features = proj(flattened map) [B, h*w, D] and
+    pooled = proj(avg-pooled map) [B, D], mirroring the ViT/CLIP encoders."""
+
+    def __init__(self, config: EncoderConfig, arch=None):
+        super().__init__()
+        name = config.pretrained_model_name or "microsoft/resnet-50"  # encoders.py:42-44
+        if arch is None:
+            if name not in RESNET_ARCHS:
+                raise ValueError(f"capk ResNetEncoder: unknown architecture '{name}' (known: {sorted(RESNET_ARCHS)})")
+            arch = RESNET_ARCHS[name]
+        self.model = CapkResNetModel(arch)
+        self.feature_dim = config.feature_dim
+        hidden = arch["hidden_sizes"][-1]
+        if hidden == self.feature_dim:
+            raise NotImplementedError("capk ResNetEncoder: identity projection (hidden == feature_dim) not wired")
+        self.proj = nn.Linear(hidden, self.feature_dim)  # encoders.py:50-54
+        if config.freeze:
+            for p in self.model.parameters():
+                p.requires_grad = False
+
+    def forward(self, images):
+        x, (B, H, W) = self.model(images)
+        feats, pooled = _ResNetHeadFn.apply(x, self.proj.weight, self, B, H, W)
+        features = feats.view(B, H * W, self.feature_dim)
+        mask = torch.ones(B, H * W, dtype=torch.bool, device=images.device)  # D4 restatement
+        return {"features": features, "pooled_features": pooled, "attention_mask": mask}
+
+
 def build_encoder(config: EncoderConfig) -> ImageEncoder:
     """encoders.py:299-312 (with D2: string types accepted)."""
     et = config.encoder_type if isinstance(config.encoder_type, EncoderType) else EncoderType(config.encoder_type)
@@ -92,6 +125,8 @@ def build_encoder(config: EncoderConfig) -> ImageEncoder:
         return ViTEncoder(config)
     if et == EncoderType.CLIP:
         return CLIPEncoder(config)
-    if et in (EncoderType.RESNET, EncoderType.SWIN):
-        raise NotImplementedError(f"capk: encoder '{et.value}' is scheduled after the ViT hot path (SURVEY §8)")
+    if et == EncoderType.RESNET:
+        return ResNetEncoder(config)
+    if et == EncoderType.SWIN:
+        raise NotImplementedError("capk: Swin is out of the hot-path scope (SURVEY §2, §8f-4)")
     raise ValueError(f"Unsupported encoder type: {config.encoder_type}")

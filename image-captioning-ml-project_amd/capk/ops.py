@@ -451,3 +451,116 @@ def attention_probs_mean(q, k, lse, B, H, Nq, Nk, hd, scale, out, key_pad=None):
                                           k.ptr(), k.bs, k.rs, _p(key_pad), _p(lse), _p(out), _stream()),
           "capk_attention_probs_mean")
     return out
+
+
+# ------------------------------------------------- convolutional encoder (A3) ---
+def conv_out_hw(H, W, k, stride, pad):
+    return (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+
+
+def im2col(x, B, H, W, C, k, stride, pad, Kp, out_dtype, strides=None, out=None):
+    """Channels-last im2col panel [B*OH*OW, Kp] (k order kh, kw, c).  `strides` =
+    element strides (sb, sh, sw, sc) of x; default = contiguous NHWC rows."""
+    _need_gpu(x)
+    OH, OW = conv_out_hw(H, W, k, stride, pad)
+    if strides is None:
+        strides = (H * W * C, W * C, C, 1)
+    if out is None:
+        out = torch.empty(B * OH * OW, Kp, dtype=out_dtype, device=x.device)
+    check(lib().capk_im2col(dtype_code(x), dtype_code(out), B, H, W, C, *[int(s) for s in strides], k, k, stride,
+                            pad, OH, OW, Kp, _p(x), _p(out), _stream()), "capk_im2col")
+    return out
+
+
+def col2im(dcol, dx, B, H, W, C, k, stride, pad, Kp, beta=0.0):
+    OH, OW = conv_out_hw(H, W, k, stride, pad)
+    check(lib().capk_col2im(dtype_code(dcol), B, H, W, C, k, k, stride, pad, OH, OW, Kp, _p(dcol), _p(dx),
+                            float(beta), _stream()), "capk_col2im")
+    return dx
+
+
+def _bn_ws(M, C, device):
+    return _ws(lib().capk_bn_workspace(M, C), device)
+
+
+def bn_stats(x, eps, momentum, running_mean=None, running_var=None):
+    """Training-mode BatchNorm statistics of the rows of x [M, C]: (mean, rstd) fp32."""
+    _need_gpu(x)
+    M, C = x.shape
+    mean = torch.empty(C, dtype=torch.float32, device=x.device)
+    rstd = torch.empty_like(mean)
+    L = lib()
+    wsb = L.capk_bn_workspace(M, C)
+    ws = _ws(wsb, x.device)
+    check(L.capk_bn_stats(dtype_code(x), M, C, _p(x), x.stride(0), float(eps), float(momentum), _p(mean), _p(rstd),
+                          _p(running_mean), _p(running_var), _p(ws), wsb, _stream()), "capk_bn_stats")
+    return mean, rstd
+
+
+def bn_eval_stats(running_mean, running_var, eps):
+    C = running_mean.numel()
+    mean = torch.empty(C, dtype=torch.float32, device=running_mean.device)
+    rstd = torch.empty_like(mean)
+    check(lib().capk_bn_eval_stats(C, _p(running_mean), _p(running_var), float(eps), _p(mean), _p(rstd), _stream()),
+          "capk_bn_eval_stats")
+    return mean, rstd
+
+
+def bn_apply(x, mean, rstd, gamma, beta, *, residual=None, relu=False, out=None):
+    M, C = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    check(lib().capk_bn_apply(dtype_code(x), M, C, _p(x), x.stride(0), _p(mean), _p(rstd), _p(gamma), _p(beta),
+                              _p(residual), residual.stride(0) if residual is not None else 0, int(relu), _p(out),
+                              out.stride(0), _stream()), "capk_bn_apply")
+    return out
+
+
+def bn_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, *, y_mask=None, dx=None, beta_acc=0.0, dz_out=None,
+           accumulate=False, batch_stats=True):
+    """BatchNorm backward (training statistics): dgamma/dbeta written (or added), dx
+    (optional, += with beta_acc), dz_out (optional) = dy * [y_mask > 0]."""
+    L = lib()
+    M, C = x.shape
+    wsb = L.capk_bn_workspace(M, C)
+    ws = _ws(wsb, x.device)
+    check(L.capk_bn_bwd(dtype_code(x), M, C, _p(dy), dy.stride(0), _p(y_mask),
+                        y_mask.stride(0) if y_mask is not None else 0, _p(x), x.stride(0), _p(mean), _p(rstd),
+                        _p(gamma), _p(dgamma), _p(dbeta), int(accumulate), _p(dx), dx.stride(0) if dx is not None else 0,
+                        float(beta_acc), _p(dz_out), dz_out.stride(0) if dz_out is not None else 0,
+                        int(batch_stats), _p(ws), wsb,
+                        _stream()), "capk_bn_bwd")
+    return dx
+
+
+def maxpool_fwd(x, B, H, W, C, k, stride, pad):
+    OH, OW = conv_out_hw(H, W, k, stride, pad)
+    y = torch.empty(B * OH * OW, C, dtype=x.dtype, device=x.device)
+    idx = torch.empty(B * OH * OW, C, dtype=torch.uint8, device=x.device)
+    check(lib().capk_maxpool_fwd(dtype_code(x), B, H, W, C, k, stride, pad, OH, OW, _p(x), _p(y), _p(idx),
+                                 _stream()), "capk_maxpool_fwd")
+    return y, idx, OH, OW
+
+
+def maxpool_bwd(dy, idx, B, H, W, C, k, stride, pad):
+    OH, OW = conv_out_hw(H, W, k, stride, pad)
+    dx = torch.empty(B * H * W, C, dtype=dy.dtype, device=dy.device)
+    check(lib().capk_maxpool_bwd(dtype_code(dy), B, H, W, C, k, stride, pad, OH, OW, _p(dy), _p(idx), _p(dx),
+                                 _stream()), "capk_maxpool_bwd")
+    return dx
+
+
+def avgpool_fwd(x, B, H, W, C, OH, OW, out=None):
+    if out is None:
+        out = torch.empty(B * OH * OW, C, dtype=x.dtype, device=x.device)
+    check(lib().capk_avgpool_fwd(dtype_code(x), B, H, W, C, OH, OW, _p(x), _p(out), out.stride(0), _stream()),
+          "capk_avgpool_fwd")
+    return out
+
+
+def avgpool_bwd(dy, B, H, W, C, OH, OW, dx=None, beta=0.0):
+    if dx is None:
+        dx = torch.empty(B * H * W, C, dtype=dy.dtype, device=dy.device)
+    check(lib().capk_avgpool_bwd(dtype_code(dy), B, H, W, C, OH, OW, _p(dy), dy.stride(0), _p(dx), float(beta),
+                                 _stream()), "capk_avgpool_bwd")
+    return dx

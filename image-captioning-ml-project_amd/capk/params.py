@@ -34,6 +34,12 @@ def _round(n):
 
 
 def _alloc_numel(p):
+    lay = getattr(p, "_capk_layout", None)
+    if lay is not None:
+        n = 1
+        for d in lay[0]:
+            n *= d
+        return n
     pr = getattr(p, "_capk_pad_rows", None)
     if pr:
         assert pr >= p.shape[0]
@@ -102,13 +108,31 @@ class ParamStore:
             req = 0
             for p in plist:
                 n = p.numel()
-                with torch.no_grad():
-                    master[off:off + n].copy_(p.detach().reshape(-1).to(self.device, torch.float32))
-                p.data = master[off:off + n].view(p.shape)
-                p._capk_grad = grad[off:off + n].view(p.shape)
-                p.grad = p._capk_grad
-                if shadow is not None:
-                    p._capk_bf16 = shadow[off:off + n].view(p.shape)
+                lay = getattr(p, "_capk_layout", None)
+                if lay is not None:
+                    # kernel-native storage (e.g. channels-last, K-padded conv weights):
+                    # the parameter is a strided view of its storage block
+                    sshape, view = lay
+                    ns = _alloc_numel(p)
+                    ms = master[off:off + ns].view(sshape)
+                    with torch.no_grad():
+                        view(ms).copy_(p.detach().to(self.device, torch.float32))
+                    p.data = view(ms)
+                    p._capk_master_store = ms
+                    p._capk_grad_store = grad[off:off + ns].view(sshape)
+                    p._capk_grad = view(p._capk_grad_store)
+                    p.grad = p._capk_grad
+                    if shadow is not None:
+                        p._capk_bf16_store = shadow[off:off + ns].view(sshape)
+                        p._capk_bf16 = view(p._capk_bf16_store)
+                else:
+                    with torch.no_grad():
+                        master[off:off + n].copy_(p.detach().reshape(-1).to(self.device, torch.float32))
+                    p.data = master[off:off + n].view(p.shape)
+                    p._capk_grad = grad[off:off + n].view(p.shape)
+                    p.grad = p._capk_grad
+                    if shadow is not None:
+                        p._capk_bf16 = shadow[off:off + n].view(p.shape)
                 pr = getattr(p, "_capk_pad_rows", None)
                 if pr:
                     # zero-padded row extension (e.g. vocab rounded up for the GEMM tiles)

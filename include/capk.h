@@ -308,6 +308,57 @@ int capk_attention_probs_mean(int dtype, int B, int H, int Nq, int Nk, int hd, f
                               int64_t q_bs, int64_t q_rs, const void* k, int64_t k_bs, int64_t k_rs,
                               const uint8_t* key_pad, const float* lse, float* out, void* stream);
 
+/* ------------------------------------------------ convolutional encoder (A3) ----
+ * Channels-last activations [B, H, W, C] (row m = (b*H + h)*W + w, C contiguous).
+ * capk_im2col: col[m, k] of a KHxKW / stride / pad convolution, m = (b, oh, ow),
+ *   k = (kh*KW + kw)*C + c, zero for padding taps and for KH*KW*C <= k < Kp; input
+ *   element (b,h,w,c) at x[b*sb + h*sh + w*sw + c*sc] (so NCHW fp32 images feed the
+ *   stem directly).  in/out dtype pairs: f32->f32, f32->bf16, bf16->bf16.
+ *   Replaces the im2col inside nn.Conv2d (transformers ResNetConvLayer /
+ *   ResNetShortCut, modeling_resnet.py:39-110; torchvision resnet101 convs).
+ * capk_col2im: dx = beta*dx + the adjoint of capk_im2col (gather-sum, deterministic).
+ * capk_bn_stats: training-mode nn.BatchNorm2d statistics over the M rows of [M, C]:
+ *   mean, rstd = 1/sqrt(biased var + eps); running_mean/var (nullable) updated with
+ *   `momentum` (running_var from the unbiased variance).  capk_bn_eval_stats: mean,
+ *   rstd from the running buffers (eval mode).
+ * capk_bn_apply: y = [relu]((x - mean)*rstd*gamma + beta [+ residual]).
+ * capk_bn_bwd: dz = dy * [y_mask > 0] (y_mask nullable: the ReLU output), dgamma,
+ *   dbeta = column sums (written, or added with accumulate), dx (nullable) =
+ *   beta_acc*dx + gamma*rstd*(dz - mean(dz) - xhat*mean(dz*xhat)); dz_out (nullable)
+ *   receives dz.  batch_stats = 0: statistics were the running buffers (eval mode),
+ *   dx = beta_acc*dx + gamma*rstd*dz.  Workspace capk_bn_workspace(M, C) bytes.
+ *   C % 8 == 0 and (C <= 2048 or C % 2048 == 0).
+ * capk_maxpool_fwd/bwd: KxK max pool, -inf padding, idx = first-max window offset
+ *   (nn.MaxPool2d, ResNetEmbeddings.pooler modeling_resnet.py:83).
+ * capk_avgpool_fwd/bwd: adaptive average pool to OHxOW (aten window rule); y rows
+ *   b*OH*OW + oh*OW + ow with row stride ldy (ResNetModel pooler
+ *   AdaptiveAvgPool2d((1,1)); legacy models/encoder.py:10 AdaptiveAvgPool2d((14,14))). */
+int capk_im2col(int in_dtype, int out_dtype, int B, int H, int W, int C, int64_t sb, int64_t sh, int64_t sw,
+                int64_t sc, int KH, int KW, int stride, int pad, int OH, int OW, int Kp, const void* x, void* col,
+                void* stream);
+int capk_col2im(int dtype, int B, int H, int W, int C, int KH, int KW, int stride, int pad, int OH, int OW, int Kp,
+                const void* dcol, void* dx, float beta, void* stream);
+size_t capk_bn_workspace(int M, int C);
+int capk_bn_stats(int dtype, int M, int C, const void* x, int64_t ldx, float eps, float momentum, float* mean,
+                  float* rstd, float* running_mean, float* running_var, void* ws, size_t ws_bytes, void* stream);
+int capk_bn_eval_stats(int C, const float* running_mean, const float* running_var, float eps, float* mean,
+                       float* rstd, void* stream);
+int capk_bn_apply(int dtype, int M, int C, const void* x, int64_t ldx, const float* mean, const float* rstd,
+                  const float* gamma, const float* beta, const void* residual, int64_t ldr, int relu, void* y,
+                  int64_t ldy, void* stream);
+int capk_bn_bwd(int dtype, int M, int C, const void* dy, int64_t lddy, const void* y_mask, int64_t ldym,
+                const void* x, int64_t ldx, const float* mean, const float* rstd, const float* gamma, float* dgamma,
+                float* dbeta, int accumulate, void* dx, int64_t lddx, float beta_acc, void* dz_out, int64_t lddz,
+                int batch_stats, void* ws, size_t ws_bytes, void* stream);
+int capk_maxpool_fwd(int dtype, int B, int H, int W, int C, int K, int stride, int pad, int OH, int OW,
+                     const void* x, void* y, uint8_t* idx, void* stream);
+int capk_maxpool_bwd(int dtype, int B, int H, int W, int C, int K, int stride, int pad, int OH, int OW,
+                     const void* dy, const uint8_t* idx, void* dx, void* stream);
+int capk_avgpool_fwd(int dtype, int B, int H, int W, int C, int OH, int OW, const void* x, void* y, int64_t ldy,
+                     void* stream);
+int capk_avgpool_bwd(int dtype, int B, int H, int W, int C, int OH, int OW, const void* dy, int64_t lddy, void* dx,
+                     float beta, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -112,3 +112,52 @@ def clip_encoder(p, images, num_layers, num_heads, patch_size, eps=1e-5):
     last_hidden_state[:, 1:] (no post-LN), pooled = pooler_output, proj = Identity."""
     seq, pooled = clip_vision(p, images, num_layers, num_heads, patch_size, eps)
     return {"features": seq[:, 1:], "pooled_features": pooled, "attention_mask": None}
+
+
+# ------------------------------------------------------------------ ResNet (A3) --
+def _conv_bn(p, pre, x, stride, training, relu, state=None, momentum=0.1, eps=1e-5):
+    """ResNetConvLayer.forward (transformers/models/resnet/modeling_resnet.py:39-71):
+    Conv2d(bias=False, padding=k//2) -> BatchNorm2d -> ReLU (or identity).
+    `state` (dict of running buffers, updated in place in training mode) defaults to p."""
+    w = p[pre + "convolution.weight"]
+    x = F.conv2d(x, w, None, stride=stride, padding=w.shape[-1] // 2)
+    st = p if state is None else state
+    rm, rv = st[pre + "normalization.running_mean"], st[pre + "normalization.running_var"]
+    x = F.batch_norm(x, rm, rv, p[pre + "normalization.weight"], p[pre + "normalization.bias"], training,
+                     momentum, eps)
+    return F.relu(x) if relu else x
+
+
+def resnet_model(p, images, hidden_sizes, depths, training=True, state=None, downsample_in_first_stage=False):
+    """ResNetModel.forward (modeling_resnet.py:291-330), bottleneck layers (v1.5, stride on
+    the 3x3: downsample_in_bottleneck=False): returns (last_hidden_state, pooler_output)."""
+    x = _conv_bn(p, "embedder.embedder.", images, 2, training, True, state)  # ResNetEmbeddings 74-92
+    x = F.max_pool2d(x, 3, 2, 1)
+    for si, depth in enumerate(depths):
+        for li in range(depth):
+            pre = f"encoder.stages.{si}.layers.{li}."
+            stride = (2 if (si > 0 or downsample_in_first_stage) else 1) if li == 0 else 1
+            # ResNetBottleNeckLayer.forward (143-190)
+            h = _conv_bn(p, pre + "layer.0.", x, 1, training, True, state)
+            h = _conv_bn(p, pre + "layer.1.", h, stride, training, True, state)
+            h = _conv_bn(p, pre + "layer.2.", h, 1, training, False, state)
+            if pre + "shortcut.convolution.weight" in p:
+                r = _conv_bn(p, pre + "shortcut.", x, stride, training, False, state)  # ResNetShortCut 95-110
+            else:
+                r = x
+            x = F.relu(h + r)
+    return x, F.adaptive_avg_pool2d(x, (1, 1))
+
+
+def resnet_encoder(p, images, hidden_sizes, depths, training=True, state=None):
+    """ResNetEncoder.forward (src/models/encoders.py:60-91) with the SURVEY §0.1 D6
+    restatement: features = proj(map.flatten(2).transpose(1,2)), pooled = proj(pool.flatten(1))."""
+    last, pool = resnet_model(_strip(p, "model."), images, hidden_sizes, depths, training,
+                              None if state is None else _strip(state, "model."))
+    feats = F.linear(last.flatten(2).transpose(1, 2), p["proj.weight"], p["proj.bias"])
+    pooled = F.linear(pool.flatten(1), p["proj.weight"], p["proj.bias"])
+    return {"features": feats, "pooled_features": pooled}
+
+
+def _strip(p, prefix):
+    return {k[len(prefix):]: v for k, v in p.items() if k.startswith(prefix)}

@@ -269,8 +269,75 @@ def case_lstm_attention(R):
     return arrs
 
 
+def case_resnet_lstm(R):
+    """Config 2 path (ResNet + LSTMDecoder + soft attention), TRAIN mode (BatchNorm on batch
+    statistics, running buffers updated) with decoder dropout 0 so the step is deterministic.
+    The encoder is the reference's HF ``ResNetModel`` + ``proj`` with the SURVEY §0.1 D6
+    restatement applied around it (encoders.py:60-91 raises as written):
+    features = proj(last_hidden_state.flatten(2).transpose(1,2)), pooled = proj(pooler.flatten(1)).
+    Tiny bottleneck net: stages 16->32 (stride-1 projection shortcut, identity shortcut),
+    ->64, ->64, ->128 (stride-2 projection shortcuts), 64x64 images -> 2x2 maps."""
+    from transformers import ResNetConfig, ResNetModel
+    torch.manual_seed(4242)
+    D, L, V, B, T = 64, 2, 53, 3, 6
+    pad = V - 1
+    rcfg = ResNetConfig(num_channels=3, embedding_size=16, hidden_sizes=[32, 64, 64, 128], depths=[2, 1, 2, 1],
+                        layer_type="bottleneck", hidden_act="relu", downsample_in_first_stage=False,
+                        downsample_in_bottleneck=False)
+    enc = R.enc.ResNetEncoder.__new__(R.enc.ResNetEncoder)
+    nn.Module.__init__(enc)
+    enc.model = ResNetModel(rcfg)
+    enc.feature_dim = D
+    enc.proj = nn.Linear(rcfg.hidden_sizes[-1], D)
+
+    def d6_forward(images):
+        out = enc.model(images)
+        feats = enc.proj(out.last_hidden_state.flatten(2).transpose(1, 2))
+        pooled = enc.proj(out.pooler_output.flatten(1))
+        return {"features": feats, "pooled_features": pooled, "attention_mask": None}  # D4/D5
+
+    enc.forward = d6_forward
+    dcfg = R.config.DecoderConfig(decoder_type=R.config.DecoderType.LSTM, hidden_dim=D, num_layers=L, num_heads=1,
+                                  dropout=0.0, max_length=50)
+    acfg = R.config.AttentionConfig(attention_type=R.config.AttentionType.SOFT, num_heads=1, temperature=1.0)
+    acfg.hidden_dim = D  # D3
+    dec = R.dec.LSTMDecoder(dcfg, acfg, vocab_size=V, pad_token_id=pad)
+    model = R.cap.ImageCaptioningModel.__new__(R.cap.ImageCaptioningModel)
+    nn.Module.__init__(model)
+    model.config = R.config.Config.__new__(R.config.Config)
+    model.encoder = enc
+    model.decoder = dec
+    model.train()
+    images = torch.randn(B, 3, 64, 64)
+    captions = torch.randint(0, V - 1, (B, T))
+    captions[2, 4:] = pad
+    state0 = {n: t.detach().clone() for n, t in model.state_dict().items()}
+    out = model(images=images, captions=captions, caption_lengths=None)
+    loss = R.loss.CombinedLoss(pad_token_id=pad)(logits=out["logits"], targets=captions)["total_loss"]
+    loss.backward()
+    with torch.no_grad():
+        feats_train = enc(images)  # second train-mode pass: updates running stats again
+        enc.eval()
+        feats_eval = enc(images)
+    state1 = {n: t.detach().clone() for n, t in model.state_dict().items()}
+    arrs = {"meta/dims": np.array([D, L, V, B, T, pad, 64], dtype=np.int64),
+            "in/images": _np(images), "in/captions": _np(captions),
+            "out/logits": _np(out["logits"]), "out/loss": _np(loss.reshape(1)),
+            "out/features_train": _np(feats_train["features"]), "out/pooled_train": _np(feats_train["pooled_features"]),
+            "out/features_eval": _np(feats_eval["features"]), "out/pooled_eval": _np(feats_eval["pooled_features"])}
+    for n, t in state0.items():
+        arrs["s0/" + n] = _np(t)
+    for n, t in state1.items():
+        if not n.endswith(("weight", "bias")) or "running" in n:
+            arrs["s2/" + n] = _np(t)  # buffers after two train-mode passes
+    for n, p in model.named_parameters():
+        if p.grad is not None:
+            arrs["grad/" + n] = _np(p.grad)
+    return arrs
+
+
 CASES = {"vit_transformer_step": case_vit_transformer, "clip_gpt2_step": case_clip_gpt2,
-         "lstm_attention": case_lstm_attention}
+         "lstm_attention": case_lstm_attention, "resnet_lstm_step": case_resnet_lstm}
 
 
 def main(names=None):

@@ -169,3 +169,43 @@ def test_lstm_attention_matches_reference(golden_dir, name, kind, heads, temp):
         ids = olstm.lstm_greedy({k: v.detach() for k, v in p.items()}, feats.detach(), pooled.detach(), 6, L, kind,
                                 pad, heads, temp)
     np.testing.assert_array_equal(ids.numpy(), z[name + "/greedy_ids"])
+
+
+# ------------------------------------------------------------ config 2 (A3 + A6/A7) --
+RESNET_TINY = dict(hidden_sizes=[32, 64, 64, 128], depths=[2, 1, 2, 1])
+
+
+def test_resnet_lstm_step_matches_reference(golden_dir):
+    """Oracle ResNet (train-mode BN) + LSTM/soft decoder vs the reference's own step:
+    logits, loss, every gradient, running buffers after two passes, eval-mode features."""
+    from oracle import lstm as olstm
+    z = _load(golden_dir, "resnet_lstm_step")
+    D, L, V, B, T, pad, img = [int(x) for x in z["meta/dims"]]
+    s0 = _params(z, "s0")
+    p = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in s0.items()}
+    images = torch.from_numpy(z["in/images"])
+    caps = torch.from_numpy(z["in/captions"])
+    state = {k: v.clone() for k, v in s0.items()}
+    enc = oenc.resnet_encoder(_sub(p, "encoder."), images, training=True, state=_sub(state, "encoder."),
+                              **RESNET_TINY)
+    logits, _ = olstm.lstm_decoder(_sub(p, "decoder."), enc["features"], enc["pooled_features"], caps, L, "soft")
+    np.testing.assert_allclose(logits.detach().numpy(), z["out/logits"], rtol=1e-4, atol=1e-5)
+    loss = otrain.shifted_ce(logits, caps, pad)
+    np.testing.assert_allclose(float(loss), float(z["out/loss"][0]), rtol=1e-5)
+    loss.backward()
+    for n, t in p.items():
+        if "grad/" + n in z.files:
+            ref = z["grad/" + n]
+            np.testing.assert_allclose(t.grad.numpy(), ref, rtol=1e-4, atol=1e-4 * float(np.abs(ref).max()) + 1e-9,
+                                       err_msg=n)
+    with torch.no_grad():
+        ftr = oenc.resnet_encoder(_sub(p, "encoder."), images, training=True, state=_sub(state, "encoder."),
+                                  **RESNET_TINY)
+        np.testing.assert_allclose(ftr["features"].numpy(), z["out/features_train"], rtol=1e-4, atol=1e-5)
+        for k in z.files:
+            if k.startswith("s2/") and "running" in k:
+                np.testing.assert_allclose(state[k[3:]].numpy(), z[k], rtol=1e-5, atol=1e-6, err_msg=k)
+        fev = oenc.resnet_encoder(_sub(p, "encoder."), images, training=False, state=_sub(state, "encoder."),
+                                  **RESNET_TINY)
+        np.testing.assert_allclose(fev["features"].numpy(), z["out/features_eval"], rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(fev["pooled_features"].numpy(), z["out/pooled_eval"], rtol=1e-4, atol=1e-5)
