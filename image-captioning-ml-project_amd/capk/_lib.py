@@ -99,6 +99,13 @@ SIGNATURES = {
     "capk_maxpool_bwd": (_i, [_i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _c_p, _c_p, _c_p, _c_p]),
     "capk_avgpool_fwd": (_i, [_i, _i, _i, _i, _i, _i, _i, _c_p, _c_p, _i64, _c_p]),
     "capk_avgpool_bwd": (_i, [_i, _i, _i, _i, _i, _i, _i, _c_p, _i64, _c_p, _f, _c_p]),
+    "capk_additive_attn_fwd": (_i, [_i, _i, _i, _i, _i, _i, _c_p, _i64, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p,
+                                    _c_p, _f, _c_p, _c_p, _i64, _c_p, _c_p]),
+    "capk_additive_attn_bwd": (_i, [_i, _i, _i, _i, _i, _i, _c_p, _i64, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p,
+                                    _f, _c_p, _c_p, _i64, _c_p, _c_p, _i64, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "capk_attn_coverage_reg": (_i, [_i, _i, _i, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "capk_clamp": (_i, [_i64, _c_p, _f, _f, _c_p]),
+    "capk_mask_rows_by_length": (_i, [_i, _i, _i, _i, _c_p, _i64, _i64, _c_p, _c_p]),
 }
 
 _lib = None

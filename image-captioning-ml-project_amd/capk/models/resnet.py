@@ -146,7 +146,21 @@ class ResNetShortCut(nn.Module):
         self.normalization = nn.BatchNorm2d(cout)
 
 
-class ResNetBottleNeckLayer(CapkModule):
+class BottleneckBlock(CapkModule):
+    """Shared launch protocol of the HF and torchvision bottleneck blocks: subclasses
+    expose their (conv, bn) pairs through units() / shortcut_units()."""
+
+    def out_hw(self, H, W):
+        for c, _ in self.units():
+            H, W = ops.conv_out_hw(H, W, c.kernel_size[0], c.stride[0], c.padding[0])
+        return H, W
+
+    def forward(self, x, B, H, W):
+        OH, OW = self.out_hw(H, W)
+        return _BottleneckFn.apply(x, self.units()[0][0].weight, self, B, H, W), OH, OW
+
+
+class ResNetBottleNeckLayer(BottleneckBlock):
     """modeling_resnet.py:143-190 (v1.5: stride on the 3x3 unless downsample_in_bottleneck)."""
 
     def __init__(self, cin, cout, stride=1, reduction=4, downsample_in_bottleneck=False):
@@ -159,15 +173,13 @@ class ResNetBottleNeckLayer(CapkModule):
             ResNetConvLayer(red, cout, 1, activation=None),
         )
 
-    def out_hw(self, H, W):
-        for cl in self.layer:
-            c = cl.convolution
-            H, W = ops.conv_out_hw(H, W, c.kernel_size[0], c.stride[0], c.padding[0])
-        return H, W
+    def units(self):
+        return [(cl.convolution, cl.normalization) for cl in self.layer]
 
-    def forward(self, x, B, H, W):
-        OH, OW = self.out_hw(H, W)
-        return _BottleneckFn.apply(x, self.layer[0].convolution.weight, self, B, H, W), OH, OW
+    def shortcut_units(self):
+        if isinstance(self.shortcut, nn.Identity):
+            return None
+        return self.shortcut.convolution, self.shortcut.normalization
 
 
 class ResNetStage(nn.Module):
@@ -189,6 +201,14 @@ class _ResNetEncoderStages(nn.Module):
             self.stages.append(ResNetStage(a, cin, cout, 2, d))
 
 
+def stem_forward(m, images):
+    """7x7/2 conv + BN + ReLU + MaxPool2d(3, 2, 1) of module m (m.stem_units() -> (conv, bn))."""
+    c = m.stem_units()[0]
+    H, W = ops.conv_out_hw(images.shape[2], images.shape[3], c.kernel_size[0], c.stride[0], c.padding[0])
+    PH, PW = ops.conv_out_hw(H, W, 3, 2, 1)
+    return _StemFn.apply(images, c.weight, m), PH, PW
+
+
 class _ResNetEmbeddings(CapkModule):
     """modeling_resnet.py:74-92: 7x7/2 conv + BN + ReLU, then MaxPool2d(3, 2, 1)."""
 
@@ -196,11 +216,11 @@ class _ResNetEmbeddings(CapkModule):
         super().__init__()
         self.embedder = ResNetConvLayer(a["num_channels"], a["embedding_size"], 7, 2)
 
+    def stem_units(self):
+        return self.embedder.convolution, self.embedder.normalization
+
     def forward(self, images):
-        c = self.embedder.convolution
-        H, W = ops.conv_out_hw(images.shape[2], images.shape[3], c.kernel_size[0], c.stride[0], c.padding[0])
-        PH, PW = ops.conv_out_hw(H, W, 3, 2, 1)
-        return _StemFn.apply(images, c.weight, self), PH, PW
+        return stem_forward(self, images)
 
 
 class CapkResNetModel(CapkModule):
@@ -245,8 +265,7 @@ class _StemFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, images, anchor, m):
         dt = m.cdtype
-        cl = m.embedder
-        conv, bn = cl.convolution, cl.normalization
+        conv, bn = m.stem_units()
         B, C, H, W = images.shape
         images = images.contiguous()
         z, col, OH, OW = conv_fwd(conv, images, B, H, W, dt, strides=(C * H * W, W, 1, H * W))
@@ -264,10 +283,10 @@ class _StemFn(torch.autograd.Function):
         B, OH, OW, Cout = ctx.geo
         col, z, y, mean, rstd, idx = ctx.saved
         ctx.saved = None
-        cl = m.embedder
+        conv, bn = m.stem_units()
         dy = ops.maxpool_bwd(dp.contiguous(), idx, B, OH, OW, Cout, 3, 2, 1)
-        dz = bn_bwd(cl.normalization, dy, z, mean, rstd, m.training, y_mask=y, dx=dy)
-        ops.linear_dw(dz, col, GK(cl.convolution.weight))
+        dz = bn_bwd(bn, dy, z, mean, rstd, m.training, y_mask=y, dx=dy)
+        ops.linear_dw(dz, col, GK(conv.weight))
         return None, None, None
 
 
@@ -279,19 +298,20 @@ class _BottleneckFn(torch.autograd.Function):
     def forward(ctx, x, anchor, L, B, H, W):
         dt = L.cdtype
         tr = L.training
-        c1, c2, c3 = L.layer
-        z1, col1, H1, W1 = conv_fwd(c1.convolution, x, B, H, W, dt)
-        y1, mu1, rs1 = bn_fwd(c1.normalization, z1, tr)
-        z2, col2, H2, W2 = conv_fwd(c2.convolution, y1, B, H1, W1, dt)
-        y2, mu2, rs2 = bn_fwd(c2.normalization, z2, tr)
-        z3, _, _, _ = conv_fwd(c3.convolution, y2, B, H2, W2, dt)
-        if isinstance(L.shortcut, nn.Identity):
+        (k1, n1), (k2, n2), (k3, n3) = L.units()
+        scu = L.shortcut_units()
+        z1, col1, H1, W1 = conv_fwd(k1, x, B, H, W, dt)
+        y1, mu1, rs1 = bn_fwd(n1, z1, tr)
+        z2, col2, H2, W2 = conv_fwd(k2, y1, B, H1, W1, dt)
+        y2, mu2, rs2 = bn_fwd(n2, z2, tr)
+        z3, _, _, _ = conv_fwd(k3, y2, B, H2, W2, dt)
+        if scu is None:
             res, sc = x, None
         else:
-            zs, cols, _, _ = conv_fwd(L.shortcut.convolution, x, B, H, W, dt)
-            res, mus, rss = bn_fwd(L.shortcut.normalization, zs, tr, relu=False)
+            zs, cols, _, _ = conv_fwd(scu[0], x, B, H, W, dt)
+            res, mus, rss = bn_fwd(scu[1], zs, tr, relu=False)
             sc = (zs, cols, mus, rss)
-        out, mu3, rs3 = bn_fwd(c3.normalization, z3, tr, residual=res)
+        out, mu3, rs3 = bn_fwd(n3, z3, tr, residual=res)
         ctx.L, ctx.geo = L, (B, H, W, H1, W1, H2, W2)
         ctx.saved = (col1, z1, y1, mu1, rs1, col2, z2, y2, mu2, rs2, z3, mu3, rs3, sc, out)
         return out
@@ -304,21 +324,22 @@ class _BottleneckFn(torch.autograd.Function):
         B, H, W, H1, W1, H2, W2 = ctx.geo
         col1, z1, y1, mu1, rs1, col2, z2, y2, mu2, rs2, z3, mu3, rs3, sc, out = ctx.saved
         ctx.saved = None
-        c1, c2, c3 = L.layer
+        (k1, n1), (k2, n2), (k3, n3) = L.units()
         dout = dout.contiguous()
         if sc is None:
             dx = torch.empty_like(dout)  # identity shortcut: dX starts as dout * [out > 0]
-            dz3 = bn_bwd(c3.normalization, dout, z3, mu3, rs3, tr, y_mask=out, dz_out=dx)
+            dz3 = bn_bwd(n3, dout, z3, mu3, rs3, tr, y_mask=out, dz_out=dx)
         else:
+            ks, ns = L.shortcut_units()
             zs, cols, mus, rss = sc
-            dz3 = bn_bwd(c3.normalization, dout, z3, mu3, rs3, tr, y_mask=out)
-            dzs = bn_bwd(L.shortcut.normalization, dout, zs, mus, rss, tr, y_mask=out)
-            dx = conv_bwd(L.shortcut.convolution, dzs, cols, B, H, W, dt)
-        dy2 = conv_bwd(c3.convolution, dz3, y2, B, H2, W2, dt)
-        dz2 = bn_bwd(c2.normalization, dy2, z2, mu2, rs2, tr, y_mask=y2, dx=dy2)
-        dy1 = conv_bwd(c2.convolution, dz2, col2, B, H1, W1, dt)
-        dz1 = bn_bwd(c1.normalization, dy1, z1, mu1, rs1, tr, y_mask=y1, dx=dy1)
-        conv_bwd(c1.convolution, dz1, col1, B, H, W, dt, dx=dx, beta=1.0)
+            dz3 = bn_bwd(n3, dout, z3, mu3, rs3, tr, y_mask=out)
+            dzs = bn_bwd(ns, dout, zs, mus, rss, tr, y_mask=out)
+            dx = conv_bwd(ks, dzs, cols, B, H, W, dt)
+        dy2 = conv_bwd(k3, dz3, y2, B, H2, W2, dt)
+        dz2 = bn_bwd(n2, dy2, z2, mu2, rs2, tr, y_mask=y2, dx=dy2)
+        dy1 = conv_bwd(k2, dz2, col2, B, H1, W1, dt)
+        dz1 = bn_bwd(n1, dy1, z1, mu1, rs1, tr, y_mask=y1, dx=dy1)
+        conv_bwd(k1, dz1, col1, B, H, W, dt, dx=dx, beta=1.0)
         return dx, None, None, None, None, None
 
 

@@ -564,3 +564,44 @@ def avgpool_bwd(dy, B, H, W, C, OH, OW, dx=None, beta=0.0):
     check(lib().capk_avgpool_bwd(dtype_code(dy), B, H, W, C, OH, OW, _p(dy), dy.stride(0), _p(dx), float(beta),
                                  _stream()), "capk_avgpool_bwd")
     return dx
+
+
+# ----------------------------------------------- legacy Show-Attend-Tell (A11) ---
+def additive_attn_fwd(act, qp, kp, v, we, be, inv_temp, ctx, w_out, key_pad=None):
+    """qp [B,D]; kp [B,S,D], v [B,S,Dv] views; ctx [B,Dv] view; w_out fp32 [B,S].
+    act 0 = tanh energy (SoftAttention), 1 = ReLU energy (legacy decoder)."""
+    B, S, D = kp.shape
+    Dv = v.shape[2]
+    check(lib().capk_additive_attn_fwd(dtype_code(qp), int(act), B, S, D, Dv, _p(qp), qp.stride(0), _p(kp),
+                                       kp.stride(0), kp.stride(1), _p(v), v.stride(0), v.stride(1), _p(we), _p(be),
+                                       float(inv_temp), _p(key_pad), _p(ctx), ctx.stride(0), _p(w_out), _stream()),
+          "capk_additive_attn_fwd")
+
+
+def additive_attn_bwd(act, qp, kp, v, we, inv_temp, w, dctx, dqp, dkp, dv, dwe_part, dbe_part, dw_in=None):
+    B, S, D = kp.shape
+    Dv = v.shape[2]
+    check(lib().capk_additive_attn_bwd(dtype_code(qp), int(act), B, S, D, Dv, _p(qp), qp.stride(0), _p(kp),
+                                       kp.stride(0), kp.stride(1), _p(v), v.stride(0), v.stride(1), _p(we),
+                                       float(inv_temp), _p(w), _p(dctx), dctx.stride(0), _p(dw_in), _p(dqp),
+                                       dqp.stride(0), _p(dkp), _p(dv), _p(dwe_part), _p(dbe_part), _stream()),
+          "capk_additive_attn_bwd")
+
+
+def attn_coverage_reg(alphas_tbs, grad_scale=None, loss_acc=None, coef=None):
+    T, B, S = alphas_tbs.shape
+    check(lib().capk_attn_coverage_reg(B, T, S, _p(alphas_tbs), _p(grad_scale), _p(loss_acc), _p(coef), _stream()),
+          "capk_attn_coverage_reg")
+
+
+def clamp_(x, lo, hi):
+    check(lib().capk_clamp(x.numel(), _p(x), float(lo), float(hi), _stream()), "capk_clamp")
+    return x
+
+
+def mask_rows_by_length(x, lengths_i32):
+    """x: [B, T, C] view (row stride x.stride(1), batch stride x.stride(0)); zero rows t >= len[b]."""
+    B, T, C = x.shape
+    check(lib().capk_mask_rows_by_length(dtype_code(x), B, T, C, _p(x), x.stride(1), x.stride(0), _p(lengths_i32),
+                                         _stream()), "capk_mask_rows_by_length")
+    return x

@@ -69,9 +69,15 @@ __global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(int B, int D, const 
 
 // ------------------------------------------------------------ soft attention --
 static constexpr int SA_MAXS = 256;
+// energy nonlinearity: 0 = tanh (SoftAttention, attention.py:100), 1 = ReLU (legacy
+// Show-Attend-Tell attention, models/decoder.py:145-146)
+template <int ACT>
+__device__ __forceinline__ float energy_act(float x) { return ACT == 0 ? tanhf(x) : (x > 0.f ? x : 0.f); }
+template <int ACT>
+__device__ __forceinline__ float energy_act_grad(float pre, float a) { return ACT == 0 ? 1.f - a * a : (pre > 0.f ? 1.f : 0.f); }
 
-template <typename T>
-__global__ __launch_bounds__(256) void soft_attn_fwd_kernel(int S, int D, const T* __restrict__ qp, int64_t ldq,
+template <typename T, int ACT>
+__global__ __launch_bounds__(256) void soft_attn_fwd_kernel(int S, int D, int Dv, const T* __restrict__ qp, int64_t ldq,
                                                             const T* __restrict__ kp, int64_t kp_bs, int64_t kp_rs,
                                                             const T* __restrict__ v, int64_t v_bs, int64_t v_rs,
                                                             const float* __restrict__ we, const float* __restrict__ be,
@@ -85,7 +91,7 @@ __global__ __launch_bounds__(256) void soft_attn_fwd_kernel(int S, int D, const 
   for (int s = w; s < S; s += 4) {
     const T* k = kb + (int64_t)s * kp_rs;
     float acc = 0.f;
-    for (int d = lane; d < D; d += 64) acc += we[d] * tanhf(to_f32(q[d]) + to_f32(k[d]));
+    for (int d = lane; d < D; d += 64) acc += we[d] * energy_act<ACT>(to_f32(q[d]) + to_f32(k[d]));
     acc = wave_sum(acc);
     if (lane == 0) {
       float e = (acc + be[0]) * inv_temp;
@@ -115,7 +121,7 @@ __global__ __launch_bounds__(256) void soft_attn_fwd_kernel(int S, int D, const 
   }
   __syncthreads();
   const T* vb = v + (int64_t)b * v_bs;
-  for (int d = tid; d < D; d += 256) {
+  for (int d = tid; d < Dv; d += 256) {
     float acc = 0.f;
     for (int s = 0; s < S; ++s) acc += sc[s] * to_f32(vb[(int64_t)s * v_rs + d]);
     ctx[(int64_t)b * ldc + d] = from_f32<T>(acc);
@@ -124,8 +130,8 @@ __global__ __launch_bounds__(256) void soft_attn_fwd_kernel(int S, int D, const 
 
 // Gradients of one step; the key/value/energy gradients ACCUMULATE (fp32) over the
 // decode steps: dkp [B,S,D], dv [B,S,D], dwe_part [B,D], dbe_part [B].
-template <typename T>
-__global__ __launch_bounds__(256) void soft_attn_bwd_kernel(int S, int D, const T* __restrict__ qp, int64_t ldq,
+template <typename T, int ACT>
+__global__ __launch_bounds__(256) void soft_attn_bwd_kernel(int S, int D, int Dv, const T* __restrict__ qp, int64_t ldq,
                                                             const T* __restrict__ kp, int64_t kp_bs, int64_t kp_rs,
                                                             const T* __restrict__ v, int64_t v_bs, int64_t v_rs,
                                                             const float* __restrict__ we, float inv_temp,
@@ -145,7 +151,7 @@ __global__ __launch_bounds__(256) void soft_attn_bwd_kernel(int S, int D, const 
   for (int s = w; s < S; s += 4) {
     const T* vr = vb + (int64_t)s * v_rs;
     float acc = 0.f;
-    for (int d = lane; d < D; d += 64) acc += to_f32(g[d]) * to_f32(vr[d]);
+    for (int d = lane; d < Dv; d += 64) acc += to_f32(g[d]) * to_f32(vr[d]);
     acc = wave_sum(acc);
     if (lane == 0) de[s] = acc + (dw_in ? dw_in[(int64_t)b * S + s] : 0.f);
   }
@@ -163,22 +169,28 @@ __global__ __launch_bounds__(256) void soft_attn_bwd_kernel(int S, int D, const 
   const T* q = qp + (int64_t)b * ldq;
   const T* kb = kp + (int64_t)b * kp_bs;
   float* dkb = dkp + (int64_t)b * S * D;
-  float* dvb = dv + (int64_t)b * S * D;
   float dbe = 0.f;
   for (int s = tid; s < S; s += 256) dbe += de[s];
   for (int d = tid; d < D; d += 256) {
-    const float qd = to_f32(q[d]), wd = we[d], gd = to_f32(g[d]);
+    const float qd = to_f32(q[d]), wd = we[d];
     float dq = 0.f, dw = 0.f;
     for (int s = 0; s < S; ++s) {
-      const float a = tanhf(qd + to_f32(kb[(int64_t)s * kp_rs + d]));
-      const float gr = de[s] * wd * (1.f - a * a);
+      const float pre = qd + to_f32(kb[(int64_t)s * kp_rs + d]);
+      const float a = energy_act<ACT>(pre);
+      const float gr = de[s] * wd * energy_act_grad<ACT>(pre, a);
       dq += gr;
       dw += de[s] * a;
       dkb[(int64_t)s * D + d] += gr;
-      dvb[(int64_t)s * D + d] += ws[s] * gd;
     }
     dqp[(int64_t)b * lddq + d] = from_f32<T>(dq);
     dwe_part[(int64_t)b * D + d] += dw;
+  }
+  if (dv) {
+    float* dvb = dv + (int64_t)b * S * Dv;
+    for (int d = tid; d < Dv; d += 256) {
+      const float gd = to_f32(g[d]);
+      for (int s = 0; s < S; ++s) dvb[(int64_t)s * Dv + d] += ws[s] * gd;
+    }
   }
   dbe = wave_sum(dbe);
   if (lane == 0) red[w] = dbe;
@@ -223,16 +235,41 @@ extern "C" int capk_lstm_cell_bwd(int dtype, int B, int D, const void* act, cons
   return CAPK_OK;
 }
 
+extern "C" int capk_additive_attn_fwd(int dtype, int act, int B, int S, int D, int Dv, const void* qp, int64_t ldq,
+                                      const void* kp, int64_t kp_bs, int64_t kp_rs, const void* v, int64_t v_bs,
+                                      int64_t v_rs, const float* we, const float* be, float inv_temp,
+                                      const uint8_t* key_pad, void* ctx, int64_t ldc, float* w_out, void* stream) {
+  CAPK_CHECK_ARG(B > 0 && S > 0 && S <= SA_MAXS && D > 0 && Dv > 0, "capk_additive_attn_fwd: need 0 < S <= %d",
+                 SA_MAXS);
+  CAPK_CHECK_ARG(act == 0 || act == 1, "capk_additive_attn_fwd: act must be 0 (tanh) or 1 (relu)");
+#define K(T, A) hipLaunchKernelGGL((soft_attn_fwd_kernel<T, A>), dim3(B), dim3(256), 0, capk::S(stream), S, D, Dv, (const T*)qp, ldq, (const T*)kp, kp_bs, kp_rs, (const T*)v, v_bs, v_rs, we, be, inv_temp, key_pad, (T*)ctx, ldc, w_out)
+  if (act == 0) DT2(dtype, K, 0); else DT2(dtype, K, 1);
+#undef K
+  CAPK_LAUNCH_CHECK("soft_attn_fwd_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_additive_attn_bwd(int dtype, int act, int B, int S, int D, int Dv, const void* qp, int64_t ldq,
+                                      const void* kp, int64_t kp_bs, int64_t kp_rs, const void* v, int64_t v_bs,
+                                      int64_t v_rs, const float* we, float inv_temp, const float* w, const void* dctx,
+                                      int64_t lddc, const float* dw_in, void* dqp, int64_t lddq, float* dkp, float* dv,
+                                      float* dwe_part, float* dbe_part, void* stream) {
+  CAPK_CHECK_ARG(B > 0 && S > 0 && S <= SA_MAXS && D > 0 && Dv > 0, "capk_additive_attn_bwd: need 0 < S <= %d",
+                 SA_MAXS);
+  CAPK_CHECK_ARG(act == 0 || act == 1, "capk_additive_attn_bwd: act must be 0 (tanh) or 1 (relu)");
+#define K(T, A) hipLaunchKernelGGL((soft_attn_bwd_kernel<T, A>), dim3(B), dim3(256), 0, capk::S(stream), S, D, Dv, (const T*)qp, ldq, (const T*)kp, kp_bs, kp_rs, (const T*)v, v_bs, v_rs, we, inv_temp, w, (const T*)dctx, lddc, dw_in, (T*)dqp, lddq, dkp, dv, dwe_part, dbe_part)
+  if (act == 0) DT2(dtype, K, 0); else DT2(dtype, K, 1);
+#undef K
+  CAPK_LAUNCH_CHECK("soft_attn_bwd_kernel");
+  return CAPK_OK;
+}
+
 extern "C" int capk_soft_attn_fwd(int dtype, int B, int S, int D, const void* qp, int64_t ldq, const void* kp,
                                   int64_t kp_bs, int64_t kp_rs, const void* v, int64_t v_bs, int64_t v_rs,
                                   const float* we, const float* be, float inv_temp, const uint8_t* key_pad, void* ctx,
                                   int64_t ldc, float* w_out, void* stream) {
-  CAPK_CHECK_ARG(B > 0 && S > 0 && S <= SA_MAXS && D > 0, "capk_soft_attn_fwd: need 0 < S <= %d", SA_MAXS);
-#define K(T, _) hipLaunchKernelGGL(soft_attn_fwd_kernel<T>, dim3(B), dim3(256), 0, capk::S(stream), S, D, (const T*)qp, ldq, (const T*)kp, kp_bs, kp_rs, (const T*)v, v_bs, v_rs, we, be, inv_temp, key_pad, (T*)ctx, ldc, w_out)
-  DT2(dtype, K, 0);
-#undef K
-  CAPK_LAUNCH_CHECK("soft_attn_fwd_kernel");
-  return CAPK_OK;
+  return capk_additive_attn_fwd(dtype, 0, B, S, D, D, qp, ldq, kp, kp_bs, kp_rs, v, v_bs, v_rs, we, be, inv_temp,
+                                key_pad, ctx, ldc, w_out, stream);
 }
 
 extern "C" int capk_soft_attn_bwd(int dtype, int B, int S, int D, const void* qp, int64_t ldq, const void* kp,
@@ -240,10 +277,6 @@ extern "C" int capk_soft_attn_bwd(int dtype, int B, int S, int D, const void* qp
                                   const float* we, float inv_temp, const float* w, const void* dctx, int64_t lddc,
                                   const float* dw_in, void* dqp, int64_t lddq, float* dkp, float* dv, float* dwe_part,
                                   float* dbe_part, void* stream) {
-  CAPK_CHECK_ARG(B > 0 && S > 0 && S <= SA_MAXS && D > 0, "capk_soft_attn_bwd: need 0 < S <= %d", SA_MAXS);
-#define K(T, _) hipLaunchKernelGGL(soft_attn_bwd_kernel<T>, dim3(B), dim3(256), 0, capk::S(stream), S, D, (const T*)qp, ldq, (const T*)kp, kp_bs, kp_rs, (const T*)v, v_bs, v_rs, we, inv_temp, w, (const T*)dctx, lddc, dw_in, (T*)dqp, lddq, dkp, dv, dwe_part, dbe_part)
-  DT2(dtype, K, 0);
-#undef K
-  CAPK_LAUNCH_CHECK("soft_attn_bwd_kernel");
-  return CAPK_OK;
+  return capk_additive_attn_bwd(dtype, 0, B, S, D, D, qp, ldq, kp, kp_bs, kp_rs, v, v_bs, v_rs, we, inv_temp, w,
+                                dctx, lddc, dw_in, dqp, lddq, dkp, dv, dwe_part, dbe_part, stream);
 }

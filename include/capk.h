@@ -359,6 +359,31 @@ int capk_avgpool_fwd(int dtype, int B, int H, int W, int C, int OH, int OW, cons
 int capk_avgpool_bwd(int dtype, int B, int H, int W, int C, int OH, int OW, const void* dy, int64_t lddy, void* dx,
                      float beta, void* stream);
 
+/* ------------------------------------------- legacy Show-Attend-Tell (A11) ----
+ * capk_additive_attn_fwd/bwd: capk_soft_attn_* generalised to the legacy decoder's
+ * attention (models/decoder.py:141-151): energy nonlinearity act (0 = tanh,
+ * 1 = ReLU) and a value width Dv != D (alpha-weighted sum of 2048-wide encoder
+ * pixels with 512-wide attention projections).  dv may be NULL (no value gradient).
+ * capk_attn_coverage_reg: alphas t-major [T, B, S] fp32 (inactive rows 0);
+ * loss_acc[0] += mean_{b,s} (1 - sum_t alphas)^2 (train.py:101) when non-NULL;
+ * coef[b, s] (nullable) = d/d alpha[b,t,s] * (*grad_scale, NULL = 1).
+ * capk_clamp: x = min(max(x, lo), hi) in place (train.py:105-110 grad clamp).
+ * capk_mask_rows_by_length: x[b*bs + t*ld + c] = 0 for t >= len[b] (device int32). */
+int capk_additive_attn_fwd(int dtype, int act, int B, int S, int D, int Dv, const void* qp, int64_t ldq,
+                           const void* kp, int64_t kp_bs, int64_t kp_rs, const void* v, int64_t v_bs, int64_t v_rs,
+                           const float* we, const float* be, float inv_temp, const uint8_t* key_pad, void* ctx,
+                           int64_t ldc, float* w_out, void* stream);
+int capk_additive_attn_bwd(int dtype, int act, int B, int S, int D, int Dv, const void* qp, int64_t ldq,
+                           const void* kp, int64_t kp_bs, int64_t kp_rs, const void* v, int64_t v_bs, int64_t v_rs,
+                           const float* we, float inv_temp, const float* w, const void* dctx, int64_t lddc,
+                           const float* dw_in, void* dqp, int64_t lddq, float* dkp, float* dv, float* dwe_part,
+                           float* dbe_part, void* stream);
+int capk_attn_coverage_reg(int B, int T, int S, const float* alphas, const float* grad_scale, float* loss_acc,
+                           float* coef, void* stream);
+int capk_clamp(int64_t n, float* x, float lo, float hi, void* stream);
+int capk_mask_rows_by_length(int dtype, int B, int T, int cols, void* x, int64_t ld, int64_t bs, const int32_t* len,
+                             void* stream);
+
 #ifdef __cplusplus
 }
 #endif

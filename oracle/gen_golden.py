@@ -336,8 +336,79 @@ def case_resnet_lstm(R):
     return arrs
 
 
+def _digest(arrs, key, t, full_max=65536):
+    """Large tensors travel as a digest: the first 4096 flat values + sum / abs-sum / norm."""
+    a = _np(t).astype(np.float64)
+    if a.size <= full_max:
+        arrs[key] = a.astype(np.float32)
+        return
+    flat = a.reshape(-1)
+    arrs[key + "@head"] = flat[:4096].astype(np.float32)
+    arrs[key + "@stats"] = np.array([flat.sum(), np.abs(flat).sum(), np.sqrt((flat * flat).sum())])
+
+
+def case_legacy_decoder(R):
+    """Config 1 decoder (models/decoder.py Decoder, use_bert=False) + the train.py step
+    (train.py:84-112): packed CE + ((1 - sum_t alpha)^2).mean(), backward, grad clamp +-5,
+    Adam(lr 4e-4) — run by the reference's own code (import needs a stub
+    `pytorch_pretrained_bert` module: it is imported at module level but unused when
+    use_bert=False).  Dropout p=0.5 is set to 0 for a deterministic step.  The decoder dims
+    are hard-coded (2048/512/512), so its parameters are NOT stored: they are re-created
+    from the seed by the build's Decoder (same construction/RNG order) and pinned by
+    digests; large gradients / updated weights travel as digests (_digest)."""
+    import importlib
+    stub = types.ModuleType("pytorch_pretrained_bert")
+    stub.BertTokenizer = stub.BertModel = object
+    sys.modules.setdefault("pytorch_pretrained_bert", stub)
+    sys.path.insert(0, os.path.join(REF, "models"))
+    try:
+        rdec = importlib.import_module("models.decoder")
+    finally:
+        sys.path.pop(0)
+    from torch.nn.utils.rnn import pack_padded_sequence
+    V, B, S = 40, 4, 16
+    lengths = [7, 6, 6, 4]
+    torch.manual_seed(2024)
+    dec = rdec.Decoder(V, False, "cpu")
+    dec.dropout.p = 0.0
+    dec.train()
+    torch.manual_seed(7)
+    enc_out = torch.randn(B, 4, 4, 2048).requires_grad_(True)
+    caps = torch.zeros(B, max(lengths), dtype=torch.long)
+    for b, L in enumerate(lengths):
+        caps[b, 0] = 1
+        caps[b, 1:L - 1] = torch.randint(3, V, (L - 2,))
+        caps[b, L - 1] = 2
+    arrs = {"meta/dims": np.array([V, B, S], dtype=np.int64), "in/lengths": np.array(lengths, dtype=np.int64),
+            "in/encoder_out": _np(enc_out), "in/captions": _np(caps)}
+    for n, p in dec.named_parameters():
+        _digest(arrs, "p0/" + n, p, full_max=0)
+    scores, caps_sorted, decode_lengths, alphas = dec(enc_out, caps, lengths)
+    arrs["out/predictions"], arrs["out/alphas"] = _np(scores), _np(alphas)
+    sp = pack_padded_sequence(scores, decode_lengths, batch_first=True)[0]
+    tg = pack_padded_sequence(caps_sorted[:, 1:], decode_lengths, batch_first=True)[0]
+    loss = nn.CrossEntropyLoss()(sp, tg)  # D12: train.py never defines `criterion`
+    loss = loss + ((1. - alphas.sum(dim=1)) ** 2).mean()
+    opt = torch.optim.Adam(params=dec.parameters(), lr=4e-4)
+    opt.zero_grad()
+    loss.backward()
+    arrs["out/loss"] = _np(loss.reshape(1))
+    arrs["out/dencoder_out"] = _np(enc_out.grad)
+    for n, p in dec.named_parameters():
+        _digest(arrs, "grad/" + n, p.grad)
+    for group in opt.param_groups:  # train.py:105-110
+        for param in group["params"]:
+            if param.grad is not None:
+                param.grad.data.clamp_(-5., 5.)
+    opt.step()
+    for n, p in dec.named_parameters():
+        _digest(arrs, "p1/" + n, p, full_max=0)
+    return arrs
+
+
 CASES = {"vit_transformer_step": case_vit_transformer, "clip_gpt2_step": case_clip_gpt2,
-         "lstm_attention": case_lstm_attention, "resnet_lstm_step": case_resnet_lstm}
+         "lstm_attention": case_lstm_attention, "resnet_lstm_step": case_resnet_lstm,
+         "legacy_decoder_step": case_legacy_decoder}
 
 
 def main(names=None):

@@ -21,6 +21,7 @@ python -c "import torch;print(torch.cuda.get_device_name(0), torch.cuda.get_devi
 [[ $STEPS == *lstm* ]] && run lstm 900 python -m pytest tests/test_gpu_lstm.py -q -rf
 [[ $STEPS == *scst* ]] && run scst 900 python -m pytest tests/test_gpu_scst.py -q -rf
 [[ $STEPS == *resnet* ]] && run resnet 900 python -u -m pytest tests/test_gpu_resnet.py -q -rf --timeout 300 --timeout-method thread
+[[ $STEPS == *legacy* ]] && run legacy 900 python -u -m pytest tests/test_gpu_legacy.py -q -rf --timeout 300 --timeout-method thread
 [[ $STEPS == *cfg4* ]] && run cfg4 900 python -m pytest tests/test_gpu_config4.py -q -rf
 [[ $STEPS == *model* ]] && run model 900 python -m pytest tests/test_gpu_model.py -q -rf
 [[ $STEPS == *gemm* ]] && run gemm 300 python tools/gemm_bench.py

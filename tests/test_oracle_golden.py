@@ -209,3 +209,52 @@ def test_resnet_lstm_step_matches_reference(golden_dir):
                                   **RESNET_TINY)
         np.testing.assert_allclose(fev["features"].numpy(), z["out/features_eval"], rtol=1e-4, atol=1e-5)
         np.testing.assert_allclose(fev["pooled_features"].numpy(), z["out/pooled_eval"], rtol=1e-4, atol=1e-5)
+
+
+# ------------------------------------------------------------ config 1 (A11) --
+def _check_digest(z, key, t, rtol, atol_frac):
+    a = t.detach().double().numpy()
+    if key in z.files:
+        ref = z[key]
+        np.testing.assert_allclose(a, ref, rtol=rtol, atol=atol_frac * float(np.abs(ref).max()) + 1e-12, err_msg=key)
+        return
+    head, stats = z[key + "@head"], z[key + "@stats"]
+    flat = a.reshape(-1)
+    np.testing.assert_allclose(flat[:head.size], head, rtol=rtol, atol=atol_frac * float(np.abs(head).max()) + 1e-12,
+                               err_msg=key)
+    got = np.array([flat.sum(), np.abs(flat).sum(), np.sqrt((flat * flat).sum())])
+    np.testing.assert_allclose(got[1:], stats[1:], rtol=rtol, err_msg=key + " stats")
+    assert abs(got[0] - stats[0]) <= rtol * stats[1] + 1e-12, (key, got[0], stats[0])
+
+
+def legacy_params_from_seed():
+    """The build's legacy Decoder created under the golden's seed (same module/RNG order as
+    models/decoder.py:9-58) -> the reference's initial parameters (pinned by digests)."""
+    from capk.legacy import Decoder
+    torch.manual_seed(2024)
+    return {n: p.detach().clone() for n, p in Decoder(40, False, "cpu").named_parameters()}
+
+
+def test_legacy_decoder_step_matches_reference(golden_dir):
+    from oracle import legacy as oleg
+    z = _load(golden_dir, "legacy_decoder_step")
+    p0 = legacy_params_from_seed()
+    for n, t in p0.items():
+        _check_digest(z, "p0/" + n, t, 0, 0)
+    p = {n: t.clone().requires_grad_(True) for n, t in p0.items()}
+    enc = torch.from_numpy(z["in/encoder_out"]).requires_grad_(True)
+    caps = torch.from_numpy(z["in/captions"])
+    lengths = [int(x) for x in z["in/lengths"]]
+    preds, alphas = oleg.legacy_decoder(p, enc, caps, lengths)
+    np.testing.assert_allclose(preds.detach().numpy(), z["out/predictions"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(alphas.detach().numpy(), z["out/alphas"], rtol=1e-4, atol=1e-7)
+    loss = oleg.legacy_loss(preds, alphas, caps, lengths)
+    np.testing.assert_allclose(float(loss), float(z["out/loss"][0]), rtol=1e-5)
+    loss.backward()
+    np.testing.assert_allclose(enc.grad.numpy(), z["out/dencoder_out"], rtol=1e-4,
+                               atol=1e-4 * float(np.abs(z["out/dencoder_out"]).max()))
+    for n, t in p.items():
+        _check_digest(z, "grad/" + n, t.grad, 1e-4, 1e-4)
+    p1 = oleg.clamp_adam_step({n: t.detach() for n, t in p.items()}, {n: t.grad for n, t in p.items()})
+    for n, t in p1.items():
+        _check_digest(z, "p1/" + n, t, 1e-5, 1e-6)
