@@ -297,6 +297,114 @@ __global__ __launch_bounds__(BMX / 32 * 64) void gemm_bf16_kernel(
   }
 }
 
+// ====================================================== 256x256 bf16 kernel ===
+// Large-grid tile: 256x256x64, 8 waves as 2 (M) x 4 (N), 128x64 outputs per wave (8x4
+// 16x16 accumulators = 128 VGPRs).  Twice the FLOP per staged byte of the 128x128 tile
+// (32 B/clk/CU of L2->LDS traffic at the MFMA rate instead of 64, the per-CU L2 limit),
+// 2-deep LDS ring (2 x 64 KiB -> 1 WG/CU), one raw barrier per K-tile: the next tile's
+// LDS-DMA is issued right after the barrier and lands under the 64 MFMAs of this one.
+template <int BKX, int NST, bool AK, bool BK, typename OutT>
+__global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A, int64_t lda,
+                                                      const bf16* __restrict__ B, int64_t ldb, int M, int N, int K,
+                                                      int splits, Epi e, float* __restrict__ ws) {
+  constexpr int BM = 256, BNN = 256;
+  constexpr int A_BYTES = BM * BKX * 2, B_BYTES = BNN * BKX * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int PIECES = STAGE / 1024 / 8;  // LDS-DMA pieces per wave per stage (A and B halves)
+  constexpr int EPI_LD = BNN + 4;
+  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int ntm = (M + BM - 1) / BM, ntn = (N + BNN - 1) / BNN, ntiles = ntm * ntn;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = wg / ntiles, tile = wg % ntiles;
+  const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BNN;
+  const int nk_all = (K + BKX - 1) / BKX;
+  const int kt_per = (nk_all + splits - 1) / splits;
+  const int kt0 = split * kt_per;
+  const int kt1 = min(nk_all, kt0 + kt_per);
+  const int nk = max(0, kt1 - kt0);
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)((int64_t)K * lda * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, (int)((int64_t)K * ldb * 2), 0x00020000);
+
+  auto stage = [&](int kt, int slot) {
+    char* base = smem + slot * STAGE;
+    stage_tile<AK, BM, BKX, PIECES / 2>(A, lda, M, m0, (kt0 + kt) * BKX, base, wave * (PIECES / 2), lane, rsA);
+    stage_tile<BK, BNN, BKX, PIECES / 2>(B, ldb, N, n0, (kt0 + kt) * BKX, base + A_BYTES, wave * (PIECES / 2), lane,
+                                         rsB);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int p = 0; p < NST - 1; ++p)
+    if (p < nk) stage(p, p);
+  for (int kt = 0; kt < nk; ++kt) {
+    // retire only tile kt (NST-2 younger tiles stay in flight), then publish it
+    if (kt + NST - 2 < nk) wait_vm<(NST - 2) * PIECES>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + NST - 1 < nk) stage(kt + NST - 1, (kt + NST - 1) % NST);
+    const char* sc = smem + (kt % NST) * STAGE;
+#pragma unroll
+    for (int s = 0; s < BKX / 32; ++s) {
+      bf16x8 bfr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = read_frag<BK, BNN, BKX>(sc + A_BYTES, wn * 64 + j * 16, s, lane);
+#pragma unroll
+      for (int ih = 0; ih < 2; ++ih) {
+        bf16x8 af[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = read_frag<AK, BM, BKX>(sc, wm * 128 + (ih * 4 + i) * 16, s, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[ih * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[ih * 4 + i][j], 0, 0, 0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- epilogue, 64 rows at a time through LDS (fp32) -> 8-wide rows
+  float* stg = (float*)smem;
+#pragma unroll
+  for (int h = 0; h < BM / 64; ++h) {
+    if (wm == (h >> 1)) {
+      const int ib = (h & 1) * 4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = i * 16 + (lane >> 4) * 4 + r;
+            const int col = wn * 64 + j * 16 + (lane & 15);
+            stg[row * EPI_LD + col] = acc[ib + i][j][r];
+          }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 64 * BNN / 8 / 512; ++it) {
+      const int idx = it * 512 + tid;
+      const int row = idx >> 5, col = (idx & 31) * 8;
+      const int gm = m0 + h * 64 + row, gn = n0 + col;
+      if (gm < M && gn < N) {
+        float v[8];
+        Vec8<float>::load(stg + row * EPI_LD + col, v);
+        if (ws) Vec8<float>::store(ws + ((int64_t)split * M + gm) * N + gn, v);
+        else epilogue8<OutT>(e, gm, gn, v);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // split-K finish: sum the fp32 slabs, then the regular epilogue.
 template <typename OutT>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, Epi e) {
@@ -386,16 +494,20 @@ static int cfg_override() {
 //   2: 256x128, BK 64, 3-deep ring (144 KiB, 1 WG/CU)
 //   3: 128x128, BK 32, 4-deep ring (64 KiB, 2 WGs/CU)
 //   4: 128x128, BK 32, 3-deep ring (48 KiB, 3 WGs/CU)
-static int slots_of(int cfg) { return cfg == 2 ? 256 : cfg == 4 ? 768 : 512; }  // resident WGs on 256 CUs
-static int tiles_of(int cfg, int M, int N) { return cdiv(M, cfg == 2 ? 256 : 128) * cdiv(N, BN); }
+static bool big_tile(int cfg) { return cfg == 5 || cfg == 6; }
+static int slots_of(int cfg) { return (cfg == 2 || big_tile(cfg)) ? 256 : cfg == 4 ? 768 : 512; }  // resident WGs
+static int tiles_of(int cfg, int M, int N) {
+  return cdiv(M, (cfg == 2 || big_tile(cfg)) ? 256 : 128) * cdiv(N, big_tile(cfg) ? 256 : BN);
+}
 // Measured per shape class (tools/gemm_bench.py, profiles/): the 3-WG/CU BK-32 ring wins when
 // the epilogue carries an activation (its stores overlap other WGs' main loops) and for the
 // split-K weight-gradient GEMMs whose grid fits one round; the 2-WG/CU BK-64 ring elsewhere.
 static int choose_cfg(int M, int N, int K, int a_kmajor, int b_kmajor, int act) {
   int o = cfg_override();
-  if (o == 2 && M < 256) o = 1;
+  if ((o == 2 || big_tile(o)) && M < 256) o = 1;
+  if ((o == 3 || o == 4 || o == 6) && (a_kmajor || b_kmajor) && K % 32) o = 1;
   if ((o == 3 || o == 4) && (a_kmajor || b_kmajor) && K % 32) o = 1;
-  if (o >= 1 && o <= 4) return o;
+  if (o >= 1 && o <= 6) return o;
   if (act && (a_kmajor || b_kmajor) && K % 32 == 0) return 4;
   if (!a_kmajor && !b_kmajor && tiles_of(4, M, N) < slots_of(4)) return 4;
   return 1;
@@ -403,7 +515,7 @@ static int choose_cfg(int M, int N, int K, int a_kmajor, int b_kmajor, int act) 
 // Split-K factor: fill one round of resident workgroups when the tile grid alone cannot
 // (any integer factor; every split keeps >= 4 K-tiles).
 static int choose_splits(int cfg, int M, int N, int K) {
-  const int bk = (cfg == 3 || cfg == 4) ? 32 : 64;
+  const int bk = (cfg == 3 || cfg == 4 || cfg == 6) ? 32 : 64;
   const int tiles = tiles_of(cfg, M, N), slots = slots_of(cfg);
   const int nk = cdiv(K, bk);
   if (2 * tiles >= slots) return 1;
@@ -421,7 +533,7 @@ extern "C" size_t capk_gemm_workspace(int in_dtype, int out_dtype, int M, int N,
   if (in_dtype != CAPK_BF16) return 0;
   // upper bound over the configurations (the launch picks one of them)
   int s = 1;
-  for (int c = 1; c <= 4; ++c) s = std::max(s, choose_splits(c, M, N, K));
+  for (int c = 1; c <= 6; ++c) s = std::max(s, choose_splits(c, M, N, K));
   return s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
 }
 
@@ -461,7 +573,7 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
   const int cfg = choose_cfg(M, N, K, a_kmajor, b_kmajor, act);
   int splits = choose_splits(cfg, M, N, K);
   if (!ws || ws_bytes < (size_t)splits * M * N * sizeof(float)) splits = 1;
-  const int tiles = cdiv(M, cfg == 2 ? 256 : 128) * cdiv(N, BN);
+  const int tiles = tiles_of(cfg, M, N);
   const int grid = tiles * splits;
   float* slab = splits > 1 ? (float*)ws : nullptr;
 #define LAUNCH1(BMX, BKX, NST, AK, BKM, OT)                                                                     \
@@ -470,6 +582,14 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
 #define LAUNCH(AK, BKM, OT)                                    \
   do {                                                         \
     switch (cfg) {                                             \
+      case 5:                                                  \
+        hipLaunchKernelGGL((gemm256_kernel<64, 2, AK, BKM, OT>), dim3(grid), dim3(512), 0, st, (const bf16*)A, \
+                           lda, (const bf16*)B, ldb, M, N, K, splits, e, slab); \
+        break;                                                 \
+      case 6:                                                  \
+        hipLaunchKernelGGL((gemm256_kernel<32, 4, AK, BKM, OT>), dim3(grid), dim3(512), 0, st, (const bf16*)A, \
+                           lda, (const bf16*)B, ldb, M, N, K, splits, e, slab); \
+        break;                                                 \
       case 2: LAUNCH1(256, 64, 3, AK, BKM, OT); break;         \
       case 3: LAUNCH1(128, 32, 4, AK, BKM, OT); break;         \
       case 4: LAUNCH1(128, 32, 3, AK, BKM, OT); break;         \
