@@ -53,6 +53,20 @@ def beam_bench(model, batch, reps, device, rank):
     return dt, gem, int(ids.shape[1])
 
 
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "round1", "gemm_traffic.json")
+
+
+def gemm_traffic():
+    """HBM bytes per GEMM launch from the committed PMC passes over this same command
+    (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md HBM section)."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)
+        return round(t["avg_hbm_bytes"]), os.path.relpath(TRAFFIC_FILE, ROOT)
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
 def build(batch, device):
     import capk
     from capk import config as C
@@ -80,11 +94,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=4)
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-batch", type=int, default=16)
+    ap.add_argument("--cpu-steps", type=int, default=6)
     ap.add_argument("--beam-batch", type=int, default=256, help="images per beam-5 batch (0 = skip)")
     ap.add_argument("--beam-reps", type=int, default=3)
-    ap.add_argument("--cpu-beam-images", type=int, default=4)
+    ap.add_argument("--cpu-beam-images", type=int, default=24)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -98,7 +112,7 @@ def main():
     torch.cuda.set_device(device)
 
     from capk import ops
-    from capk.train.dp import allreduce_grads
+    from capk.train.dp import GradBucketer
     from capk.train.optim import cosine_schedule_with_warmup
     cfg, model, store, opt, loss_fn, cpu_sd = build(args.batch, device)
     B = args.batch
@@ -107,6 +121,8 @@ def main():
     g1 = torch.Generator(device=device).manual_seed(1 + 1000 * rank)
     captions = torch.randint(0, 50256, (B, 20), device=device, generator=g1)
     total_steps = 10_000
+    # DP: gradient all-reduce buckets launched during the backward (capk/train/dp.py)
+    bucketer = GradBucketer(store) if world > 1 else None
     step_no = [0]
     model.train()  # trainer.py:210: decoder dropout (p=0.1) active in the timed step
 
@@ -114,8 +130,8 @@ def main():
         out = model(images=images, captions=captions, caption_lengths=None)
         loss = loss_fn(logits=out["logits"], targets=captions)["total_loss"]
         loss.backward()
-        if world > 1:
-            allreduce_grads(store)
+        if bucketer is not None:
+            bucketer.finish()
         lr = cosine_schedule_with_warmup(step_no[0], cfg.training.learning_rate, cfg.training.warmup_steps,
                                          total_steps)
         opt.step(lr=lr)
@@ -157,6 +173,7 @@ def main():
         ms = elapsed / args.steps * 1e3
         value = B * world * args.steps / elapsed
         achieved = gem["avg_flops"] / (gem["avg_ms"] * 1e-3) / 1e12 if gem["launches"] else 0.0
+        traffic, traffic_src = gemm_traffic()
         rec = {
             "metric": "images/sec train (ViT+Transformer bs=256) at 1/2/4/8 GPUs; beam-5 captions/sec",
             "value": round(value, 2),
@@ -175,7 +192,9 @@ def main():
                        "vocab": 50257, "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "kernel": "gemm_bf16_kernel (all bf16 GEMM launches in the timed steps)",
                          "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                         "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes": round(gem["avg_bytes"]),
                          "launches": gem["launches"], "avg_launch_ms": round(gem["avg_ms"], 4),
                          "gemm_share_of_step": round(gem["total_ms"] / (elapsed * 1e3), 3)},
             "model_flops": {"per_image": FLOP_PER_IMAGE,

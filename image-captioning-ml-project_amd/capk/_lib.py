@@ -16,6 +16,7 @@ BF16 = 1
 
 ACT_NONE, ACT_GELU_ERF, ACT_GELU_TANH, ACT_QUICK_GELU, ACT_TANH, ACT_RELU, ACT_SIGMOID = 0, 1, 2, 3, 4, 5, 6
 ACT_BWD = 16
+ACT_DERIV = 32  # forward: preact <- act'(pre); backward: aux already holds act'(pre)
 
 _c_p = ctypes.c_void_p
 _i = ctypes.c_int

@@ -26,7 +26,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from .._lib import ACT_GELU_TANH
+from .._lib import ACT_DERIV, ACT_GELU_TANH
 from ..ops import HeadView
 from .common import G, CapkModule, W, heads, next_seed
 from .transformer import _padded_grad, _pad64
@@ -217,7 +217,7 @@ class _GPT2Fn(torch.autograd.Function):
             h2, mu2, rs2 = ops.layernorm_fwd(x1, blk.ln_2.weight.detach(), blk.ln_2.bias.detach(), blk.ln_2.eps)
             I = mlp.c_fc.weight.shape[1]
             f_pre = torch.empty(BT, I, dtype=dt, device=dev)
-            f = ops.conv1d(h2, W(mlp.c_fc.weight, dt), mlp.c_fc.bias.detach(), act=ACT_GELU_TANH, preact=f_pre)
+            f = ops.conv1d(h2, W(mlp.c_fc.weight, dt), mlp.c_fc.bias.detach(), act=ACT_GELU_TANH | ACT_DERIV, preact=f_pre)
             x = ops.conv1d(f, W(mlp.c_proj.weight, dt), mlp.c_proj.bias.detach(), residual=x1, drop=drops[2])
             saved.append((x_in, h1, mu1, rs1, qkv, kvb, a, lse, kpu, x1, h2, mu2, rs2, f_pre, f, drops))
         xf, muf, rsf = ops.layernorm_fwd(x, tr.ln_f.weight.detach(), tr.ln_f.bias.detach(), tr.ln_f.eps)
@@ -260,7 +260,7 @@ class _GPT2Fn(torch.autograd.Function):
             saved[li] = None
             # x = x1 + drop(c_proj(gelu_new(c_fc(ln_2 x1))))
             dym = ops.dropout_apply(dx, drops[2])
-            dfp = ops.conv1d_dx(dym, W(mlp.c_proj.weight, dt), act_bwd=ACT_GELU_TANH, aux=f_pre)
+            dfp = ops.conv1d_dx(dym, W(mlp.c_proj.weight, dt), act_bwd=ACT_GELU_TANH | ACT_DERIV, aux=f_pre)
             ops.linear_dw(f, dym, G(mlp.c_proj.weight))
             ops.colsum(dym, G(mlp.c_proj.bias))
             dh2 = ops.conv1d_dx(dfp, W(mlp.c_fc.weight, dt))

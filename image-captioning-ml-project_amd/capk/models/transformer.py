@@ -26,7 +26,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from .._lib import ACT_GELU_ERF
+from .._lib import ACT_DERIV, ACT_GELU_ERF
 from .common import G, CapkModule, W, heads, linear_bwd, next_seed
 from ..ops import HeadView
 
@@ -151,7 +151,7 @@ class _DecoderFn(torch.autograd.Function):
             x2, mu2, rs2 = ops.layernorm_fwd(s2, L.norm2.weight.detach(), L.norm2.bias.detach(), L.norm2.eps)
             I = L.linear1.weight.shape[0]
             f_pre = torch.empty(BT, I, dtype=dt, device=x.device)
-            f = ops.linear(x2, W(L.linear1.weight, dt), L.linear1.bias.detach(), act=ACT_GELU_ERF, preact=f_pre,
+            f = ops.linear(x2, W(L.linear1.weight, dt), L.linear1.bias.detach(), act=ACT_GELU_ERF | ACT_DERIV, preact=f_pre,
                            drop=drops[4])
             s3 = ops.linear(f, W(L.linear2.weight, dt), L.linear2.bias.detach(), residual=x2, drop=drops[5])
             x, mu3, rs3 = ops.layernorm_fwd(s3, L.norm3.weight.detach(), L.norm3.bias.detach(), L.norm3.eps)
@@ -216,7 +216,7 @@ class _DecoderFn(torch.autograd.Function):
 
             # norm3(x2 + dropout3(linear2(dropout(gelu(linear1(x2))))))
             ds3, ds3m = ln_bwd(dx, s3, L.norm3, mu3, rs3, drops[5])
-            dfp = linear_bwd(ds3m, f, L.linear2.weight, L.linear2.bias, dt, act_bwd=ACT_GELU_ERF, aux=f_pre,
+            dfp = linear_bwd(ds3m, f, L.linear2.weight, L.linear2.bias, dt, act_bwd=ACT_GELU_ERF | ACT_DERIV, aux=f_pre,
                              drop=drops[4])
             ops.linear_dw(dfp, x2, G(L.linear1.weight))
             ops.colsum(dfp, G(L.linear1.bias))

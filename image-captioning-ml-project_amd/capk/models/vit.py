@@ -21,8 +21,8 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from .._lib import ACT_GELU_ERF, ACT_TANH
-from ..params import Fused
+from .._lib import ACT_DERIV, ACT_GELU_ERF, ACT_TANH
+from ..params import Fused, notify_final, store_of
 from .common import G, CapkModule, W, heads, linear_bwd, mark
 
 VIT_ARCHS = {
@@ -220,7 +220,8 @@ class _ViTLayerFn(torch.autograd.Function):
         h2, mu2, rs2 = ops.layernorm_fwd(x1, ln2.weight.detach(), ln2.bias.detach(), L.eps)
         I = fc1.weight.shape[0]
         f_pre = torch.empty(x.shape[0], I, dtype=x.dtype, device=x.device)
-        f = ops.linear(h2, W(fc1.weight, dt), fc1.bias.detach(), act=act, preact=f_pre)
+        # f_pre keeps act'(pre) (CAPK_ACT_DERIV): the backward epilogue is a plain multiply
+        f = ops.linear(h2, W(fc1.weight, dt), fc1.bias.detach(), act=act | ACT_DERIV, preact=f_pre)
         y = ops.linear(f, W(fc2.weight, dt), fc2.bias.detach(), residual=x1)
         ctx.L, ctx.B, ctx.N = L, B, N
         ctx.saved = (x, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, f_pre, f)
@@ -238,7 +239,7 @@ class _ViTLayerFn(torch.autograd.Function):
         hd = D // H
         at, fc1, fc2, act = L.attn, L.fc1, L.fc2, L.act
         ln1, ln2 = L.ln1, L.ln2
-        dfp = linear_bwd(dy, f, fc2.weight, fc2.bias, dt, act_bwd=act, aux=f_pre)
+        dfp = linear_bwd(dy, f, fc2.weight, fc2.bias, dt, act_bwd=act | ACT_DERIV, aux=f_pre)
         dh2 = linear_bwd(dfp, h2, fc1.weight, fc1.bias, dt)
         dx1 = ops.layernorm_bwd(dh2, x1, ln2.weight.detach(), mu2, rs2, G(ln2.weight), G(ln2.bias), dres=dy)
         do = linear_bwd(dx1, o, at.o_proj.weight, at.o_proj.bias, dt)
@@ -248,6 +249,7 @@ class _ViTLayerFn(torch.autograd.Function):
                           heads(dqkv, 2 * D, B, N), B, H, N, N, hd, 1.0 / math.sqrt(hd))
         dh1 = linear_bwd(dqkv, h1, None, None, dt, fused=(at.qkv_w, at.qkv_b))
         dx = ops.layernorm_bwd(dh1, x, ln1.weight.detach(), mu1, rs1, G(ln1.weight), G(ln1.bias), dres=dx1)
+        notify_final(store_of(L), L.parameters())  # this layer's gradients are complete
         return dx, None, None, None, None
 
 
@@ -292,4 +294,6 @@ class _ViTHeadFn(torch.autograd.Function):
             ops.linear_dx(dpre, W(dense.weight, dt), out=dcls, beta=1.0)
         ln = m.layernorm
         dx = ops.layernorm_bwd(dseq, x, ln.weight.detach(), mu, rs, G(ln.weight), G(ln.bias))
+        # the decoder and this head are done: everything but the embeddings and the layers is final
+        notify_final(store_of(m), all_except=list(m.embeddings.parameters()) + list(m.layers.parameters()))
         return dx, None, None, None, None

@@ -51,7 +51,7 @@ class KernelTimer:
 
     def __init__(self):
         self.enabled = False
-        self.records = []  # (start_event, end_event, flops, in_dtype)
+        self.records = []  # (start_event, end_event, flops, in_dtype, algorithmic HBM bytes)
 
     def start(self):
         self.records = []
@@ -62,13 +62,14 @@ class KernelTimer:
 
     def summary(self):
         torch.cuda.synchronize()
-        tot_ms, tot_flops, n = 0.0, 0.0, 0
-        for s, e, fl, _ in self.records:
+        tot_ms, tot_flops, tot_bytes, n = 0.0, 0.0, 0.0, 0
+        for s, e, fl, _, by in self.records:
             tot_ms += s.elapsed_time(e)
             tot_flops += fl
+            tot_bytes += by
             n += 1
         return {"launches": n, "total_ms": tot_ms, "flops": tot_flops,
-                "avg_ms": tot_ms / max(n, 1), "avg_flops": tot_flops / max(n, 1)}
+                "avg_ms": tot_ms / max(n, 1), "avg_flops": tot_flops / max(n, 1), "avg_bytes": tot_bytes / max(n, 1)}
 
 
 GEMM_TIMER = KernelTimer()
@@ -96,7 +97,10 @@ def gemm(A, a_kmajor, B, b_kmajor, M, N, K, C, *, lda, ldb, ldc, alpha=1.0, beta
     check(rc, "capk_gemm")
     if timed:
         ev1.record()
-        GEMM_TIMER.records.append((ev0, ev1, 2.0 * M * N * K, it))
+        # algorithmic bytes: A and B read once, C written once (+ read when beta != 0)
+        ein, eout = A.element_size(), C.element_size()
+        nbytes = ein * (M * K + N * K) + eout * M * N * (2 if beta else 1)
+        GEMM_TIMER.records.append((ev0, ev1, 2.0 * M * N * K, it, nbytes))
     return C
 
 

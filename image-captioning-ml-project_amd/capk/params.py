@@ -77,19 +77,17 @@ class ParamStore:
         for m in model.modules():
             for p in getattr(m, "_capk_optional_params", lambda: [])():
                 self.optional.add(id(p))
-        # order: fused groups first (kept adjacent), then the rest in registration order;
-        # optional-grad parameters last within each buffer
+        # order: registration order, a fused group placed (adjacent) at its first member;
+        # optional-grad parameters last within each buffer.  The backward finishes the
+        # modules in reverse registration order, so the final gradients of each buffer
+        # grow as a suffix (dp.GradBucketer launches its all-reduce buckets from that).
         seen = set()
         order = []
-        for f in fused:
-            for p in f.params:
-                if id(p) not in seen:
-                    seen.add(id(p))
-                    order.append(p)
         for _, p in named:
-            if id(p) not in seen:
-                seen.add(id(p))
-                order.append(p)
+            for q in (in_fused[id(p)].params if id(p) in in_fused else (p,)):
+                if id(q) not in seen:
+                    seen.add(id(q))
+                    order.append(q)
         for p in order:
             g = "no_decay" if no_decay(names[id(p)]) else "decay"
             self.groups[g].append(p)
@@ -203,6 +201,21 @@ class ParamStore:
 
 def store_of(module):
     return getattr(module, "_capk_store", None)
+
+
+def notify_final(store, params=None, all_except=None):
+    """Tell the store's gradient bucketer (dp.GradBucketer, if one is installed) that the
+    gradients of `params` -- or of every parameter not in `all_except` -- are final for
+    this backward.  No-op without a bucketer (single process)."""
+    b = getattr(store, "_capk_bucketer", None) if store is not None else None
+    if b is None or not b.active:
+        return
+    if all_except is not None:
+        skip = {id(p) for p in all_except}
+        ids = [id(p) for p in store.params if id(p) not in skip]
+    else:
+        ids = [id(p) for p in params]
+    b.mark_final(ids)
 
 
 def attach(model, device, bf16_shadow=True):

@@ -1,18 +1,33 @@
 """Data parallelism: one process per GPU, gradient all-reduce over RCCL/xGMI.
 
-The reference has no distributed code; the build adds plain DP:
-every rank computes the full train step on its own batch shard and the flat
-fp32 gradient buffers of the ParamStore are averaged with bucketed
+The reference has no distributed code; the build adds plain DP
+(SURVEY §8e): every rank computes the full train step on its own batch shard and
+the flat fp32 gradient buffers of the ParamStore are averaged with bucketed
 ``all_reduce`` (backend "nccl" = RCCL on ROCm).  Buckets are contiguous slices
-of the flat buffers (no packing copies).  Buckets can be launched while the
-backward is still running (``GradBucketer.launch_ready``) on a side stream so
-the exchange overlaps the remaining backward; ``finish()`` joins them before the
-optimizer step.
+of the flat buffers (no packing copies).
+
+``GradBucketer`` overlaps that exchange with the backward.  Model code reports
+when gradients are final (``params.notify_final``: each encoder layer at the end
+of its backward, the encoder head once the decoder and the head are done).  The
+flat buffers are laid out in registration order (params.py) and the backward
+finishes the modules in reverse order, so in every buffer the final gradients
+form a growing suffix.  Whenever that suffix has grown by a bucket, the bucketer
+launches ``all_reduce(async_op=True)`` on it: RCCL runs the collective on its own
+stream, ordered after the work already queued on the compute stream, while the
+compute stream carries on with the next layer's backward.  ``finish()`` launches
+the remainder and makes the compute stream wait for every collective before the
+optimizer step.  Every rank issues the same collectives in the same order (the
+notifications follow the same backward on every rank).
 """
-import torch
 import torch.distributed as dist
 
+from ..params import _alloc_numel, _round
+
 BUCKET_ELEMS = 16 * 1024 * 1024  # 64 MiB of fp32 per all-reduce
+
+
+def _active():
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
 def _avg_op():
@@ -23,7 +38,7 @@ def _avg_op():
 
 def allreduce_grads(store, bucket_elems=BUCKET_ELEMS):
     """Average every gradient buffer across ranks (blocking on the current stream)."""
-    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size() == 1:
+    if not _active():
         return
     op, need_scale = _avg_op()
     world = dist.get_world_size()
@@ -35,3 +50,61 @@ def allreduce_grads(store, bucket_elems=BUCKET_ELEMS):
             dist.all_reduce(chunk, op=op)
             if need_scale:
                 chunk.div_(world)
+
+
+class GradBucketer:
+    """Backward-overlapped gradient averaging for one ParamStore.
+
+    Per step: ``loss.backward(); bucketer.finish(); optimizer.step()``.
+    Installs itself on the store (``store._capk_bucketer``) so model code can notify it.
+    """
+
+    def __init__(self, store, bucket_elems=BUCKET_ELEMS):
+        self.store = store
+        self.bucket_elems = int(bucket_elems)
+        self.active = _active()
+        # per group: [start, end) of every parameter, in buffer order
+        self.spans = {}
+        for g, plist in store.groups.items():
+            self.spans[g] = sorted((p._capk_offset, p._capk_offset + _round(_alloc_numel(p)), id(p)) for p in plist)
+        if self.active:
+            self.op, self.need_scale = _avg_op()
+            self.world = dist.get_world_size()
+        store._capk_bucketer = self
+        self.reset()
+
+    def reset(self):
+        self.final = set()
+        self.works = []
+        self.k = {g: 0 for g in self.spans}                       # spans known final, counted from the end
+        self.lo = {g: self.store.grad[g].numel() for g in self.spans}  # start of the final suffix
+        self.hi = dict(self.lo)                                    # [hi, end) already launched
+
+    def mark_final(self, ids):
+        self.final.update(ids)
+        for g, spans in self.spans.items():
+            n = len(spans)
+            while self.k[g] < n and spans[n - 1 - self.k[g]][2] in self.final:
+                self.lo[g] = spans[n - 1 - self.k[g]][0]
+                self.k[g] += 1
+            if self.hi[g] - self.lo[g] >= self.bucket_elems:
+                self._launch(g, self.lo[g], self.hi[g])
+                self.hi[g] = self.lo[g]
+
+    def _launch(self, g, lo, hi):
+        buf = self.store.grad[g]
+        for s in range(lo, hi, self.bucket_elems):
+            chunk = buf[s:min(hi, s + self.bucket_elems)]
+            self.works.append((dist.all_reduce(chunk, op=self.op, async_op=True), chunk))
+
+    def finish(self):
+        """Launch what is left, then join every collective (the current stream waits)."""
+        if self.active:
+            for g in self.spans:
+                if self.hi[g] > 0:
+                    self._launch(g, 0, self.hi[g])
+            for work, chunk in self.works:
+                work.wait()
+                if self.need_scale:
+                    chunk.div_(self.world)
+        self.reset()

@@ -72,6 +72,43 @@ template <> struct Vec8<bf16> {
   }
 };
 
+// ------------------------------------------------------ partial-sum finish ---
+// Column i of part[nparts][ld] summed over the parts ph, ph+PH, ph+2PH, ... with four
+// independent accumulators (four loads in flight per thread).  The finish kernels run
+// 16 columns x 64 part-phases per 1024-thread block and reduce the phases in LDS:
+// deterministic, and the whole partial matrix is read in about one memory round trip.
+template <int PH>
+__device__ __forceinline__ float sum_parts(const float* __restrict__ part, int64_t ld, int nparts, int i, int ph) {
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int b = ph;
+  for (; b + 3 * PH < nparts; b += 4 * PH) {
+    s0 += part[(int64_t)b * ld + i];
+    s1 += part[(int64_t)(b + PH) * ld + i];
+    s2 += part[(int64_t)(b + 2 * PH) * ld + i];
+    s3 += part[(int64_t)(b + 3 * PH) * ld + i];
+  }
+  for (; b < nparts; b += PH) s0 += part[(int64_t)b * ld + i];
+  return (s0 + s1) + (s2 + s3);
+}
+// 1024-thread finish block: returns the column total in threads 0..15 (column blockIdx.x*16 + tid).
+__device__ __forceinline__ float finish_parts16(const float* __restrict__ part, int64_t ld, int nparts, int ncols) {
+  __shared__ float red[64][17];
+  const int c = threadIdx.x & 15, ph = threadIdx.x >> 4;
+  const int i = blockIdx.x * 16 + c;
+  red[ph][c] = i < ncols ? sum_parts<64>(part, ld, nparts, i, ph) : 0.f;
+  __syncthreads();
+  if (threadIdx.x < 64) {  // 4 lanes per column, 16 phases each, then two shuffles
+    const int cc = threadIdx.x & 15, q = threadIdx.x >> 4;
+    float s = 0.f;
+#pragma unroll
+    for (int p = 0; p < 16; ++p) s += red[q * 16 + p][cc];
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    return s;
+  }
+  return 0.f;
+}
+
 // ------------------------------------------------------------ activations ---
 __device__ __forceinline__ float act_fwd(int act, float x) {
   switch (act) {
@@ -131,6 +168,12 @@ __device__ __forceinline__ float act_fwd_fast(int act, float x) {
 __device__ __forceinline__ float act_grad_fast(int act, float x) {
   if (act == CAPK_ACT_GELU_ERF) { float c, p; phi_fast(x, c, p); return c + x * p; }
   return act_grad(act, x);
+}
+// act(x) and act'(x) together (one Phi/phi evaluation for GELU): CAPK_ACT_DERIV epilogues
+__device__ __forceinline__ float act_fwd_grad_fast(int act, float x, float& d) {
+  if (act == CAPK_ACT_GELU_ERF) { float c, p; phi_fast(x, c, p); d = c + x * p; return x * c; }
+  d = act_grad(act, x);
+  return act_fwd(act, x);
 }
 
 // --------------------------------------------------------------- dropout ----

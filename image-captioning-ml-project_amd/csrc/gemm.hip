@@ -37,8 +37,24 @@ struct Epi {
   Drop drop;  // mask index m*N + n, applied after the activation (or with act'), before the residual
 };
 
+// One 8-wide row segment of an epilogue side operand (aux or residual), raw in registers.
+template <typename T> struct Raw8;
+template <> struct Raw8<bf16> {
+  bf16x8 v;
+  __device__ __forceinline__ void load(const bf16* p) { v = *(const bf16x8*)p; }
+  __device__ __forceinline__ float get(int i) const { return (float)v[i]; }
+};
+template <> struct Raw8<float> {
+  f32x4 a, b;
+  __device__ __forceinline__ void load(const float* p) { a = *(const f32x4*)p; b = *(const f32x4*)(p + 4); }
+  __device__ __forceinline__ float get(int i) const { return i < 4 ? a[i] : b[i - 4]; }
+};
+
+// bias8 / side: operands the caller loaded before its first store (nullptr: load here).
+// side is aux for a backward activation, else the residual.
 template <typename OutT>
-__device__ __forceinline__ void epilogue8(const Epi& e, int m, int n, float (&v)[8]) {
+__device__ __forceinline__ void epilogue8(const Epi& e, int m, int n, float (&v)[8], const float* bias8 = nullptr,
+                                          const Raw8<OutT>* side = nullptr) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) v[i] *= e.alpha;
   if (e.beta != 0.f) {
@@ -49,20 +65,43 @@ __device__ __forceinline__ void epilogue8(const Epi& e, int m, int n, float (&v)
   }
   if (e.bias) {
     float b[8];
-    Vec8<float>::load(e.bias + n, b);
+    if (bias8) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) b[i] = bias8[i];
+    } else {
+      Vec8<float>::load(e.bias + n, b);
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] += b[i];
   }
   if (e.act & CAPK_ACT_BWD) {
     float a[8];
-    Vec8<OutT>::load((const OutT*)e.aux + (int64_t)m * e.ldx + n, a);
+    if (side) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] = side->get(i);
+    } else {
+      Vec8<OutT>::load((const OutT*)e.aux + (int64_t)m * e.ldx + n, a);
+    }
     const int act = e.act & 15;
+    if (e.act & CAPK_ACT_DERIV) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] *= act_grad_fast(act, a[i]);
+      for (int i = 0; i < 8; ++i) v[i] *= a[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] *= act_grad_fast(act, a[i]);
+    }
   } else if (e.act) {
-    if (e.pre) Vec8<OutT>::store((OutT*)e.pre + (int64_t)m * e.ldx + n, v);
+    const int act = e.act & 15;
+    if (e.pre && (e.act & CAPK_ACT_DERIV)) {
+      float d[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = act_fwd_fast(e.act, v[i]);
+      for (int i = 0; i < 8; ++i) v[i] = act_fwd_grad_fast(act, v[i], d[i]);
+      Vec8<OutT>::store((OutT*)e.pre + (int64_t)m * e.ldx + n, d);
+    } else {
+      if (e.pre) Vec8<OutT>::store((OutT*)e.pre + (int64_t)m * e.ldx + n, v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = act_fwd_fast(act, v[i]);
+    }
   }
   if (e.drop.on()) {
     const uint64_t base = (uint64_t)m * e.N + n;
@@ -71,11 +110,48 @@ __device__ __forceinline__ void epilogue8(const Epi& e, int m, int n, float (&v)
   }
   if (e.res) {
     float r[8];
-    Vec8<OutT>::load((const OutT*)e.res + (int64_t)m * e.ldr + n, r);
+    if (side && !(e.act & CAPK_ACT_BWD)) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r[i] = side->get(i);
+    } else {
+      Vec8<OutT>::load((const OutT*)e.res + (int64_t)m * e.ldr + n, r);
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] += r[i];
   }
   Vec8<OutT>::store((OutT*)e.C + (int64_t)m * e.ldc + n, v);
+}
+
+// Epilogue operand prefetch.  On gfx9 vmcnt counts stores as well as loads, in order,
+// so a load issued after a store cannot be waited for without waiting for that store:
+// an epilogue that loads bias / aux / residual per 8-wide segment serialises one
+// store round trip per segment.  Kernels therefore load every side segment of the
+// tile (and the thread's bias columns) before the first store, and separate the LDS
+// staging chunks with LDS-only barriers (s_waitcnt lgkmcnt(0) + s_barrier) instead of
+// __syncthreads, which would also drain the stores.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <typename OutT, int NH, int ITS, int THREADS, int SEGS_PER_ROW>
+__device__ __forceinline__ bool prefetch_side(const Epi& e, int m0, int gn, int tid, float (&bias8)[8],
+                                              Raw8<OutT> (&side)[NH][ITS]) {
+  const bool bwd = e.act & CAPK_ACT_BWD;
+  const OutT* sp = (const OutT*)(bwd ? e.aux : e.res);
+  const int64_t sld = bwd ? e.ldx : e.ldr;
+  if (gn >= e.N) return false;
+  if (e.bias) Vec8<float>::load(e.bias + gn, bias8);
+  if (!sp) return false;
+#pragma unroll
+  for (int h = 0; h < NH; ++h)
+#pragma unroll
+    for (int it = 0; it < ITS; ++it) {
+      const int gm = m0 + h * 64 + (it * THREADS + tid) / SEGS_PER_ROW;
+      if (gm < e.M) side[h][it].load(sp + (int64_t)gm * sld + gn);
+    }
+  return true;
 }
 
 template <typename OutT>
@@ -84,10 +160,12 @@ __device__ __forceinline__ void epilogue1(const Epi& e, int m, int n, float v) {
   if (e.beta != 0.f) v += e.beta * to_f32(((const OutT*)e.C)[(int64_t)m * e.ldc + n]);
   if (e.bias) v += e.bias[n];
   if (e.act & CAPK_ACT_BWD) {
-    v *= act_grad(e.act & 15, to_f32(((const OutT*)e.aux)[(int64_t)m * e.ldx + n]));
+    const float a = to_f32(((const OutT*)e.aux)[(int64_t)m * e.ldx + n]);
+    v *= (e.act & CAPK_ACT_DERIV) ? a : act_grad(e.act & 15, a);
   } else if (e.act) {
-    if (e.pre) ((OutT*)e.pre)[(int64_t)m * e.ldx + n] = from_f32<OutT>(v);
-    v = act_fwd(e.act, v);
+    if (e.pre)
+      ((OutT*)e.pre)[(int64_t)m * e.ldx + n] = from_f32<OutT>((e.act & CAPK_ACT_DERIV) ? act_grad(e.act & 15, v) : v);
+    v = act_fwd(e.act & 15, v);
   }
   if (e.drop.on()) v *= e.drop.mul((uint64_t)m * e.N + n);
   if (e.res) v += to_f32(((const OutT*)e.res)[(int64_t)m * e.ldr + n]);
@@ -261,10 +339,16 @@ __global__ __launch_bounds__(BMX / 32 * 64) void gemm_bf16_kernel(
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  // (the last K-tile was waited with vmcnt(0): no operand load is outstanding here)
 
-  // ---- epilogue, 64 rows at a time: accumulators -> LDS (fp32) -> 8-wide rows
+  // ---- epilogue, 64 rows at a time: accumulators -> LDS (fp32) -> 8-wide rows.
+  // Each thread owns the same 8 columns in every row it stores (THREADS % 16 == 0).
+  constexpr int ITS = 64 * BN / 8 / C::THREADS;
+  const int ecol = (tid & 15) * 8, egn = n0 + ecol;
+  float bias8[8];
+  Raw8<OutT> side[BMX / 64][ITS];
+  const bool has_side = !ws && prefetch_side<OutT, BMX / 64, ITS, C::THREADS, 16>(e, m0, egn, tid, bias8, side);
+  lds_barrier();
   float* stg = (float*)smem;
 #pragma unroll
   for (int h = 0; h < BMX / 64; ++h) {
@@ -280,20 +364,19 @@ __global__ __launch_bounds__(BMX / 32 * 64) void gemm_bf16_kernel(
             stg[row * C::EPI_LD + col] = acc[i][j][r];
           }
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
-    for (int it = 0; it < 64 * BN / 8 / C::THREADS; ++it) {
-      const int idx = it * C::THREADS + tid;
-      const int row = idx >> 4, col = (idx & 15) * 8;
-      const int gm = m0 + h * 64 + row, gn = n0 + col;
-      if (gm < M && gn < N) {
+    for (int it = 0; it < ITS; ++it) {
+      const int row = (it * C::THREADS + tid) >> 4;
+      const int gm = m0 + h * 64 + row;
+      if (gm < M && egn < N) {
         float v[8];
-        Vec8<float>::load(stg + row * C::EPI_LD + col, v);
-        if (ws) Vec8<float>::store(ws + ((int64_t)split * M + gm) * N + gn, v);
-        else epilogue8<OutT>(e, gm, gn, v);
+        Vec8<float>::load(stg + row * C::EPI_LD + ecol, v);
+        if (ws) Vec8<float>::store(ws + ((int64_t)split * M + gm) * N + egn, v);
+        else epilogue8<OutT>(e, gm, egn, v, e.bias ? bias8 : nullptr, has_side ? &side[h][it] : nullptr);
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
 }
 
@@ -368,10 +451,15 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
       }
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  // (the last K-tile was waited with vmcnt(0): no operand load is outstanding here)
 
-  // ---- epilogue, 64 rows at a time through LDS (fp32) -> 8-wide rows
+  // ---- epilogue, 64 rows at a time through LDS (fp32) -> 8-wide rows (fixed 8 columns per thread)
+  constexpr int ITS = 64 * BNN / 8 / 512;
+  const int ecol = (tid & 31) * 8, egn = n0 + ecol;
+  float bias8[8];
+  Raw8<OutT> side[BM / 64][ITS];
+  const bool has_side = !ws && prefetch_side<OutT, BM / 64, ITS, 512, 32>(e, m0, egn, tid, bias8, side);
+  lds_barrier();
   float* stg = (float*)smem;
 #pragma unroll
   for (int h = 0; h < BM / 64; ++h) {
@@ -388,20 +476,19 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
             stg[row * EPI_LD + col] = acc[ib + i][j][r];
           }
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
-    for (int it = 0; it < 64 * BNN / 8 / 512; ++it) {
-      const int idx = it * 512 + tid;
-      const int row = idx >> 5, col = (idx & 31) * 8;
-      const int gm = m0 + h * 64 + row, gn = n0 + col;
-      if (gm < M && gn < N) {
+    for (int it = 0; it < ITS; ++it) {
+      const int row = (it * 512 + tid) >> 5;
+      const int gm = m0 + h * 64 + row;
+      if (gm < M && egn < N) {
         float v[8];
-        Vec8<float>::load(stg + row * EPI_LD + col, v);
-        if (ws) Vec8<float>::store(ws + ((int64_t)split * M + gm) * N + gn, v);
-        else epilogue8<OutT>(e, gm, gn, v);
+        Vec8<float>::load(stg + row * EPI_LD + ecol, v);
+        if (ws) Vec8<float>::store(ws + ((int64_t)split * M + gm) * N + egn, v);
+        else epilogue8<OutT>(e, gm, egn, v, e.bias ? bias8 : nullptr, has_side ? &side[h][it] : nullptr);
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
 }
 
@@ -506,7 +593,6 @@ static int choose_cfg(int M, int N, int K, int a_kmajor, int b_kmajor, int act) 
   int o = cfg_override();
   if ((o == 2 || big_tile(o)) && M < 256) o = 1;
   if ((o == 3 || o == 4 || o == 6) && (a_kmajor || b_kmajor) && K % 32) o = 1;
-  if ((o == 3 || o == 4) && (a_kmajor || b_kmajor) && K % 32) o = 1;
   if (o >= 1 && o <= 6) return o;
   if (act && (a_kmajor || b_kmajor) && K % 32 == 0) return 4;
   if (!a_kmajor && !b_kmajor && tiles_of(4, M, N) < slots_of(4)) return 4;

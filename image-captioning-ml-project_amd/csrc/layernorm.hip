@@ -147,20 +147,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T
   }
 }
 
-// sum the per-block partials: 64 columns x 4 row-phases per 256-thread block, coalesced
-__global__ __launch_bounds__(256) void ln_bwd_finish_kernel(int nblocks, int cols, const float* __restrict__ part,
-                                                            float* __restrict__ dw, float* __restrict__ db,
-                                                            int accumulate) {
-  __shared__ float red[4][64];
-  const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
-  const int i = blockIdx.x * 64 + lane;  // index into [2*cols]
-  float s = 0.f;
-  if (i < 2 * cols)
-    for (int bidx = ph; bidx < nblocks; bidx += 4) s += part[(int64_t)bidx * 2 * cols + i];
-  red[ph][lane] = s;
-  __syncthreads();
-  if (ph == 0 && i < 2 * cols) {
-    s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+// sum the per-block partials [nblocks][2*cols] (sum_parts / finish_parts16, common.h)
+__global__ __launch_bounds__(1024) void ln_bwd_finish_kernel(int nblocks, int cols, const float* __restrict__ part,
+                                                             float* __restrict__ dw, float* __restrict__ db,
+                                                             int accumulate) {
+  const float s = finish_parts16(part, 2 * cols, nblocks, 2 * cols);
+  const int i = blockIdx.x * 16 + threadIdx.x;
+  if (threadIdx.x < 16 && i < 2 * cols) {
     float* dst = i < cols ? dw + i : db + (i - cols);
     *dst = accumulate ? *dst + s : s;
   }
@@ -211,7 +204,7 @@ extern "C" int capk_layernorm_bwd(int dtype, int rows, int cols, const void* dy,
   else { set_error("capk_layernorm_bwd: dtype"); return CAPK_EINVAL; }
 #undef L
   CAPK_LAUNCH_CHECK("ln_bwd_kernel");
-  hipLaunchKernelGGL(ln_bwd_finish_kernel, dim3(cdiv(2 * cols, 64)), dim3(256), 0, st, nb, cols, (const float*)ws, dw,
+  hipLaunchKernelGGL(ln_bwd_finish_kernel, dim3(cdiv(2 * cols, 16)), dim3(1024), 0, st, nb, cols, (const float*)ws, dw,
                      db, accumulate);
   CAPK_LAUNCH_CHECK("ln_bwd_finish_kernel");
   return CAPK_OK;

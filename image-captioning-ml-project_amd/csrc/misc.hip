@@ -213,7 +213,7 @@ __global__ void ce_finish_kernel(int rows, const float* __restrict__ row_loss, c
 }
 
 // ------------------------------------------------------------ colsum --------
-constexpr int CS_ROWS_PER_SPLIT = 128;
+constexpr int CS_ROWS_PER_SPLIT = 256;
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_kernel(int M, int N, const T* __restrict__ dy, int64_t ldy,
                                                      float* __restrict__ part) {
@@ -223,7 +223,17 @@ __global__ __launch_bounds__(256) void colsum_kernel(int M, int N, const T* __re
   const int m0 = blockIdx.y * CS_ROWS_PER_SPLIT, m1 = min(M, m0 + CS_ROWS_PER_SPLIT);
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (c * 8 < N) {
-    for (int m = m0 + ph; m < m1; m += 4) {
+    int m = m0 + ph;
+    for (; m + 12 < m1; m += 16) {  // four independent row loads in flight
+      float v0[8], v1[8], v2[8], v3[8];
+      Vec8<T>::load(dy + (int64_t)m * ldy + c * 8, v0);
+      Vec8<T>::load(dy + (int64_t)(m + 4) * ldy + c * 8, v1);
+      Vec8<T>::load(dy + (int64_t)(m + 8) * ldy + c * 8, v2);
+      Vec8<T>::load(dy + (int64_t)(m + 12) * ldy + c * 8, v3);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += (v0[i] + v1[i]) + (v2[i] + v3[i]);
+    }
+    for (; m < m1; m += 4) {
       float v[8];
       Vec8<T>::load(dy + (int64_t)m * ldy + c * 8, v);
 #pragma unroll
@@ -239,20 +249,11 @@ __global__ __launch_bounds__(256) void colsum_kernel(int M, int N, const T* __re
   }
 }
 
-__global__ __launch_bounds__(256) void colsum_finish_kernel(int splits, int N, const float* __restrict__ part,
-                                                            float* __restrict__ out, int accumulate) {
-  __shared__ float red[4][64];
-  const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
-  const int n = blockIdx.x * 64 + lane;
-  float s = 0.f;
-  if (n < N)
-    for (int k = ph; k < splits; k += 4) s += part[(int64_t)k * N + n];
-  red[ph][lane] = s;
-  __syncthreads();
-  if (ph == 0 && n < N) {
-    s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-    out[n] = accumulate ? out[n] + s : s;
-  }
+__global__ __launch_bounds__(1024) void colsum_finish_kernel(int splits, int N, const float* __restrict__ part,
+                                                             float* __restrict__ out, int accumulate) {
+  const float s = finish_parts16(part, N, splits, N);
+  const int n = blockIdx.x * 16 + threadIdx.x;
+  if (threadIdx.x < 16 && n < N) out[n] = accumulate ? out[n] + s : s;
 }
 
 // ------------------------------------------------------------ copies -------
@@ -415,7 +416,7 @@ extern "C" int capk_colsum(int dtype, int M, int N, const void* dy, int64_t ldy,
   DT_DISPATCH(dtype, L, 0)
 #undef L
   CAPK_LAUNCH_CHECK("colsum_kernel");
-  hipLaunchKernelGGL(colsum_finish_kernel, dim3(cdiv(N, 64)), dim3(256), 0, S(stream), splits, N, (const float*)ws, db,
+  hipLaunchKernelGGL(colsum_finish_kernel, dim3(cdiv(N, 16)), dim3(1024), 0, S(stream), splits, N, (const float*)ws, db,
                      accumulate);
   CAPK_LAUNCH_CHECK("colsum_finish_kernel");
   return CAPK_OK;

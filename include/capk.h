@@ -41,6 +41,8 @@ extern "C" {
 #define CAPK_ACT_SIGMOID 6    /* AoA info gate, adaptive sentinel gate (attention.py:258,318) */
 /* backward forms: out = acc * act'(aux) where aux is the saved pre-activation */
 #define CAPK_ACT_BWD 16
+#define CAPK_ACT_DERIV 32 /* forward: preact receives act'(pre) instead of pre; with CAPK_ACT_BWD:
+                           aux already holds act'(pre), so v = pre * aux[m,n] (no activation math) */
 
 const char* capk_last_error(void);
 int capk_version(void);

@@ -91,6 +91,56 @@ def _worker(rank, world, port, golden, out):
     dist.destroy_process_group()
 
 
+def _worker_overlap(rank, world, port, golden, out):
+    """GradBucketer: gradients become final in reverse registration order (as in the
+    backward), each followed by a notification; buckets launch asynchronously while
+    later gradients are still being written."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    m, sd, dims = _tiny(golden)
+    from capk.params import attach, notify_final
+    from capk.train.dp import GradBucketer
+    store = attach(m, "cpu")
+    bucketer = GradBucketer(store, bucket_elems=1000)
+    D, Le, He, Ld, Hd, V, pad, patch, img = dims
+    g = torch.Generator().manual_seed(123)
+    images = torch.randn(4, 3, img, img, generator=g)
+    caps = torch.randint(0, V - 1, (4, 7), generator=g)
+    shard = slice(rank * 2, rank * 2 + 2)
+    named = dict(m.named_parameters())
+    full = _oracle_grads(sd, dims, images, caps)
+    for step in range(2):  # the bucketer resets between steps
+        grads = _oracle_grads(sd, dims, images[shard], caps[shard])
+        for buf in store.grad.values():
+            buf.fill_(float("nan"))  # a bucket launched before its gradients were written would poison the result
+        launched = []
+        # the optional pooler (buffer tail) is final with the encoder head, before the encoder layers
+        order = [n for n in reversed(list(named)) if id(named[n]) in store.optional]
+        order += [n for n in reversed(list(named)) if id(named[n]) not in store.optional]
+        for n in order:
+            with torch.no_grad():
+                named[n]._capk_grad.copy_(grads[n])
+            notify_final(store, [named[n]])
+            launched.append(len(bucketer.works))
+        bucketer.finish()
+        err = max(float((named[n]._capk_grad - full[n]).abs().max()) for n in full)
+        if rank == 0:
+            torch.save({"err": err, "early": launched[len(launched) // 2]}, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_overlapped_buckets_equal_full_batch(tmp_path, golden_dir):
+    out = str(tmp_path / "dpo.pt")
+    golden = os.path.join(golden_dir, "vit_transformer_step.npz")
+    mp.spawn(_worker_overlap, args=(2, _free_port(), golden, out), nprocs=2, join=True)
+    res = torch.load(out, weights_only=True)
+    assert res["err"] < 1e-5, res
+    assert res["early"] > 0, res  # collectives were in flight before the last gradient was written
+
+
 def test_dp_allreduce_equals_full_batch(tmp_path, golden_dir):
     out = str(tmp_path / "dp.pt")
     golden = os.path.join(golden_dir, "vit_transformer_step.npz")
