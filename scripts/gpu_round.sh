@@ -23,6 +23,7 @@ python -c "import torch;print(torch.cuda.get_device_name(0), torch.cuda.get_devi
 [[ $STEPS == *resnet* ]] && run resnet 900 python -u -m pytest tests/test_gpu_resnet.py -q -rf --timeout 300 --timeout-method thread
 [[ $STEPS == *legacy* ]] && run legacy 900 python -u -m pytest tests/test_gpu_legacy.py -q -rf --timeout 300 --timeout-method thread
 [[ $STEPS == *cfg4* ]] && run cfg4 900 python -m pytest tests/test_gpu_config4.py -q -rf
+[[ $STEPS == *dp* ]] && run dp 300 python -u -m pytest tests/test_gpu_dp.py -q -rf --timeout 240 --timeout-method thread
 [[ $STEPS == *model* ]] && run model 900 python -m pytest tests/test_gpu_model.py -q -rf
 [[ $STEPS == *gemm* ]] && run gemm 300 python tools/gemm_bench.py
 [[ $STEPS == *smoke* ]] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
