@@ -16,6 +16,8 @@
 //       blocks): S^T, dP^T recomputed; dQ^T += K^T dS^T (K^T by tr reads).  No
 //       atomics: every output element has one owner.
 // f32 path (parity): straightforward per-query / per-key loops, exact fp32.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace capk {
@@ -150,70 +152,62 @@ __global__ __launch_bounds__(512) void attn_fwd_bf16(AttnArgs a) {
   }
   __syncthreads();
 
-  const int NKB = NKP / 16;
   const float sl2 = a.scale * kLog2e;  // scores kept in the log2 domain: exp2(s*scale*log2e - max)
+  // Online softmax over 32-key chunks (two 16-key S blocks = one PV MFMA step): only one
+  // chunk of scores is live, so the wave stays far below 128 VGPRs and two workgroups
+  // share a CU (the whole-row version held 16 score blocks and spilled).
   for (int qt = wave; qt * 16 < a.Nq; qt += nwaves) {
     if (qt != wave) load_q_frags<HDP>(a, qsrc, qt, lane, qf);
     const int qi = qt * 16 + (lane & 15);
-    f32x4 sc[16];
-    float mx = -INFINITY;
+    float m = -INFINITY, l = 0.f;  // running max (per query, reduced over the lane group), lane-partial sum
+    f32x4 o[HDP / 16];
 #pragma unroll
-    for (int kb = 0; kb < 16; ++kb) {
-      if (kb < NKB) {
+    for (int db = 0; db < HDP / 16; ++db) o[db] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < NKP / 32; ++t) {
+      f32x4 sc[2];
+      float cm = -INFINITY;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int kb = 2 * t + c;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < HDP / 32; ++s) {
           bf16x8 kf = *(const bf16x8*)(Ks + (kb * 16 + (lane & 15)) * ST + s * 32 + 8 * (lane >> 4));
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s], acc, 0, 0, 0);
         }
+        const bool full = full_kb(a, kb);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          if (full_kb(a, kb)) {
-            acc[r] *= sl2;
-          } else {
-            const int key = kb * 16 + (lane >> 4) * 4 + r;
-            acc[r] = key_ok(a, b, key, qi) ? acc[r] * sl2 : -INFINITY;
-          }
-          mx = fmaxf(mx, acc[r]);
+          const int key = kb * 16 + (lane >> 4) * 4 + r;
+          acc[r] = (full || key_ok(a, b, key, qi)) ? acc[r] * sl2 : -INFINITY;
+          cm = fmaxf(cm, acc[r]);
         }
-        sc[kb] = acc;
+        sc[c] = acc;
       }
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    float l = 0.f;
+      cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+      cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+      const float mn = fmaxf(m, cm);
+      const float mref = mn == -INFINITY ? 0.f : mn;  // nothing unmasked yet: p = 0, no NaN
+      const float alpha = exp2f(m - mref);
+      m = mn;
+      l *= alpha;
 #pragma unroll
-    for (int kb = 0; kb < 16; ++kb) {
-      if (kb < NKB) {
+      for (int db = 0; db < HDP / 16; ++db) o[db] *= alpha;
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(sc[kb][r] - mx);
-          sc[kb][r] = p;
-          l += p;
+          const float p = exp2f(sc[c][r] - mref);
+          l += p;  // the normaliser excludes dropout
+          sc[c][r] = a.drop.on() ? p * pdrop(a, b, h, qi, (2 * t + c) * 16 + (lane >> 4) * 4 + r) : p;
         }
-      }
+      const bf16x8 pb = pack8(sc[0], sc[1]);
+#pragma unroll
+      for (int db = 0; db < HDP / 16; ++db)  // O^T += V^T P^T, V^T fragments by transposed LDS reads
+        o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_read8(Vs, ST, 32 * t, db * 16, lane), pb, o[db], 0, 0, 0);
     }
     l += __shfl_xor(l, 16, 64);
     l += __shfl_xor(l, 32, 64);
-    if (a.drop.on()) {  // dropout on the normalised probabilities (normaliser l unchanged)
-#pragma unroll
-      for (int kb = 0; kb < 16; ++kb)
-        if (kb < NKB)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) sc[kb][r] *= pdrop(a, b, h, qi, kb * 16 + (lane >> 4) * 4 + r);
-    }
-    f32x4 o[HDP / 16];
-#pragma unroll
-    for (int db = 0; db < HDP / 16; ++db) o[db] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      if (2 * t < NKB) {
-        const bf16x8 pb = pack8(sc[2 * t], sc[2 * t + 1]);
-#pragma unroll
-        for (int db = 0; db < HDP / 16; ++db)  // O^T += V^T P^T, V^T fragments by transposed LDS reads
-          o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_read8(Vs, ST, 32 * t, db * 16, lane), pb, o[db], 0, 0, 0);
-      }
-    }
     if (qi < a.Nq) {
       const float inv = 1.f / l;
       bf16* orow = (bf16*)a.out + (int64_t)b * a.out_bs + (int64_t)qi * a.out_rs + hoff;
@@ -222,7 +216,7 @@ __global__ __launch_bounds__(512) void attn_fwd_bf16(AttnArgs a) {
         const int d0 = db * 16 + (lane >> 4) * 4;
         if (d0 < a.hd) store4(orow + d0, o[db], inv);
       }
-      if ((lane >> 4) == 0) a.lse[((int64_t)b * a.H + h) * a.Nq + qi] = (mx + __log2f(l)) * kLn2;
+      if ((lane >> 4) == 0) a.lse[((int64_t)b * a.H + h) * a.Nq + qi] = (m + __log2f(l)) * kLn2;
     }
   }
 }
@@ -373,6 +367,188 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16(AttnArgs a) {
   }
 }
 
+// Backward split in two kernels so that each holds only two head images in LDS (two
+// workgroups per CU instead of one): dK/dV with Q, dO staged and the wave's own K/V rows
+// in registers; dQ with K, V staged and the wave's own Q/dO rows in registers.  Same
+// arithmetic as attn_bwd_bf16 phases A and B (which remains for reference shapes that
+// do not fit this split's launch checks).
+template <int HDP, int WPE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void attn_bwd_kv_bf16(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+  const int NQP = (a.Nq + 31) & ~31, NKP = (a.Nk + 31) & ~31;
+  constexpr int ST = HDP + 8;
+  constexpr int NCH = HDP / 8;
+  bf16* Qs = (bf16*)smem;
+  bf16* dOs = Qs + NQP * ST;
+  float* lse_s = (float*)(dOs + NQP * ST);
+  float* del_s = lse_s + NQP;
+  float* part = del_s + NQP;  // [NQP][NCH]
+  const int hoff = h * a.hd;
+  {
+    const StageSrc S[2] = {{Qs, (const bf16*)a.q + (int64_t)b * a.q_bs + hoff, a.q_rs, a.Nq, NQP},
+                           {dOs, (const bf16*)a.dout + (int64_t)b * a.do_bs + hoff, a.do_rs, a.Nq, NQP}};
+    stage_images<HDP, 2, 512>(S, a.hd);
+  }
+  for (int q = threadIdx.x; q < NQP; q += blockDim.x)
+    lse_s[q] = q < a.Nq ? a.lse_in[((int64_t)b * a.H + h) * a.Nq + q] * kLog2e : 0.f;  // log2 domain
+  for (int idx = threadIdx.x; idx < NQP * NCH; idx += blockDim.x) {
+    const int q = idx / NCH, c = idx % NCH;
+    float s = 0.f;
+    if (q < a.Nq && c * 8 < a.hd) {
+      const bf16x8 ov = ld8((const bf16*)a.o + (int64_t)b * a.o_bs + (int64_t)q * a.o_rs + hoff + c * 8);
+      const bf16x8 dv = *(const bf16x8*)(dOs + q * ST + c * 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += (float)ov[i] * (float)dv[i];
+    }
+    part[idx] = s;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < NQP; q += blockDim.x) {
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) s += part[q * NCH + c];
+    del_s[q] = s;
+  }
+  __syncthreads();
+  const float sl2 = a.scale * kLog2e;
+  const bf16* kbase = (const bf16*)a.k + (int64_t)b * a.k_bs + hoff;
+  const bf16* vbase = (const bf16*)a.v + (int64_t)b * a.v_bs + hoff;
+  for (int kb = wave; kb < NKP / 16; kb += nwaves) {
+    const int keyl = kb * 16 + (lane & 15);
+    bf16x8 kf[HDP / 32], vf[HDP / 32];
+#pragma unroll
+    for (int s = 0; s < HDP / 32; ++s) {
+      const int d = s * 32 + 8 * (lane >> 4);
+      const bool in = keyl < a.Nk && d < a.hd;
+      kf[s] = in ? ld8(kbase + (int64_t)keyl * a.k_rs + d) : zero8();
+      vf[s] = in ? ld8(vbase + (int64_t)keyl * a.v_rs + d) : zero8();
+    }
+    f32x4 dvt[HDP / 16], dkt[HDP / 16];
+#pragma unroll
+    for (int db = 0; db < HDP / 16; ++db) dvt[db] = dkt[db] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < NQP / 32; ++t) {
+      f32x4 p[2], ds[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int qa = t * 32 + c * 16 + (lane & 15);
+        f32x4 s_acc = {0.f, 0.f, 0.f, 0.f}, dp_acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < HDP / 32; ++s) {
+          const int d = s * 32 + 8 * (lane >> 4);
+          s_acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(Qs + qa * ST + d), kf[s], s_acc, 0, 0, 0);
+          dp_acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(dOs + qa * ST + d), vf[s], dp_acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = t * 32 + c * 16 + (lane >> 4) * 4 + r;
+          const bool ok = q < a.Nq && (full_kb(a, kb) || key_ok(a, b, keyl, q));
+          const float pv = ok ? exp2f(s_acc[r] * sl2 - lse_s[q]) : 0.f;
+          const float mk = a.drop.on() && q < a.Nq ? pdrop(a, b, h, q, keyl) : 1.f;
+          p[c][r] = pv * mk;
+          ds[c][r] = pv * (dp_acc[r] * mk - del_s[q]);
+        }
+      }
+      const bf16x8 pb = pack8(p[0], p[1]), dsb = pack8(ds[0], ds[1]);
+#pragma unroll
+      for (int db = 0; db < HDP / 16; ++db) {
+        dvt[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_read8(dOs, ST, t * 32, db * 16, lane), pb, dvt[db], 0, 0, 0);
+        dkt[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_read8(Qs, ST, t * 32, db * 16, lane), dsb, dkt[db], 0, 0, 0);
+      }
+    }
+    if (keyl < a.Nk) {
+      bf16* dkrow = (bf16*)a.dk + (int64_t)b * a.dk_bs + (int64_t)keyl * a.dk_rs + hoff;
+      bf16* dvrow = (bf16*)a.dv + (int64_t)b * a.dv_bs + (int64_t)keyl * a.dv_rs + hoff;
+#pragma unroll
+      for (int db = 0; db < HDP / 16; ++db) {
+        const int d0 = db * 16 + (lane >> 4) * 4;
+        if (d0 < a.hd) {
+          store4(dkrow + d0, dkt[db], a.scale);
+          store4(dvrow + d0, dvt[db], 1.f);
+        }
+      }
+    }
+  }
+}
+
+template <int HDP>
+__global__ __launch_bounds__(512) void attn_bwd_q_bf16(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+  const int NQP = (a.Nq + 31) & ~31, NKP = (a.Nk + 31) & ~31;
+  constexpr int ST = HDP + 8;
+  bf16* Ks = (bf16*)smem;
+  bf16* Vs = Ks + NKP * ST;
+  const int hoff = h * a.hd;
+  {
+    const StageSrc S[2] = {{Ks, (const bf16*)a.k + (int64_t)b * a.k_bs + hoff, a.k_rs, a.Nk, NKP},
+                           {Vs, (const bf16*)a.v + (int64_t)b * a.v_bs + hoff, a.v_rs, a.Nk, NKP}};
+    stage_images<HDP, 2, 512>(S, a.hd);
+  }
+  __syncthreads();
+  const float sl2 = a.scale * kLog2e;
+  const bf16* qbase = (const bf16*)a.q + (int64_t)b * a.q_bs + hoff;
+  const bf16* dobase = (const bf16*)a.dout + (int64_t)b * a.do_bs + hoff;
+  const bf16* obase = (const bf16*)a.o + (int64_t)b * a.o_bs + hoff;
+  for (int qb = wave; qb < NQP / 16; qb += nwaves) {
+    const int ql = qb * 16 + (lane & 15);
+    bf16x8 qf[HDP / 32], dof[HDP / 32];
+    float dd = 0.f;  // delta_q = sum_d dO * O, this lane's 8-dim chunks, then over the lane group
+#pragma unroll
+    for (int s = 0; s < HDP / 32; ++s) {
+      const int d = s * 32 + 8 * (lane >> 4);
+      const bool in = ql < a.Nq && d < a.hd;
+      qf[s] = in ? ld8(qbase + (int64_t)ql * a.q_rs + d) : zero8();
+      dof[s] = in ? ld8(dobase + (int64_t)ql * a.do_rs + d) : zero8();
+      const bf16x8 ov = in ? ld8(obase + (int64_t)ql * a.o_rs + d) : zero8();
+#pragma unroll
+      for (int i = 0; i < 8; ++i) dd += (float)ov[i] * (float)dof[s][i];
+    }
+    dd += __shfl_xor(dd, 16, 64);
+    dd += __shfl_xor(dd, 32, 64);
+    const float lq = ql < a.Nq ? a.lse_in[((int64_t)b * a.H + h) * a.Nq + ql] * kLog2e : 0.f;
+    f32x4 dqt[HDP / 16];
+#pragma unroll
+    for (int db = 0; db < HDP / 16; ++db) dqt[db] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < NKP / 32; ++t) {
+      f32x4 ds[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int ka = t * 32 + c * 16 + (lane & 15);
+        f32x4 s_acc = {0.f, 0.f, 0.f, 0.f}, dp_acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < HDP / 32; ++s) {
+          const int d = s * 32 + 8 * (lane >> 4);
+          s_acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(Ks + ka * ST + d), qf[s], s_acc, 0, 0, 0);
+          dp_acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(Vs + ka * ST + d), dof[s], dp_acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = t * 32 + c * 16 + (lane >> 4) * 4 + r;
+          const bool ok = ql < a.Nq && (full_kb(a, 2 * t + c) || key_ok(a, b, key, ql));
+          const float pv = ok ? exp2f(s_acc[r] * sl2 - lq) : 0.f;
+          const float mk = a.drop.on() && ok ? pdrop(a, b, h, ql, key) : 1.f;
+          ds[c][r] = pv * (dp_acc[r] * mk - dd);
+        }
+      }
+      const bf16x8 dsb = pack8(ds[0], ds[1]);
+#pragma unroll
+      for (int db = 0; db < HDP / 16; ++db)
+        dqt[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_read8(Ks, ST, t * 32, db * 16, lane), dsb, dqt[db], 0, 0, 0);
+    }
+    if (ql < a.Nq) {
+      bf16* dqrow = (bf16*)a.dq + (int64_t)b * a.dq_bs + (int64_t)ql * a.dq_rs + hoff;
+#pragma unroll
+      for (int db = 0; db < HDP / 16; ++db) {
+        const int d0 = db * 16 + (lane >> 4) * 4;
+        if (d0 < a.hd) store4(dqrow + d0, dqt[db], a.scale);
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------ f32 parity path
 template <int HD>
 __global__ __launch_bounds__(64) void attn_fwd_f32(AttnArgs a) {
@@ -488,6 +664,10 @@ __global__ __launch_bounds__(64) void attn_bwd_dkv_f32(AttnArgs a) {
 static size_t fwd_smem(int Nk, int hdp) {
   const int NKP = (Nk + 31) & ~31;
   return (size_t)2 * NKP * (hdp + 8) * 2;
+}
+static size_t bwd_kv_smem(int Nq, int hdp) {
+  const int NQP = (Nq + 31) & ~31;
+  return (size_t)2 * NQP * (hdp + 8) * 2 + (size_t)2 * NQP * 4 + (size_t)NQP * (hdp / 8) * 4;
 }
 static size_t bwd_smem(int Nq, int Nk, int hdp) {
   const int NQP = (Nq + 31) & ~31, NKP = (Nk + 31) & ~31;
@@ -739,9 +919,40 @@ extern "C" int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int h
                      dk_rs % 4 == 0 && dv_rs % 4 == 0,
                  "capk_attention_bwd(bf16): strides must allow vector access");
   const int hdp = hdp_of(hd);
+  const dim3 grid(B * H), block(512);
+  {
+    // split backward: dK/dV kernel, then dQ kernel (two head images in LDS each)
+    const size_t s1 = bwd_kv_smem(Nq, hdp), s2 = fwd_smem(Nk, hdp);
+    // (measured: ViT N=197 bwd 554 -> 460 us; for Nq <= 32 the second launch costs more than it saves)
+    if (Nq > 32 && s1 <= 80 * 1024 && s2 <= 80 * 1024) {
+      int rc2;
+      static const int wpe = [] { const char* e = getenv("CAPK_ATTN_WPE"); return e ? atoi(e) : 4; }();
+      if (wpe == 4) {  // <= 128 VGPRs: two workgroups per CU
+        switch (hdp) {
+          case 32: rc2 = launch_dyn(attn_bwd_kv_bf16<32, 4>, grid, block, s1, st, a, "attn_bwd_kv_bf16"); break;
+          case 64: rc2 = launch_dyn(attn_bwd_kv_bf16<64, 4>, grid, block, s1, st, a, "attn_bwd_kv_bf16"); break;
+          case 96: rc2 = launch_dyn(attn_bwd_kv_bf16<96, 4>, grid, block, s1, st, a, "attn_bwd_kv_bf16"); break;
+          default: rc2 = launch_dyn(attn_bwd_kv_bf16<128, 4>, grid, block, s1, st, a, "attn_bwd_kv_bf16"); break;
+        }
+      } else {
+        switch (hdp) {
+          case 32: rc2 = launch_dyn(attn_bwd_kv_bf16<32, 2>, grid, block, s1, st, a, "attn_bwd_kv_bf16"); break;
+          case 64: rc2 = launch_dyn(attn_bwd_kv_bf16<64, 2>, grid, block, s1, st, a, "attn_bwd_kv_bf16"); break;
+          case 96: rc2 = launch_dyn(attn_bwd_kv_bf16<96, 2>, grid, block, s1, st, a, "attn_bwd_kv_bf16"); break;
+          default: rc2 = launch_dyn(attn_bwd_kv_bf16<128, 2>, grid, block, s1, st, a, "attn_bwd_kv_bf16"); break;
+        }
+      }
+      if (rc2) return rc2;
+      switch (hdp) {
+        case 32: return launch_dyn(attn_bwd_q_bf16<32>, grid, block, s2, st, a, "attn_bwd_q_bf16");
+        case 64: return launch_dyn(attn_bwd_q_bf16<64>, grid, block, s2, st, a, "attn_bwd_q_bf16");
+        case 96: return launch_dyn(attn_bwd_q_bf16<96>, grid, block, s2, st, a, "attn_bwd_q_bf16");
+        default: return launch_dyn(attn_bwd_q_bf16<128>, grid, block, s2, st, a, "attn_bwd_q_bf16");
+      }
+    }
+  }
   const size_t shm = bwd_smem(Nq, Nk, hdp);
   CAPK_CHECK_ARG(shm <= 160 * 1024, "capk_attention_bwd: LDS %zu > 160 KiB", shm);
-  const dim3 grid(B * H), block(512);
   switch (hdp) {
     case 32: return launch_dyn(attn_bwd_bf16<32>, grid, block, shm, st, a, "attn_bwd_bf16");
     case 64: return launch_dyn(attn_bwd_bf16<64>, grid, block, shm, st, a, "attn_bwd_bf16");
