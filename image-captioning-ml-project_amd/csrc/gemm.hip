@@ -610,6 +610,13 @@ static int choose_splits(int cfg, int M, int N, int K) {
   return std::max(1, s);
 }
 
+// blaslt.cpp
+bool lt_enabled();
+bool lt_gemm(int out_f32, int M, int N, int K, const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ldb,
+             int b_kmajor, void* C, int64_t ldc, float alpha, float beta, const float* bias, const void* residual,
+             int64_t ldr, void* ws, size_t ws_bytes, hipStream_t st);
+size_t lt_workspace_bytes();
+
 }  // namespace capk
 
 using namespace capk;
@@ -620,7 +627,8 @@ extern "C" size_t capk_gemm_workspace(int in_dtype, int out_dtype, int M, int N,
   // upper bound over the configurations (the launch picks one of them)
   int s = 1;
   for (int c = 1; c <= 6; ++c) s = std::max(s, choose_splits(c, M, N, K));
-  return s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
+  const size_t slabs = s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
+  return lt_enabled() ? std::max(slabs, lt_workspace_bytes()) : slabs;
 }
 
 extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const void* A, int64_t lda,
@@ -656,6 +664,11 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
   CAPK_CHECK_ARG(((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % 8 == 0 && ldb % 8 == 0,
                  "capk_gemm(bf16): A/B must be 16-B aligned with lda, ldb %% 8 == 0");
   CAPK_CHECK_ARG(((uintptr_t)C % 16 == 0) && (ldc * esz) % 16 == 0, "capk_gemm(bf16): C alignment");
+  // plain products with a K-major A (forward Linear without activation, dX) -> hipBLASLt
+  if (lt_enabled() && act == 0 && !(drop_p > 0.f) && a_kmajor &&
+      lt_gemm(out_dtype == CAPK_F32, M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, alpha, beta, bias, residual,
+              ldr, ws, ws_bytes, st))
+    return CAPK_OK;
   const int cfg = choose_cfg(M, N, K, a_kmajor, b_kmajor, act);
   int splits = choose_splits(cfg, M, N, K);
   if (!ws || ws_bytes < (size_t)splits * M * N * sizeof(float)) splits = 1;
