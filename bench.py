@@ -190,7 +190,10 @@ def main():
             "config": {"workload": "config 3: ViT-B/16 + Transformer(6L,8H) + multi_head, CE train step",
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": 20, "image_tokens": 197,
                        "vocab": 50257, "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": "gemm_bf16_kernel (all bf16 GEMM launches in the timed steps)",
+            "roofline": {"bound": "mfma", "kernel": "bf16 GEMM family: every capk_gemm launch in the timed steps "
+                                                    "(hand-written gemm_bf16_kernel + hipBLASLt plain products)",
+                         "by_route": {k: {"launches": v["launches"], "ms": round(v["total_ms"], 2),
+                                          "tflops": round(v["tflops"], 1)} for k, v in gem["by_route"].items()},
                          "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
@@ -211,7 +214,7 @@ def main():
                             "ms_per_batch": round(bdt / args.beam_reps * 1e3, 3), "num_beams": 5, "max_length": 20,
                             "output_length": blen, "dtype": "bf16",
                             "workload": "ViT-B/16 encoder fwd + KV-cached Transformer beam-5 decode (HF semantics)",
-                            "roofline": {"bound": "mfma", "kernel": "gemm_bf16_kernel (all GEMM launches)",
+                            "roofline": {"bound": "mfma", "kernel": "bf16 GEMM family (all capk_gemm launches)",
                                          "achieved": round(bach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                                          "frac": round(bach / PEAK_BF16_TFLOPS, 4),
                                          "gemm_share": round(bgem["total_ms"] / (bdt * 1e3), 3)},

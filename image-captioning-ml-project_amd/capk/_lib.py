@@ -32,6 +32,7 @@ SIGNATURES = {
     "capk_version": (_i, []),
     "capk_device_arch": (_i, [ctypes.c_char_p, _i]),
     "capk_gemm_workspace": (_sz, [_i, _i, _i, _i, _i]),
+    "capk_gemm_last_route": (_i, []),
     "capk_gemm": (_i, [_i, _i, _i, _i, _i, _c_p, _i64, _i, _c_p, _i64, _i, _c_p, _i64, _f, _f,
                        _c_p, _c_p, _i64, _i, _c_p, _c_p, _i64, _f, _u32, _c_p, _sz, _c_p]),
     "capk_dropout_mask": (_i, [_i64, _u64, _f, _u32, _c_p, _c_p]),

@@ -11,7 +11,7 @@
 // column n) is the BIAS epilogue over D's rows; a residual is passed as C with beta = 1.
 // One plan (descriptors + heuristic algorithm) per shape/stride/type key, built once.
 // The workspace is the caller's (capk_gemm_workspace covers it); the library allocates
-// nothing and the algorithm choice is fixed per shape.  Opt-in: CAPK_GEMM_BLASLT=1.
+// nothing and the algorithm choice is fixed per shape.  CAPK_GEMM_BLASLT=0 turns the route off.
 #include <hipblaslt/hipblaslt.h>
 #include <stdlib.h>
 
@@ -103,7 +103,7 @@ bool build_plan(hipblasLtHandle_t h, const LtKey& k, LtPlan& p) {
 bool lt_enabled() {
   static const bool on = [] {
     const char* e = getenv("CAPK_GEMM_BLASLT");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return on;
 }

@@ -621,6 +621,9 @@ size_t lt_workspace_bytes();
 
 using namespace capk;
 
+static thread_local int g_last_route = 0;
+extern "C" int capk_gemm_last_route(void) { return g_last_route; }
+
 extern "C" size_t capk_gemm_workspace(int in_dtype, int out_dtype, int M, int N, int K) {
   (void)out_dtype;
   if (in_dtype != CAPK_BF16) return 0;
@@ -665,10 +668,14 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
                  "capk_gemm(bf16): A/B must be 16-B aligned with lda, ldb %% 8 == 0");
   CAPK_CHECK_ARG(((uintptr_t)C % 16 == 0) && (ldc * esz) % 16 == 0, "capk_gemm(bf16): C alignment");
   // plain products with a K-major A (forward Linear without activation, dX) -> hipBLASLt
-  if (lt_enabled() && act == 0 && !(drop_p > 0.f) && a_kmajor &&
+  // (K >= 32768, the LM-head dX, measured no faster there)
+  if (lt_enabled() && act == 0 && !(drop_p > 0.f) && a_kmajor && K < 32768 &&
       lt_gemm(out_dtype == CAPK_F32, M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, alpha, beta, bias, residual,
-              ldr, ws, ws_bytes, st))
+              ldr, ws, ws_bytes, st)) {
+    g_last_route = 1;
     return CAPK_OK;
+  }
+  g_last_route = 0;
   const int cfg = choose_cfg(M, N, K, a_kmajor, b_kmajor, act);
   int splits = choose_splits(cfg, M, N, K);
   if (!ws || ws_bytes < (size_t)splits * M * N * sizeof(float)) splits = 1;

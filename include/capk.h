@@ -72,6 +72,10 @@ int capk_dropout_mask(int64_t n, uint64_t offset, float p, uint32_t seed, uint8_
  * Workspace (split-K partial slabs, fp32) — query with capk_gemm_workspace();
  * pass ws=NULL/ws_bytes=0 to disable split-K. */
 size_t capk_gemm_workspace(int in_dtype, int out_dtype, int M, int N, int K);
+/* Which path ran the calling thread's last capk_gemm: 0 = hand-written kernels (gemm.hip),
+ * 1 = hipBLASLt (plain bf16 products with a K-major A; CAPK_GEMM_BLASLT=0 disables).  For
+ * per-path timing in bench.py. */
+int capk_gemm_last_route(void);
 int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K,
               const void* A, int64_t lda, int a_kmajor,
               const void* B, int64_t ldb, int b_kmajor,

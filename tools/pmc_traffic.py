@@ -8,7 +8,8 @@ global_load_lds / buffer_load ... lds alike -- how every GEMM operand tile is st
 so it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores (the GEMM epilogue).
 Infinity-Cache hits are counted, so tile re-reads absorbed on-die still show up here.
 
-usage: pmc_traffic.py FETCH_DIR WRITE_DIR [--match gemm_bf16_kernel,gemm256_kernel] [--out FILE] [--cmd TEXT]
+usage: pmc_traffic.py FETCH_DIR WRITE_DIR [--match gemm_bf16_kernel,gemm256_kernel,Cijk_] [--out FILE] [--cmd TEXT]
+(Cijk_* = hipBLASLt's GEMM kernels, the library route of capk_gemm)
 """
 import argparse
 import csv
@@ -38,7 +39,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
-    ap.add_argument("--match", default="gemm_bf16_kernel,gemm256_kernel")
+    ap.add_argument("--match", default="gemm_bf16_kernel,gemm256_kernel,Cijk_")
     ap.add_argument("--out")
     ap.add_argument("--cmd", default="")
     a = ap.parse_args()
