@@ -629,7 +629,7 @@ static int choose_cfg(int M, int N, int K, int a_kmajor, int b_kmajor, int act) 
   if ((o == 3 || o == 4 || o == 6) && (a_kmajor || b_kmajor) && K % 32) o = 1;
   if (o >= 1 && o <= 6) return o;
   if (act && (a_kmajor || b_kmajor) && K % 32 == 0) return 4;
-  if (!a_kmajor && !b_kmajor && tiles_of(4, M, N) < slots_of(4)) return 4;
+  if (!a_kmajor && !b_kmajor && tiles_of(4, M, N) < slots_of(4)) return 1;  // split-K dW (cfg 4 measured slower)
   return 1;
 }
 // Split-K factor: fill one round of resident workgroups when the tile grid alone cannot
