@@ -496,16 +496,25 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
 // forward: C holds pre = acc + bias; writes act(pre) to C and pre or act'(pre)
 // (CAPK_ACT_DERIV) to `pre`.  Backward: C holds dY.W; multiplies by act'(aux) or by aux
 // itself (CAPK_ACT_DERIV).  One HBM pass, 8-wide segments, grid-stride.
+// from_pre: the library wrote pre = acc + bias straight into `pre` (plain forward act with a
+// kept pre-activation): read it there and write only act(pre) to C.
 template <typename OutT>
 __global__ __launch_bounds__(256) void act_pass_kernel(int M, int N, OutT* __restrict__ C, int64_t ldc,
                                                        OutT* __restrict__ pre, const OutT* __restrict__ aux,
-                                                       int64_t ldx, int act) {
+                                                       int64_t ldx, int act, int from_pre) {
   const int nseg = N / 8;
   const int64_t total = (int64_t)M * nseg;
   const int a = act & 15;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int m = (int)(i / nseg), n = (int)(i % nseg) * 8;
     float v[8];
+    if (from_pre) {
+      Vec8<OutT>::load(pre + (int64_t)m * ldx + n, v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = act_fwd_fast(a, v[k]);
+      Vec8<OutT>::store(C + (int64_t)m * ldc + n, v);
+      continue;
+    }
     Vec8<OutT>::load(C + (int64_t)m * ldc + n, v);
     if (act & CAPK_ACT_BWD) {
       float g[8];
@@ -712,14 +721,16 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
   // activation products (bias + act with its side output, or x act'): library GEMM for the
   // product, then one elementwise pass -- measured faster than the fused epilogue on the
   // FFN shapes because the library main loop is faster than gemm_bf16_kernel's
+  // (a plain forward act that keeps pre writes the product straight into preact: one stream less)
+  const int from_pre = !(act & CAPK_ACT_BWD) && !(act & CAPK_ACT_DERIV) && preact != nullptr;
   if (lt_enabled() && (act & 15) && !(drop_p > 0.f) && a_kmajor && K < 32768 && !residual && beta == 0.f &&
       out_dtype == CAPK_BF16 &&
-      lt_gemm(0, M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, alpha, 0.f,
+      lt_gemm(0, M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, from_pre ? preact : C, from_pre ? ldx : ldc, alpha, 0.f,
               (act & CAPK_ACT_BWD) ? nullptr : bias, nullptr, 0, ws, ws_bytes, st)) {
     const int64_t segs = (int64_t)M * (N / 8);
     const int grid_a = (int)std::min<int64_t>(cdiv(segs, 256), 8192);
     hipLaunchKernelGGL(act_pass_kernel<bf16>, dim3(grid_a), dim3(256), 0, st, M, N, (bf16*)C, ldc, (bf16*)preact,
-                       (const bf16*)aux, ldx, act);
+                       (const bf16*)aux, ldx, act, from_pre);
     CAPK_LAUNCH_CHECK("act_pass_kernel");
     g_last_route = 1;
     return CAPK_OK;

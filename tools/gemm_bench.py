@@ -7,7 +7,7 @@ sys.path.insert(0, os.path.join(ROOT, "image-captioning-ml-project_amd"))
 import torch  # noqa: E402
 
 from capk import ops  # noqa: E402
-from capk._lib import ACT_DERIV, ACT_GELU_ERF  # noqa: E402
+from capk._lib import ACT_GELU_ERF  # noqa: E402
 
 T = 256 * 197
 SHAPES = [  # name, M, N, K, kind
@@ -29,12 +29,12 @@ def run(name, M, N, K, kind, iters=20):
         w = (torch.randn(N, K, device=dev, generator=g) * 0.02).bfloat16()
         b = torch.zeros(N, device=dev)
         pre = torch.empty(M, N, device=dev, dtype=torch.bfloat16) if "gelu" in kind else None
-        fn = lambda: ops.linear(x, w, b, act=(ACT_GELU_ERF | ACT_DERIV) if pre is not None else 0, preact=pre)
+        fn = lambda: ops.linear(x, w, b, act=ACT_GELU_ERF if pre is not None else 0, preact=pre)
     elif kind.startswith("dx"):  # dX[M,K'] = dY[M,N'] W[N',K'] with K'=N, N'=K of the table entry
         dy = torch.randn(M, K, device=dev, generator=g).bfloat16()
         w = (torch.randn(K, N, device=dev, generator=g) * 0.02).bfloat16()
         aux = torch.randn(M, N, device=dev, generator=g).bfloat16() if "gelu" in kind else None
-        fn = lambda: ops.linear_dx(dy, w, act_bwd=(ACT_GELU_ERF | ACT_DERIV) if aux is not None else 0, aux=aux)
+        fn = lambda: ops.linear_dx(dy, w, act_bwd=ACT_GELU_ERF if aux is not None else 0, aux=aux)
     else:  # dW[N,K] = dY[M,N]^T X[M,K]
         dy = torch.randn(M, N, device=dev, generator=g).bfloat16()
         x = torch.randn(M, K, device=dev, generator=g).bfloat16()
