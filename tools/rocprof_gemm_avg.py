@@ -12,7 +12,7 @@ import json
 import sys
 
 MAIN = ("gemm_bf16_kernel", "gemm256_kernel", "Cijk_")
-AUX = ("splitk_reduce_kernel",)
+AUX = ("splitk_reduce_kernel", "act_pass_kernel")  # both launched inside capk_gemm (gemm.hip)
 
 
 def main():
@@ -26,7 +26,8 @@ def main():
             name = r["Name"]
             if any(m in name for m in MAIN + AUX):
                 tot_ns += float(r["TotalDurationNs"])
-                key = "hipblaslt" if "Cijk_" in name else ("splitk_reduce" if "splitk" in name else "gemm_bf16_kernel")
+                key = ("hipblaslt" if "Cijk_" in name else "splitk_reduce" if "splitk" in name
+                       else "act_pass" if "act_pass" in name else "gemm_bf16_kernel")
                 e = by.setdefault(key, [0, 0.0])
                 e[0] += int(r["Calls"])
                 e[1] += float(r["TotalDurationNs"])
