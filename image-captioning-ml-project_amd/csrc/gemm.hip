@@ -505,7 +505,54 @@ __global__ __launch_bounds__(256) void act_pass_kernel(int M, int N, OutT* __res
   const int nseg = N / 8;
   const int64_t total = (int64_t)M * nseg;
   const int a = act & 15;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  if (from_pre && ldc == N && ldx == N) {
+    // dense rows (the FFN activations): flat index, two 16-B segments in flight per lane
+    int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    for (; i + stride < total; i += 2 * stride) {
+      float v[8], w[8];
+      Vec8<OutT>::load(pre + i * 8, v);
+      Vec8<OutT>::load(pre + (i + stride) * 8, w);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        v[k] = act_fwd_fast(a, v[k]);
+        w[k] = act_fwd_fast(a, w[k]);
+      }
+      Vec8<OutT>::store(C + i * 8, v);
+      Vec8<OutT>::store(C + (i + stride) * 8, w);
+    }
+    if (i < total) {
+      float v[8];
+      Vec8<OutT>::load(pre + i * 8, v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = act_fwd_fast(a, v[k]);
+      Vec8<OutT>::store(C + i * 8, v);
+    }
+    return;
+  }
+  if ((act & CAPK_ACT_BWD) && ldc == N && ldx == N) {
+    // dense rows (FC2 dX x act'): flat index, two segments in flight per lane
+    int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    for (; i < total; i += 2 * stride) {
+      const bool two = i + stride < total;
+      float v[8], g[8], w[8], h[8];
+      Vec8<OutT>::load(C + i * 8, v);
+      Vec8<OutT>::load(aux + i * 8, g);
+      if (two) {
+        Vec8<OutT>::load(C + (i + stride) * 8, w);
+        Vec8<OutT>::load(aux + (i + stride) * 8, h);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        v[k] *= (act & CAPK_ACT_DERIV) ? g[k] : act_grad_fast(a, g[k]);
+        if (two) w[k] *= (act & CAPK_ACT_DERIV) ? h[k] : act_grad_fast(a, h[k]);
+      }
+      Vec8<OutT>::store(C + i * 8, v);
+      if (two) Vec8<OutT>::store(C + (i + stride) * 8, w);
+    }
+    return;
+  }
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += stride) {
     const int m = (int)(i / nseg), n = (int)(i % nseg) * 8;
     float v[8];
     if (from_pre) {
