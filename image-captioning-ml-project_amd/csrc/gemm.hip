@@ -775,7 +775,9 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
       lt_gemm(0, M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, from_pre ? preact : C, from_pre ? ldx : ldc, alpha, 0.f,
               (act & CAPK_ACT_BWD) ? nullptr : bias, nullptr, 0, ws, ws_bytes, st)) {
     const int64_t segs = (int64_t)M * (N / 8);
-    const int grid_a = (int)std::min<int64_t>(cdiv(segs, 256), 8192);
+    // dense rows: one launch-wide pass, each lane a pair of segments (flat paths in act_pass_kernel)
+    const bool dense = ldc == N && ldx == N && (from_pre || (act & CAPK_ACT_BWD));
+    const int grid_a = (int)std::min<int64_t>(dense ? cdiv(segs, 512) : cdiv(segs, 256), dense ? (1 << 20) : 8192);
     hipLaunchKernelGGL(act_pass_kernel<bf16>, dim3(grid_a), dim3(256), 0, st, M, N, (bf16*)C, ldc, (bf16*)preact,
                        (const bf16*)aux, ldx, act, from_pre);
     CAPK_LAUNCH_CHECK("act_pass_kernel");
