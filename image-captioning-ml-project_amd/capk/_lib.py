@@ -108,6 +108,7 @@ SIGNATURES = {
     "capk_attn_coverage_reg": (_i, [_i, _i, _i, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "capk_clamp": (_i, [_i64, _c_p, _f, _f, _c_p]),
     "capk_mask_rows_by_length": (_i, [_i, _i, _i, _i, _c_p, _i64, _i64, _c_p, _c_p]),
+    "capk_cider_d": (_i, [_i, _c_p, _c_p, _c_p, _c_p, _c_p, _i, ctypes.c_double, _i, _c_p]),
 }
 
 _lib = None

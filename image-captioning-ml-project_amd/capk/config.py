@@ -1,9 +1,11 @@
 """Configuration surface — mirrors src/config.py of the reference (same dataclasses,
 field names, defaults and Enums) with the documented fixes of SURVEY §0.1:
 
-* D2: string values coming from the CLI are coerced to the Enum members
-  (``EncoderConfig(encoder_type="vit")`` works; the reference compared 'vit'
-  against EncoderType.VIT and raised ValueError in the factories).
+* D2: string values coming from the CLI are coerced to the Enum members, both at
+  construction (``EncoderConfig(encoder_type="vit")``) and on later assignment
+  (``cfg.model.encoder.encoder_type = "vit"``, what src/main.py:119-124
+  ``_update_config_from_args`` does); the reference stored the string and its
+  factories, comparing 'vit' against EncoderType.VIT, raised ValueError.
 * D13: ``save_config`` serialises nested Enums; ``load_config`` rebuilds the
   nested dataclasses and Enums (the reference left them as dicts).
 * Mutable dataclass defaults use ``default_factory`` (the reference's
@@ -44,20 +46,31 @@ def _coerce(enum_cls, v):
     return v if isinstance(v, enum_cls) else enum_cls(v)
 
 
+class _EnumFields:
+    """Coerce the Enum-typed field on every assignment (D2), not only in __init__."""
+    _ENUM_FIELDS = {}
+
+    def __setattr__(self, name, value):
+        cls = self._ENUM_FIELDS.get(name)
+        super().__setattr__(name, _coerce(cls, value) if cls is not None else value)
+
+
 @dataclass
-class EncoderConfig:
+class EncoderConfig(_EnumFields):
+    _ENUM_FIELDS = {"encoder_type": EncoderType}
+
     encoder_type: EncoderType = EncoderType.VIT
     pretrained_model_name: str = "google/vit-base-patch16-224"
     freeze: bool = False
     feature_dim: int = 768
     use_object_features: bool = False
 
-    def __post_init__(self):
-        self.encoder_type = _coerce(EncoderType, self.encoder_type)
 
 
 @dataclass
-class DecoderConfig:
+class DecoderConfig(_EnumFields):
+    _ENUM_FIELDS = {"decoder_type": DecoderType}
+
     decoder_type: DecoderType = DecoderType.GPT2
     pretrained_model_name: str = "gpt2"
     hidden_dim: int = 768
@@ -66,12 +79,12 @@ class DecoderConfig:
     dropout: float = 0.1
     max_length: int = 50
 
-    def __post_init__(self):
-        self.decoder_type = _coerce(DecoderType, self.decoder_type)
 
 
 @dataclass
-class AttentionConfig:
+class AttentionConfig(_EnumFields):
+    _ENUM_FIELDS = {"attention_type": AttentionType}
+
     attention_type: AttentionType = AttentionType.MULTI_HEAD
     num_heads: int = 8
     temperature: float = 1.0
@@ -80,8 +93,6 @@ class AttentionConfig:
     # AttentionConfig lacks; build_decoder fills it from DecoderConfig.hidden_dim.
     hidden_dim: int = 768
 
-    def __post_init__(self):
-        self.attention_type = _coerce(AttentionType, self.attention_type)
 
 
 @dataclass

@@ -18,6 +18,9 @@ Parameters that the reference leaves without a gradient in some
 configurations (the ViT pooler when the decoder ignores ``pooled_features``:
 torch AdamW then skips them) are placed at the tail of their buffer and marked
 optional; the optimizer only updates them in steps where a backward wrote them.
+Frozen parameters (``requires_grad=False``, e.g. ``EncoderConfig.freeze``) sit
+behind those and are never handed to the optimizer: the reference builds its
+AdamW groups from ``p.requires_grad`` parameters only (trainer.py:117-126).
 """
 import torch
 
@@ -62,6 +65,7 @@ class ParamStore:
     def __init__(self, model, device, bf16_shadow=True):
         self.device = torch.device(device)
         named = list(model.named_parameters())
+        self.named = named  # reference order (torch optimizer state-dict numbering)
         names = {id(p): n for n, p in named}
         fused = []
         for m in model.modules():
@@ -77,6 +81,7 @@ class ParamStore:
         for m in model.modules():
             for p in getattr(m, "_capk_optional_params", lambda: [])():
                 self.optional.add(id(p))
+        self.frozen = {id(p) for _, p in named if not p.requires_grad}
         # order: registration order, a fused group placed (adjacent) at its first member;
         # optional-grad parameters last within each buffer.  The backward finishes the
         # modules in reverse registration order, so the final gradients of each buffer
@@ -91,8 +96,11 @@ class ParamStore:
         for p in order:
             g = "no_decay" if no_decay(names[id(p)]) else "decay"
             self.groups[g].append(p)
+        def tail_rank(p):  # stable sort: required, then optional, then frozen
+            return 2 if id(p) in self.frozen else int(id(p) in self.optional)
+
         for g in self.groups:
-            self.groups[g].sort(key=lambda p: id(p) in self.optional)  # stable: optional to the tail
+            self.groups[g].sort(key=tail_rank)
         self.master, self.grad, self.bf16, self.offsets = {}, {}, {}, {}
         self.required_numel = {}
         self.params = []
@@ -145,7 +153,7 @@ class ParamStore:
                 self.offsets[id(p)] = (g, off)
                 self.names[id(p)] = names[id(p)]
                 off += _round(_alloc_numel(p))
-                if id(p) not in self.optional:
+                if id(p) not in self.optional and id(p) not in self.frozen:
                     req = off
                 self.params.append(p)
             self.master[g], self.grad[g], self.bf16[g] = master, grad, shadow
@@ -178,8 +186,18 @@ class ParamStore:
             elif self.bf16[g] is not None:
                 self.bf16[g].copy_(self.master[g])
 
+    def param_view(self, p, bufs):
+        """`p`-shaped view into a flat buffer dict laid out like the master buffers
+        (e.g. the optimizer's moments)."""
+        g, off = self.offsets[id(p)]
+        lay = getattr(p, "_capk_layout", None)
+        if lay is not None:
+            sshape, view = lay
+            return view(bufs[g][off:off + _alloc_numel(p)].view(sshape))
+        return bufs[g][off:off + p.numel()].view(p.shape)
+
     def mark_written(self, p):
-        if id(p) in self.optional:
+        if id(p) in self.optional and id(p) not in self.frozen:
             self.written_optional.add(id(p))
 
     def relink_grads(self):
@@ -193,7 +211,7 @@ class ParamStore:
         parameter; optional parameters advance only in steps that produced a gradient)."""
         segs = [((group, "required"), 0, self.required_numel[group])] if self.required_numel[group] else []
         for p in self.groups[group]:
-            if id(p) in self.optional and id(p) in self.written_optional:
+            if id(p) in self.optional and id(p) in self.written_optional and id(p) not in self.frozen:
                 off = p._capk_offset
                 segs.append(((group, off), off, off + _round(_alloc_numel(p))))
         return segs

@@ -74,7 +74,7 @@ class GradBucketer:
         self.reset()
 
     def reset(self):
-        self.final = set()
+        self.final = set(self.store.frozen)  # frozen parameters never receive a gradient
         self.works = []
         self.k = {g: 0 for g in self.spans}                       # spans known final, counted from the end
         self.lo = {g: self.store.grad[g].numel() for g in self.spans}  # start of the final suffix

@@ -5,8 +5,9 @@ _calculate_rewards (src/train/trainer.py:319-484) with the SURVEY fixes:
 
 * D8  — the advantage is per sample (r_sample - r_baseline) and the loss is the mean of
         -logp * advantage over the sampled tokens up to and including the first EOS;
-* D9  — the reward is a per-sample CIDEr-D computed here on token ids (pycocoevalcap is
-        absent: parity unpinned, restated from the published metric);
+* D9  — the reward is a per-sample CIDEr-D on token ids, scored by the host C++ scorer
+        (capk.cider -> csrc/cider.cpp; pycocoevalcap is absent: parity unpinned vs it,
+        pinned by known answers and the oracle/cider.py restatement);
 * sampling — the reference re-runs the full decoder on the prefix every step and keeps the
         log-prob graph; here the sampler runs the KV-cached decode step without a graph
         (softmax + inverse-CDF kernel, counter-based uniforms) and ONE teacher-forced
@@ -16,76 +17,16 @@ _calculate_rewards (src/train/trainer.py:319-484) with the SURVEY fixes:
 * baseline — model.generate (greedy for the Transformer decoder, beam-4 for GPT-2), reusing
         the encoder features of the step instead of re-encoding the images.
 """
-import math
-from collections import Counter, defaultdict
-
 import numpy as np
 import torch
 
 from .. import ops
+from ..cider import cider_d
 from .losses import _padded_base
 
+EOS_CHECK_EVERY = 4  # sampled steps between host checks of the all-EOS stop rule
+
 PG_IGNORE = -100
-
-
-# --------------------------------------------------------------- CIDEr-D -----
-def _ngrams(tokens, n):
-    return Counter(tuple(tokens[i:i + n]) for i in range(len(tokens) - n + 1))
-
-
-def _cook(tokens, nmax=4):
-    c = Counter()
-    for n in range(1, nmax + 1):
-        c.update(_ngrams(tokens, n))
-    return c
-
-
-def cider_d(candidates, references, n=4, sigma=6.0):
-    """Per-sample CIDEr-D (Vedantam et al. 2015; the pycocoevalcap CiderD scorer):
-    tf-idf n-gram vectors (n = 1..4) with document frequencies over this corpus of
-    references, clipped cosine similarity, Gaussian length penalty (sigma 6), averaged
-    over n and references, x10.  candidates: list of token lists; references: list (per
-    candidate) of lists of token lists."""
-    crefs = [[_cook(r, n) for r in refs] for refs in references]
-    df = defaultdict(float)
-    for refs in crefs:
-        for ng in set(ng for r in refs for ng in r):
-            df[ng] += 1.0
-    ref_len = math.log(float(len(crefs)))
-
-    def vec(cnts):
-        v = [defaultdict(float) for _ in range(n)]
-        norm = [0.0] * n
-        length = 0
-        for ng, tf in cnts.items():
-            k = len(ng) - 1
-            d = math.log(max(1.0, df[ng]))
-            v[k][ng] = float(tf) * (ref_len - d)
-            norm[k] += v[k][ng] ** 2
-            if k == 1:
-                length += tf
-        return v, [math.sqrt(x) for x in norm], length
-
-    def sim(vh, vr, nh, nr, lh, lr):
-        delta = float(lh - lr)
-        val = np.zeros(n)
-        for k in range(n):
-            for ng, c in vh[k].items():
-                val[k] += min(vh[k][ng], vr[k][ng]) * vr[k][ng]
-            if nh[k] != 0 and nr[k] != 0:
-                val[k] /= nh[k] * nr[k]
-            val[k] *= math.e ** (-(delta ** 2) / (2 * sigma ** 2))
-        return val
-
-    scores = np.zeros(len(candidates))
-    for i, (cand, refs) in enumerate(zip(candidates, crefs)):
-        vh, nh, lh = vec(_cook(cand, n))
-        acc = np.zeros(n)
-        for r in refs:
-            vr, nr, lr = vec(r)
-            acc += sim(vh, vr, nh, nr, lh, lr)
-        scores[i] = float(np.mean(acc)) / max(len(refs), 1) * 10.0
-    return scores
 
 
 def strip_special(ids, eos, pad, bos=None):
@@ -147,10 +88,16 @@ def policy_gradient_loss(logits, sample_ids, advantages, eos):
 
 # ------------------------------------------------------------- sampling ------
 @torch.no_grad()
-def sample_captions(decoder, encoder_features, max_length, seed):
+def sample_captions(decoder, encoder_features, max_length, seed, check_every=EOS_CHECK_EVERY):
     """_sample_captions (trainer.py:383-438): start from bos, sample from
-    softmax(last logits), stop when every sampled token of a step is EOS.  Returns
-    sampled ids [B, T'+1] (bos first) and the log-probs of the sampled tokens [B, T']."""
+    softmax(last logits), stop after the first step whose sampled tokens are ALL EOS
+    (trainer.py:435-436).  Returns sampled ids [B, T'+1] (bos first) and the log-probs of
+    the sampled tokens [B, T'].
+
+    The stop rule is evaluated on the device every step (one flag per step) and read by
+    the host only every `check_every` steps: the uniforms are counter-based per
+    (seed, step, row), so steps sampled past the stop are simply cut off and the result
+    equals a per-step check, without a host sync per token."""
     from ..models.decoders import GPT2Decoder, TransformerDecoder
     if isinstance(decoder, TransformerDecoder):
         from ..models.transformer import KVDecodeRunner
@@ -167,25 +114,33 @@ def sample_captions(decoder, encoder_features, max_length, seed):
     ids = torch.empty(B, max_length, dtype=torch.long, device=dev)
     ids[:, 0] = decoder.bos_token_id
     logp = torch.empty(max_length - 1, B, dtype=torch.float32, device=dev)
+    alleos = torch.zeros(max_length - 1, dtype=torch.bool, device=dev)
     cur = ids[:, 0].contiguous()
-    T = 1
+    steps = max_length - 1
     for t in range(max_length - 1):
         logits = runner.step(t + 1, cur, None)
         nxt = torch.empty(B, dtype=torch.long, device=dev)
         ops.sample_rows(logits, decoder.vocab_size, seed, t, nxt, logp[t])
         ids[:, t + 1] = nxt
         cur = nxt
-        T = t + 2
-        if bool((nxt == decoder.eos_token_id).all()):
-            break
-    return ids[:, :T], logp[:T - 1].t()
+        alleos[t] = (nxt == decoder.eos_token_id).all()
+        if (t + 1) % check_every == 0 or t == max_length - 2:
+            hit = torch.nonzero(alleos[:t + 1])
+            if hit.numel():
+                steps = int(hit[0, 0]) + 1
+                break
+    T = steps + 1
+    return ids[:, :T], logp[:steps].t()
 
 
-def scst_step(model, images, references, optimizer, lr, max_length=20, seed=0, baseline_kwargs=None):
+def scst_step(model, images, references, optimizer, lr, seed, max_length=20, baseline_kwargs=None, bucketer=None):
     """One SCST update (trainer.py:338-381): encoder forward, sampled captions, baseline
     captions (model.generate), per-sample CIDEr-D rewards, loss = masked mean of
     -logp * (r_sample - r_baseline), backward, AdamW step.  references: per image a list
-    of token-id lists.  Returns (loss, mean sample reward, mean baseline reward)."""
+    of token-id lists.  `seed` keys the sampler's uniforms: pass a fresh value per update
+    (the trainer derives it from its step counter) or every update reuses the same draws.
+    `lr` = None uses the optimizer's scheduled rate.  Returns (loss, mean sample reward,
+    mean baseline reward)."""
     dec = model.decoder
     enc = model.encoder(images)
     enc_nograd = {k: (v.detach() if torch.is_tensor(v) else v) for k, v in enc.items()}
@@ -206,5 +161,7 @@ def scst_step(model, images, references, optimizer, lr, max_length=20, seed=0, b
             logits, _ = dec.forward_logits(enc["features"], ids, use_pad_mask=False)
     loss = policy_gradient_loss(logits, ids, adv, eos)
     loss.backward()
+    if bucketer is not None:  # DP: rewards are rank-local, gradients are averaged
+        bucketer.finish()
     optimizer.step(lr=lr)
     return loss.detach(), float(np.mean(r_s)), float(np.mean(r_b))

@@ -390,6 +390,19 @@ int capk_clamp(int64_t n, float* x, float lo, float hi, void* stream);
 int capk_mask_rows_by_length(int dtype, int B, int T, int cols, void* x, int64_t ld, int64_t bs, const int32_t* len,
                              void* stream);
 
+/* ------------------------------------------------------ CIDEr-D (host) ----
+ * SCST reward: replaces src/evaluate/metrics.py:46-110 (pycocoevalcap
+ * CiderD, via CaptioningTrainer._calculate_rewards, src/train/trainer.py:440-484) with a
+ * per-sample score.  HOST code (no device memory, no stream): token-id sentences as
+ * CSR arrays — candidate i = cand_tok[cand_off[i] .. cand_off[i+1]); reference r =
+ * ref_tok[ref_off[r] .. ref_off[r+1]); the references of candidate i are r in
+ * [ref_img[i], ref_img[i+1]).  Document frequencies are taken over this corpus (one
+ * entry per candidate).  n_max = 4, sigma = 6 for CIDEr-D; scores[i] in the
+ * scorer's x10 scale.  threads <= 0: all hardware threads. */
+int capk_cider_d(int n_cand, const int32_t* cand_tok, const int64_t* cand_off, const int32_t* ref_tok,
+                 const int64_t* ref_off, const int64_t* ref_img, int n_max, double sigma, int threads,
+                 double* scores);
+
 #ifdef __cplusplus
 }
 #endif

@@ -146,3 +146,44 @@ def test_param_store_layout_cpu():
     assert pool.weight._capk_group == "decay" and pool.bias._capk_group == "no_decay"
     assert pool.weight._capk_offset >= st.required_numel["decay"]
     assert m.encoder.model.layers[0].layernorm_before.weight._capk_group == "decay"  # name rule (D-note)
+
+
+def test_param_store_frozen_encoder_outside_optimizer_cpu():
+    """EncoderConfig.freeze: the reference's AdamW groups hold only requires_grad
+    parameters (trainer.py:117-126), so frozen encoder weights must lie outside every
+    range the optimizer updates (and be pre-final for the DP bucketer)."""
+    from capk import config as C
+    from capk.models import captioning_model as cm
+    from capk.models import encoders as E
+    from capk.params import attach
+    from capk.train.dp import GradBucketer
+    cfg = C.Config()
+    cfg.model.encoder = C.EncoderConfig(encoder_type="vit", feature_dim=64, freeze=True)
+    cfg.model.decoder = C.DecoderConfig(decoder_type="transformer", hidden_dim=64, num_layers=1, num_heads=2)
+    cfg.model.vocab_size, cfg.model.pad_token_id = 70, 69
+    arch = dict(hidden_size=64, num_hidden_layers=1, num_attention_heads=2, intermediate_size=128, image_size=32,
+                patch_size=16, num_channels=3, layer_norm_eps=1e-12)
+    orig = E.VIT_ARCHS["google/vit-base-patch16-224"]
+    E.VIT_ARCHS["google/vit-base-patch16-224"] = arch
+    try:
+        m = cm.ImageCaptioningModel(cfg)
+    finally:
+        E.VIT_ARCHS["google/vit-base-patch16-224"] = orig
+    st = attach(m, "cpu")
+    frozen = [p for p in m.encoder.parameters()]
+    assert frozen and all(not p.requires_grad for p in frozen)
+    for g in st.groups:
+        ranges = st.segments(g)
+        for p in frozen:
+            st.mark_written(p)  # even a stray notification must not enrol a frozen parameter
+        ranges = st.segments(g)
+        for p in frozen:
+            if p._capk_group != g:
+                continue
+            assert all(not (s <= p._capk_offset < e) for _, s, e in ranges), st.names[id(p)]
+    trainable = [p for p in m.decoder.parameters()]
+    for p in trainable:
+        g = p._capk_group
+        assert p._capk_offset < st.required_numel[g], st.names[id(p)]
+    b = GradBucketer(st)
+    assert {id(p) for p in frozen} <= b.final

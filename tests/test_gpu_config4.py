@@ -128,3 +128,73 @@ def test_gpt2_beam5_vs_oracle_fp32():
     assert torch.equal(ids.cpu(), ref["sequences"])
     assert torch.equal(info["beam_indices"].cpu(), ref["beam_indices"])
     torch.testing.assert_close(info["sequences_scores"].cpu(), ref["sequences_scores"], rtol=1e-4, atol=1e-5)
+
+
+@cuda
+def test_gpt2_scst_sampling_and_update_vs_oracle():
+    """Config-5 RL step (A16 on A12): the KV-cached GPT-2 sampler (D7 prefix) vs the oracle
+    sampler (oracle/scst.py) over the oracle GPT-2 re-run on each prefix (trainer.py:383-438
+    semantics: generate()'s all-ones mask); then one SCST update with the reference's GPT-2
+    baseline (beam-4 generate, trainer.py:353-356 -> decoders.py:645-654): the loss and every
+    decoder gradient vs torch autograd of the oracle decoder."""
+    import torch.nn.functional as F
+    from capk.train import CapkAdamW
+    from capk.train.scst import cider_d, pg_targets, sample_captions, scst_step, strip_special
+    from oracle import decoders as odec
+    from oracle import encoders as oenc
+    from oracle import scst as oscst
+    z, model, store, cfg = _model("fp32")
+    D, Le, He, Ld, Hd, V, pad, patch, img = [int(x) for x in z["meta/dims"]]
+    images = torch.from_numpy(z["in/images"]).cuda()
+    B = images.shape[0]
+    seed, L = 91, 9
+    sd = {k: v.detach().cpu().float().clone() for k, v in model.state_dict().items()}
+    with torch.no_grad():
+        enc = model.encoder(images)
+        ids, logp = sample_captions(model.decoder, enc, L, seed=seed)
+    p = {k[len("decoder."):]: v for k, v in sd.items() if k.startswith("decoder.")}
+    with torch.no_grad():
+        pooled = oenc.clip_encoder({k[len("encoder.model."):]: v for k, v in sd.items()
+                                    if k.startswith("encoder.model.")}, images.cpu(), Le, He, patch)["pooled_features"]
+        oids = torch.full((B, 1), pad, dtype=torch.long)
+        olp = []
+        for t in range(L - 1):
+            lg = odec.gpt2_decoder(p, pooled, oids, Ld, Hd, pad, use_pad_mask=False)[:, -1]
+            picks = [oscst.sample_row(lg[r].numpy(), seed, t, r) for r in range(B)]
+            nxt = torch.tensor([tok for tok, _, _ in picks])
+            olp.append([lp for _, lp, _ in picks])
+            oids = torch.cat([oids, nxt[:, None]], 1)
+            if bool((nxt == pad).all()):
+                break
+    assert torch.equal(ids.cpu(), oids), (ids.cpu(), oids)
+    np.testing.assert_allclose(logp.cpu().numpy(), np.array(olp, dtype=np.float32).T, rtol=1e-4, atol=1e-4)
+    # one SCST update with the beam-4 baseline
+    refs = [[[3, 5, 7, 9], [5, 7]], [[1, 2, 3]], [[4, 4, 8, 15, 16]]][:B]
+    while len(refs) < B:
+        refs.append([[2, 4, 6]])
+    opt = CapkAdamW(store, lr=0.0, weight_decay=0.0)
+    loss, rs, rb = scst_step(model, images, refs, opt, lr=0.0, seed=seed, max_length=L,
+                             baseline_kwargs={"num_beams": 4})
+    samp = [strip_special(r, pad, pad, pad) for r in ids.cpu().tolist()]
+    with torch.no_grad():
+        base_ids, _ = model.decoder.generate({"pooled_features": enc["pooled_features"]}, L, num_beams=4)
+    base = [strip_special(r, pad, pad, pad) for r in base_ids.cpu().tolist()]
+    adv = torch.tensor(cider_d(samp, refs) - cider_d(base, refs), dtype=torch.float32)
+    assert abs(float(adv.abs().sum())) > 0  # a non-trivial advantage exercises the gradient
+    pr = {k: v.clone().requires_grad_(True) for k, v in p.items()}
+    logits = odec.gpt2_decoder(pr, pooled, ids.cpu(), Ld, Hd, pad, use_pad_mask=False)
+    tgt = pg_targets(ids.cpu(), pad)
+    lp = F.log_softmax(logits[:, :-1], -1).gather(-1, tgt[:, 1:].clamp(min=0)[..., None])[..., 0]
+    mask = (tgt[:, 1:] != -100).float()
+    ref = -(lp * adv[:, None] * mask).sum() / mask.sum()
+    ref.backward()
+    torch.testing.assert_close(loss.cpu(), ref.detach(), rtol=1e-4, atol=1e-6)
+    checked = 0
+    for n, prm in model.decoder.named_parameters():
+        if pr[n].grad is None:
+            continue
+        gref = pr[n].grad
+        torch.testing.assert_close(prm._capk_grad.cpu(), gref, rtol=2e-3, atol=2e-3 * float(gref.abs().max()) + 1e-8,
+                                   msg=lambda m: f"{n}: {m}")
+        checked += 1
+    assert checked >= 4 * Ld

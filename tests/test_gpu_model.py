@@ -273,3 +273,33 @@ def test_decoder_train_mode_dropout_matches_masked_reference(golden_dir):
     for n, t in dec.named_parameters():
         g = P[n].grad if P[n].grad is not None else torch.zeros_like(P[n])
         torch.testing.assert_close(t._capk_grad, g, rtol=1e-3, atol=1e-6, msg=n)
+
+
+@cuda
+def test_vit_pooler_vs_golden_fp32(golden_dir):
+    """A1c: final LayerNorm (eps 1e-12) + tanh pooler on the CLS row (modeling_vit.py:289-301)
+    vs the reference's own ViTModel pooler output (vit_transformer_step.npz out/pooled), and
+    the features that feed the decoder (last_hidden_state[:, 1:], encoders.py:122)."""
+    z = np.load(os.path.join(golden_dir, "vit_transformer_step.npz"), allow_pickle=False)
+    model, store, cfg = _tiny_model(z, "fp32")
+    images = torch.from_numpy(z["in/images"]).cuda()
+    with torch.no_grad():
+        enc = model.encoder(images)
+    np.testing.assert_allclose(enc["pooled_features"].float().cpu().numpy(), z["out/pooled"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(enc["features"].float().cpu().numpy(), z["out/features"], rtol=1e-4, atol=1e-5)
+
+
+@cuda
+def test_vit_pooler_full_bf16_vs_oracle():
+    """A1c in the benchmarked precision at the full ViT-B/16 shape (the tiny golden model's
+    width is below the bf16 GEMM's K granularity): pooled output within 3e-2 relative of the
+    fp32 oracle (oracle/encoders.py vit_model + pooler)."""
+    from oracle import encoders as oenc
+    model, store, cfg, sd = _full_model("bf16")
+    g = torch.Generator().manual_seed(5)
+    images = torch.randn(2, 3, 224, 224, generator=g)
+    with torch.no_grad():
+        got = model.encoder(images.cuda())["pooled_features"].float().cpu()
+        ref = oenc.vit_encoder(_sub(sd, "encoder.model."), images, 12, 12, 16)["pooled_features"]
+    rel = float((got - ref).norm() / ref.norm())
+    assert rel < 3e-2, rel
