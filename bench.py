@@ -53,18 +53,70 @@ def beam_bench(model, batch, reps, device, rank):
     return dt, gem, int(ids.shape[1])
 
 
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "round1", "gemm_traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "round2", "gemm_traffic.json")
+KERNEL_SOURCES = ["gemm.hip", "gemm8p.hip", "gemm_common.h", "common.h", "blaslt.cpp"]
+
+
+def kernel_source_hash():
+    """sha256 over the GEMM kernel sources: ties a committed PMC traffic file to the code it
+    measured (tools/pmc_traffic.py --src-hash writes the same digest)."""
+    import hashlib
+    h = hashlib.sha256()
+    for n in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, "image-captioning-ml-project_amd", "csrc", n), "rb") as f:
+            h.update(n.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
 
 
 def gemm_traffic():
     """HBM bytes per GEMM launch from the committed PMC passes over this same command
-    (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md HBM section)."""
+    (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md HBM section).
+    Reported only when the file was produced from the kernel sources in this tree (source
+    hash match); otherwise null with the reason."""
     try:
         with open(TRAFFIC_FILE) as f:
             t = json.load(f)
-        return round(t["avg_hbm_bytes"]), os.path.relpath(TRAFFIC_FILE, ROOT)
-    except (OSError, KeyError, ValueError):
-        return None, None
+    except (OSError, ValueError):
+        return None, "no traffic file"
+    src = kernel_source_hash()
+    if t.get("src_hash") != src:
+        return None, f"stale: {os.path.relpath(TRAFFIC_FILE, ROOT)} measured sources {t.get('src_hash')}, tree has {src}"
+    return round(t["avg_hbm_bytes"]), os.path.relpath(TRAFFIC_FILE, ROOT)
+
+
+def host_cpus():
+    """CPU threads for the CPU baseline: the node's physical cores, capped by what this
+    process may use (affinity mask and cgroup CPU quota -- a GPU box grants each job a
+    share of the node).  Returns (threads, info)."""
+    phys = set()
+    try:
+        cur = {}
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if ":" in line:
+                    k, v = [x.strip() for x in line.split(":", 1)]
+                    cur[k] = v
+                elif cur:
+                    phys.add((cur.get("physical id"), cur.get("core id")))
+                    cur = {}
+        if cur:
+            phys.add((cur.get("physical id"), cur.get("core id")))
+    except OSError:
+        pass
+    n_phys = len(phys) or (os.cpu_count() or 1)
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
+    limit = min(x for x in (n_phys, aff, quota, omp) if x)
+    return limit, {"node_physical_cores": n_phys, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+                   "omp_num_threads": omp}
 
 
 def build(batch, device):
@@ -222,17 +274,19 @@ def main():
                                             "tflops": round(FLOP_PER_CAPTION * cps / world / 1e12, 1)}}
             if world == 1 and not args.no_cpu_baseline:
                 from oracle.step import time_cpu_beam
-                threads = min(16, os.cpu_count() or 1)
+                threads, hinfo = host_cpus()
                 cps_cpu, cdt = time_cpu_beam(cpu_sd, images=args.cpu_beam_images, threads=threads)
                 rec["beam5"]["cpu_baseline"] = {
                     "value": round(cps_cpu, 3), "unit": "captions/s", "cores": threads, "kind": "port",
+                    "host": hinfo,
                     "sample": f"oracle fp32 CPU: ViT fwd + beam-5 (oracle/beam.py) re-running the decoder on each "
                               f"prefix, {args.cpu_beam_images} images, max_length 20 ({cdt:.1f} s)"}
         if world == 1 and not args.no_cpu_baseline:
             from oracle.step import time_cpu_baseline
-            threads = min(16, os.cpu_count() or 1)
+            threads, hinfo = host_cpus()
             ips, dt = time_cpu_baseline(cpu_sd, batch=args.cpu_batch, steps=args.cpu_steps, threads=threads)
             rec["cpu_baseline"] = {"value": round(ips, 3), "unit": "images/s", "cores": threads, "kind": "port",
+                                   "host": hinfo,
                                    "sample": f"oracle fp32 CPU train step (torch CPU), batch {args.cpu_batch}, "
                                              f"{args.cpu_steps} timed steps after 1 warm-up ({dt:.1f} s)"}
         print(json.dumps(rec), flush=True)

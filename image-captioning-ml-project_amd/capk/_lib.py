@@ -9,7 +9,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcapk.so")
+LIB_PATH = os.environ.get("CAPK_LIB_PATH") or os.path.join(_HERE, "libcapk.so")  # override: diagnostic builds
 
 F32 = 0
 BF16 = 1
@@ -33,6 +33,8 @@ SIGNATURES = {
     "capk_device_arch": (_i, [ctypes.c_char_p, _i]),
     "capk_gemm_workspace": (_sz, [_i, _i, _i, _i, _i]),
     "capk_gemm_last_route": (_i, []),
+    "capk_gemm_last_config": (_i, []),
+    "capk_gemm_force_config": (_i, [_i, _i]),
     "capk_gemm": (_i, [_i, _i, _i, _i, _i, _c_p, _i64, _i, _c_p, _i64, _i, _c_p, _i64, _f, _f,
                        _c_p, _c_p, _i64, _i, _c_p, _c_p, _i64, _f, _u32, _c_p, _sz, _c_p]),
     "capk_dropout_mask": (_i, [_i64, _u64, _f, _u32, _c_p, _c_p]),

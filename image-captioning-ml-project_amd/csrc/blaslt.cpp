@@ -102,8 +102,8 @@ bool build_plan(hipblasLtHandle_t h, const LtKey& k, LtPlan& p) {
 
 bool lt_enabled() {
   static const bool on = [] {
-    const char* e = getenv("CAPK_GEMM_BLASLT");
-    return !(e && e[0] == '0');
+    const char* e = getenv("CAPK_GEMM_BLASLT");  // opt-in A/B reference only (=1)
+    return e && e[0] == '1';
   }();
   return on;
 }

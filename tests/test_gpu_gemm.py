@@ -1,0 +1,90 @@
+"""The 256x256 phased bf16 GEMM (csrc/gemm8p.hip) against a PyTorch fp32 reference of the
+same op on the bf16-rounded inputs: all four operand layouts (forward Linear, dX = dY W,
+dW = dY^T X, and A M-major / B K-major), bf16 and fp32 outputs, ragged M / N tails, K
+tails of the MN-major (token-reduction) operands, split-K slabs, and the fused epilogue
+(bias + GELU + kept pre-activation + residual; backward GELU'; beta accumulate).
+Tolerances: 1e-2 relative with a bf16 output (one bf16 rounding of C), 3e-3 with fp32."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+cuda = pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from capk import _lib, ops as _ops
+    lib = _lib.load()
+    lib.capk_gemm_force_config(5, 0)  # the 256x256 kernel, library route off
+    yield _ops
+    lib.capk_gemm_force_config(-1, -1)
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-30))
+
+
+def _operand(rows, cols, kmajor, g, scale=1.0):
+    """Logical [rows, K=cols] operand stored K-major ([rows][cols]) or MN-major ([cols][rows])."""
+    x = (torch.randn(rows, cols, device="cuda", generator=g) * scale).bfloat16()
+    return x, (x if kmajor else x.t().contiguous())
+
+
+@cuda
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(1000, 520, 640), (768, 256, 1152), (256, 264, 64)])
+@pytest.mark.parametrize("out", [torch.bfloat16, torch.float32])
+def test_layouts_and_tails(ops, ak, bk, M, N, K, out):
+    from capk import _lib
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    a, A = _operand(M, K, ak, g)
+    b, B = _operand(N, K, bk, g, 1.0 / math.sqrt(K))
+    C = torch.empty(M, N, device="cuda", dtype=out)
+    ops.gemm(A, ak, B, bk, M, N, K, C, lda=A.stride(0), ldb=B.stride(0), ldc=C.stride(0))
+    assert _lib.load().capk_gemm_last_config() == 5
+    ref = a.float() @ b.float().t()
+    assert _rel(C, ref) < (1e-2 if out == torch.bfloat16 else 3e-3), (ak, bk, M, N, K)
+
+
+@cuda
+@pytest.mark.parametrize("K", [1000, 50432 // 4])
+def test_weight_gradient_split_k_with_token_tail(ops, K):
+    """dW[N, Kd] = dY^T X with the token reduction K not a multiple of 64 (zero-filled tail)
+    and long enough for split-K slabs; fp32 output accumulated with beta = 1."""
+    g = torch.Generator(device="cuda").manual_seed(K)
+    N, Kd = 768, 512
+    dy = torch.randn(K, N, device="cuda", generator=g).bfloat16()
+    x = torch.randn(K, Kd, device="cuda", generator=g).bfloat16()
+    dw = torch.randn(N, Kd, device="cuda", generator=g)
+    dw0 = dw.clone()
+    ops.linear_dw(dy, x, dw, accumulate=True)
+    ref = dw0 + dy.float().t() @ x.float()
+    assert _rel(dw, ref) < 3e-3
+
+
+@cuda
+def test_fused_epilogues(ops):
+    from capk._lib import ACT_GELU_ERF
+    g = torch.Generator(device="cuda").manual_seed(7)
+    M, N, K = 1100, 768, 768
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)).bfloat16()
+    bias = torch.randn(N, device="cuda", generator=g)
+    res = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    y = ops.linear(x, w, bias, residual=res, act=ACT_GELU_ERF, preact=pre)
+    ref_pre = x.float() @ w.float().t() + bias
+    assert _rel(pre, ref_pre) < 1e-2
+    assert _rel(y, F.gelu(ref_pre) + res.float()) < 1e-2
+    # bias + GELU with kept pre-activation and no residual (the FFN1 shape)
+    y2 = ops.linear(x, w, bias, act=ACT_GELU_ERF, preact=pre)
+    assert _rel(y2, F.gelu(ref_pre)) < 1e-2
+    # backward: dX * gelu'(aux)
+    dy = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    dxa = ops.linear_dx(dy, w, act_bwd=ACT_GELU_ERF, aux=pre)  # N == K here: aux has dX's shape
+    a = pre.float().requires_grad_(True)
+    F.gelu(a).backward(dy.float() @ w.float())
+    assert _rel(dxa, a.grad) < 1e-2

@@ -7,7 +7,7 @@ sys.path.insert(0, os.path.join(ROOT, "image-captioning-ml-project_amd"))
 import torch  # noqa: E402
 
 from capk import ops  # noqa: E402
-from capk._lib import ACT_GELU_ERF  # noqa: E402
+from capk._lib import ACT_DERIV, ACT_GELU_ERF  # noqa: E402
 
 T = 256 * 197
 SHAPES = [  # name, M, N, K, kind
@@ -18,6 +18,11 @@ SHAPES = [  # name, M, N, K, kind
     ("vit_qkv_dw", T, 2304, 768, "dw"),
     ("lm_head_fwd", 5120, 50304, 768, "fwd"), ("lm_head_dx", 5120, 768, 50304, "dx"), ("lm_head_dw", 5120, 50304, 768, "dw"),
     ("dec_fc1_fwd", 5120, 3072, 768, "fwd_gelu"), ("dec_kv_fwd", T - 1, 1536, 768, "fwd"),
+    # epilogue isolation: the FFN shapes without their activation
+    ("vit_fc1_fwd_plain", T, 3072, 768, "fwd"), ("vit_fc2_dx_plain", T, 3072, 768, "dx"),
+    ("vit_fc1_fwd_bias_res", T, 3072, 768, "fwd_res"),
+    # the model's forms: GELU with CAPK_ACT_DERIV (kept act'(pre); backward multiplies by it)
+    ("vit_fc1_fwd_gelu_deriv", T, 3072, 768, "fwd_gelu_deriv"), ("vit_fc2_dx_gelu_deriv", T, 3072, 768, "dx_gelu_deriv"),
 ]
 
 
@@ -29,12 +34,15 @@ def run(name, M, N, K, kind, iters=20):
         w = (torch.randn(N, K, device=dev, generator=g) * 0.02).bfloat16()
         b = torch.zeros(N, device=dev)
         pre = torch.empty(M, N, device=dev, dtype=torch.bfloat16) if "gelu" in kind else None
-        fn = lambda: ops.linear(x, w, b, act=ACT_GELU_ERF if pre is not None else 0, preact=pre)
+        res = torch.randn(M, N, device=dev, generator=g).bfloat16() if "res" in kind else None
+        act = (ACT_GELU_ERF | (ACT_DERIV if "deriv" in kind else 0)) if pre is not None else 0
+        fn = lambda: ops.linear(x, w, b, act=act, preact=pre, residual=res)
     elif kind.startswith("dx"):  # dX[M,K'] = dY[M,N'] W[N',K'] with K'=N, N'=K of the table entry
         dy = torch.randn(M, K, device=dev, generator=g).bfloat16()
         w = (torch.randn(K, N, device=dev, generator=g) * 0.02).bfloat16()
         aux = torch.randn(M, N, device=dev, generator=g).bfloat16() if "gelu" in kind else None
-        fn = lambda: ops.linear_dx(dy, w, act_bwd=ACT_GELU_ERF if aux is not None else 0, aux=aux)
+        act = (ACT_GELU_ERF | (ACT_DERIV if "deriv" in kind else 0)) if aux is not None else 0
+        fn = lambda: ops.linear_dx(dy, w, act_bwd=act, aux=aux)
     else:  # dW[N,K] = dY[M,N]^T X[M,K]
         dy = torch.randn(M, N, device=dev, generator=g).bfloat16()
         x = torch.randn(M, K, device=dev, generator=g).bfloat16()

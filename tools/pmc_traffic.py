@@ -8,7 +8,9 @@ global_load_lds / buffer_load ... lds alike -- how every GEMM operand tile is st
 so it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores (the GEMM epilogue).
 Infinity-Cache hits are counted, so tile re-reads absorbed on-die still show up here.
 
-usage: pmc_traffic.py FETCH_DIR WRITE_DIR [--match gemm_bf16_kernel,gemm256_kernel,Cijk_] [--out FILE] [--cmd TEXT]
+usage: pmc_traffic.py FETCH_DIR WRITE_DIR [--match ...] [--out FILE] [--cmd TEXT]
+The output records src_hash (bench.kernel_source_hash() of this tree): bench.py reports the
+traffic only while the GEMM sources still hash to it.
 (Cijk_* = hipBLASLt's GEMM kernels, the library route of capk_gemm)
 """
 import argparse
@@ -39,7 +41,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
-    ap.add_argument("--match", default="gemm_bf16_kernel,gemm256_kernel,Cijk_")
+    ap.add_argument("--match", default="gemm_bf16_kernel,gemm8p_kernel,Cijk_,act_pass_kernel,splitk_reduce_kernel")
     ap.add_argument("--out")
     ap.add_argument("--cmd", default="")
     a = ap.parse_args()
@@ -54,7 +56,13 @@ def main():
         e = by_kernel[fn[k][:90]]
         e[0] += 1
         e[1] += 2.0 * 1024.0 * v
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))), "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
     res = {"counters": ["FETCH_SIZE", "WRITE_SIZE"], "kernels_matched": match, "command": a.cmd,
+           "src_hash": bench.kernel_source_hash(),
            "dispatches_fetch_pass": nf, "dispatches_write_pass": nw,
            "avg_fetch_bytes": fetch, "avg_write_bytes": write, "avg_hbm_bytes": fetch + write,
            "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 reports half of 16-B/lane streaming reads); WRITE_SIZE KiB x1024",
