@@ -139,6 +139,51 @@ def build(batch, device):
     return cfg, model, store, opt, loss_fn, cpu_sd
 
 
+def dist_init(backend=None):
+    """One process per GPU (torchrun env).  backend: "nccl" (= RCCL) on the GPU node; the
+    CPU tests drive this same path with "gloo"."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if (backend or "nccl") == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    return world, rank, local
+
+
+def timed_steps(step, steps, warmup, world, sync, device="cuda"):
+    """W untimed steps, then exactly K timed steps bracketed by barrier + device sync on
+    both sides; returns the MAX elapsed seconds over ranks (the driver's contract)."""
+    for _ in range(warmup):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    return elapsed
+
+
+def throughput(per_rank_batch, world, steps, elapsed):
+    """Whole-job images/s: every rank's images over the slowest rank's time (weak scaling)."""
+    return per_rank_batch * world * steps / elapsed
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -151,15 +196,11 @@ def main():
     ap.add_argument("--beam-batch", type=int, default=256, help="images per beam-5 batch (0 = skip)")
     ap.add_argument("--beam-reps", type=int, default=3)
     ap.add_argument("--cpu-beam-images", type=int, default=24)
+    ap.add_argument("--grad-exchange", choices=["fp32", "bf16"], default="bf16",
+                    help="DP gradient all-reduce precision (fp32 master weights either way)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    world, rank, local = dist_init("nccl")
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
@@ -174,7 +215,7 @@ def main():
     captions = torch.randint(0, 50256, (B, 20), device=device, generator=g1)
     total_steps = 10_000
     # DP: gradient all-reduce buckets launched during the backward (capk/train/dp.py)
-    bucketer = GradBucketer(store) if world > 1 else None
+    bucketer = GradBucketer(store, exchange=args.grad_exchange) if world > 1 else None
     step_no = [0]
     model.train()  # trainer.py:210: decoder dropout (p=0.1) active in the timed step
 
@@ -190,26 +231,17 @@ def main():
         step_no[0] += 1
         return loss
 
+    last = [None]
+
+    def timed_step():
+        last[0] = step()
+
     for _ in range(args.warmup):
-        loss = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ops.GEMM_TIMER.start()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+        timed_step()
+    ops.GEMM_TIMER.start()  # HIP events around every capk_gemm launch of the timed steps
+    elapsed = timed_steps(timed_step, args.steps, 0, world, torch.cuda.synchronize, device)
     ops.GEMM_TIMER.stop()
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
+    loss = last[0]
     gem = ops.GEMM_TIMER.summary()
     final_loss = float(loss)
     beam = None
@@ -223,7 +255,7 @@ def main():
 
     if rank == 0:
         ms = elapsed / args.steps * 1e3
-        value = B * world * args.steps / elapsed
+        value = throughput(B, world, args.steps, elapsed)
         achieved = gem["avg_flops"] / (gem["avg_ms"] * 1e-3) / 1e12 if gem["launches"] else 0.0
         traffic, traffic_src = gemm_traffic()
         rec = {
@@ -241,7 +273,8 @@ def main():
             "data": "synthetic (randn 224x224x3 images, randint 20-token captions), random-init weights",
             "config": {"workload": "config 3: ViT-B/16 + Transformer(6L,8H) + multi_head, CE train step",
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": 20, "image_tokens": 197,
-                       "vocab": 50257, "parallelism": f"dp{world}"},
+                       "vocab": 50257, "parallelism": f"dp{world}",
+                       "grad_exchange": args.grad_exchange if world > 1 else None},
             "roofline": {"bound": "mfma", "kernel": "bf16 GEMM family: every capk_gemm launch in the timed steps "
                                                     "(hand-written gemm_bf16_kernel + hipBLASLt plain products)",
                          "by_route": {k: {"launches": v["launches"], "ms": round(v["total_ms"], 2),

@@ -18,7 +18,14 @@ compute stream carries on with the next layer's backward.  ``finish()`` launches
 the remainder and makes the compute stream wait for every collective before the
 optimizer step.  Every rank issues the same collectives in the same order (the
 notifications follow the same backward on every rank).
+
+``exchange="bf16"`` halves the wire bytes (SURVEY §5 budgets bf16): each bucket is cast
+to a bf16 staging copy on the compute stream, the all-reduce runs on the copy, and
+``finish()`` writes the averaged values back into the fp32 gradient buffer (the fp32
+master weights and moments are untouched; only the exchanged gradient is rounded to
+bf16, once per rank and once per ring reduction step).
 """
+import torch
 import torch.distributed as dist
 
 from ..params import _alloc_numel, _round
@@ -59,10 +66,16 @@ class GradBucketer:
     Installs itself on the store (``store._capk_bucketer``) so model code can notify it.
     """
 
-    def __init__(self, store, bucket_elems=BUCKET_ELEMS):
+    def __init__(self, store, bucket_elems=BUCKET_ELEMS, exchange="fp32"):
+        if exchange not in ("fp32", "bf16"):
+            raise ValueError(f"GradBucketer: exchange must be 'fp32' or 'bf16', got {exchange!r}")
         self.store = store
         self.bucket_elems = int(bucket_elems)
+        self.exchange = exchange
         self.active = _active()
+        # bf16 staging buffers, one per gradient group, laid out like the fp32 buffers
+        self.stage = ({g: torch.empty(b.numel(), dtype=torch.bfloat16, device=b.device) for g, b in store.grad.items()}
+                      if exchange == "bf16" and self.active else None)
         # per group: [start, end) of every parameter, in buffer order
         self.spans = {}
         for g, plist in store.groups.items():
@@ -95,7 +108,12 @@ class GradBucketer:
         buf = self.store.grad[g]
         for s in range(lo, hi, self.bucket_elems):
             chunk = buf[s:min(hi, s + self.bucket_elems)]
-            self.works.append((dist.all_reduce(chunk, op=self.op, async_op=True), chunk))
+            if self.stage is not None:
+                wire = self.stage[g][s:min(hi, s + self.bucket_elems)]
+                _cast(chunk, wire)
+            else:
+                wire = chunk
+            self.works.append((dist.all_reduce(wire, op=self.op, async_op=True), chunk, wire))
 
     def finish(self):
         """Launch what is left, then join every collective (the current stream waits)."""
@@ -103,8 +121,20 @@ class GradBucketer:
             for g in self.spans:
                 if self.hi[g] > 0:
                     self._launch(g, 0, self.hi[g])
-            for work, chunk in self.works:
+            for work, chunk, wire in self.works:
                 work.wait()
+                if wire is not chunk:
+                    _cast(wire, chunk)
                 if self.need_scale:
                     chunk.div_(self.world)
         self.reset()
+
+
+def _cast(src, dst):
+    """dst <- src (fp32 <-> bf16) on the current stream: the capk cast kernel on the GPU,
+    torch on the CPU (gloo tests)."""
+    if src.is_cuda:
+        from .. import ops
+        ops.cast(src, dst)
+    else:
+        dst.copy_(src)

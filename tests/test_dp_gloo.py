@@ -91,7 +91,7 @@ def _worker(rank, world, port, golden, out):
     dist.destroy_process_group()
 
 
-def _worker_overlap(rank, world, port, golden, out):
+def _worker_overlap(rank, world, port, golden, out, exchange="fp32"):
     """GradBucketer: gradients become final in reverse registration order (as in the
     backward), each followed by a notification; buckets launch asynchronously while
     later gradients are still being written."""
@@ -103,7 +103,7 @@ def _worker_overlap(rank, world, port, golden, out):
     from capk.params import attach, notify_final
     from capk.train.dp import GradBucketer
     store = attach(m, "cpu")
-    bucketer = GradBucketer(store, bucket_elems=1000)
+    bucketer = GradBucketer(store, bucket_elems=1000, exchange=exchange)
     D, Le, He, Ld, Hd, V, pad, patch, img = dims
     g = torch.Generator().manual_seed(123)
     images = torch.randn(4, 3, img, img, generator=g)
@@ -126,18 +126,23 @@ def _worker_overlap(rank, world, port, golden, out):
             launched.append(len(bucketer.works))
         bucketer.finish()
         err = max(float((named[n]._capk_grad - full[n]).abs().max()) for n in full)
+        gmax = max(float(full[n].abs().max()) for n in full)
         if rank == 0:
-            torch.save({"err": err, "early": launched[len(launched) // 2]}, out)
+            torch.save({"err": err, "gmax": gmax, "early": launched[len(launched) // 2]}, out)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_dp_overlapped_buckets_equal_full_batch(tmp_path, golden_dir):
+@pytest.mark.parametrize("exchange,tol", [("fp32", 1e-5), ("bf16", 1e-2)])
+def test_dp_overlapped_buckets_equal_full_batch(tmp_path, golden_dir, exchange, tol):
+    """fp32 exchange: equal to the full-batch gradient to fp32 rounding.  bf16 exchange:
+    every gradient element within 1e-2 x the largest gradient magnitude (one bf16 rounding
+    per rank and per reduction step, 8 significant bits)."""
     out = str(tmp_path / "dpo.pt")
     golden = os.path.join(golden_dir, "vit_transformer_step.npz")
-    mp.spawn(_worker_overlap, args=(2, _free_port(), golden, out), nprocs=2, join=True)
+    mp.spawn(_worker_overlap, args=(2, _free_port(), golden, out, exchange), nprocs=2, join=True)
     res = torch.load(out, weights_only=True)
-    assert res["err"] < 1e-5, res
+    assert res["err"] < tol * max(1.0, res["gmax"]), res
     assert res["early"] > 0, res  # collectives were in flight before the last gradient was written
 
 
@@ -147,3 +152,66 @@ def test_dp_allreduce_equals_full_batch(tmp_path, golden_dir):
     mp.spawn(_worker, args=(2, _free_port(), golden, out), nprocs=2, join=True)
     res = torch.load(out, weights_only=True)
     assert res["err"] < 1e-5, res
+
+
+def _worker_bench(rank, world, port, golden, out):
+    """bench.py's own N>1 path on CPU: dist_init (torchrun env vars), the backward-overlapped
+    GradBucketer with the bf16 exchange bench.py uses by default, timed_steps' barrier +
+    MAX-over-ranks timing, and the whole-job throughput formula."""
+    import importlib.util
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    w, r, local = bench.dist_init("gloo")
+    assert (w, r, local) == (world, rank, rank)
+    torch.manual_seed(0)
+    m, sd, dims = _tiny(golden)
+    from capk.params import attach, notify_final
+    from capk.train.dp import GradBucketer
+    store = attach(m, "cpu")
+    bucketer = GradBucketer(store, bucket_elems=4096, exchange="bf16")
+    D, Le, He, Ld, Hd, V, pad, patch, img = dims
+    g = torch.Generator().manual_seed(7)
+    images = torch.randn(4, 3, img, img, generator=g)
+    caps = torch.randint(0, V - 1, (4, 7), generator=g)
+    shard = slice(rank * 2, rank * 2 + 2)
+    named = dict(m.named_parameters())
+    order = [n for n in reversed(list(named)) if id(named[n]) in store.optional]
+    order += [n for n in reversed(list(named)) if id(named[n]) not in store.optional]
+    n_steps = [0]
+
+    def step():  # the backward writes gradients in reverse order and notifies, then finish()
+        grads = _oracle_grads(sd, dims, images[shard], caps[shard])
+        for n in order:
+            with torch.no_grad():
+                named[n]._capk_grad.copy_(grads[n])
+            notify_final(store, [named[n]])
+        bucketer.finish()
+        n_steps[0] += 1
+        if rank == 1:
+            import time
+            time.sleep(0.05)  # the slower rank sets the reported time
+
+    elapsed = bench.timed_steps(step, 2, 1, world, sync=lambda: None, device="cpu")
+    full = _oracle_grads(sd, dims, images, caps)
+    err = max(float((named[n]._capk_grad - full[n]).abs().max()) for n in full)
+    gmax = max(float(full[n].abs().max()) for n in full)
+    value = bench.throughput(2, world, 2, elapsed)
+    torch.save({"elapsed": elapsed, "err": err, "gmax": gmax, "steps": n_steps[0], "value": value},
+               out + f".{rank}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_dp_path_gloo(tmp_path, golden_dir):
+    out = str(tmp_path / "bench")
+    golden = os.path.join(golden_dir, "vit_transformer_step.npz")
+    mp.spawn(_worker_bench, args=(2, _free_port(), golden, out), nprocs=2, join=True)
+    r0 = torch.load(out + ".0", weights_only=True)
+    r1 = torch.load(out + ".1", weights_only=True)
+    assert r0["steps"] == r1["steps"] == 3  # 1 warm-up + 2 timed
+    assert r0["elapsed"] == r1["elapsed"] >= 0.1  # MAX over ranks: rank 1's 2 x 50 ms sleeps
+    assert abs(r0["value"] - 2 * 2 * 2 / r0["elapsed"]) < 1e-9
+    assert r0["err"] < 1e-2 * max(1.0, r0["gmax"]), r0  # bf16 exchange of the averaged gradient
