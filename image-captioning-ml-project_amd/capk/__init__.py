@@ -16,9 +16,14 @@ __version__ = "0.1.0"
 
 def prepare(model, device="cuda", precision="bf16"):
     """Move `model` to the GPU, re-home its parameters into the flat ParamStore and
-    select the kernel precision ('bf16' throughput path, 'fp32' parity path)."""
+    select the kernel precision ('bf16' throughput path, 'fp32' parity path, 'fp8' =
+    bf16 with the large forward Linear / Conv1D products on e4m3 scaled MFMA -- config 5)."""
     _lib.load()
     model.to(device)
     store = attach(model, device)
-    set_precision(model, precision)
+    set_precision(model, "bf16" if precision == "fp8" else precision)
+    if precision == "fp8":
+        ops.FP8.enable(store)
+    elif ops.FP8.enabled:
+        ops.FP8.disable()
     return store

@@ -55,7 +55,7 @@ def build_parser():
     # offline extras
     p.add_argument("--steps", type=int, default=None,
                    help="synthetic batches to run (train: CE steps; eval: generate); 0 = build only")
-    p.add_argument("--precision", type=str, default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--precision", type=str, default="bf16", choices=["bf16", "fp32", "fp8"])
     p.add_argument("--seed", type=int, default=None)
     return p
 

@@ -63,7 +63,7 @@ class KernelTimer:
     def summary(self):
         torch.cuda.synchronize()
         tot_ms, tot_flops, tot_bytes, n = 0.0, 0.0, 0.0, 0
-        route = {0: [0, 0.0, 0.0], 1: [0, 0.0, 0.0]}  # per path: launches, ms, flops
+        route = {0: [0, 0.0, 0.0], 1: [0, 0.0, 0.0], 2: [0, 0.0, 0.0]}  # per path: launches, ms, flops
         for s, e, fl, _, by, rt in self.records:
             ms = s.elapsed_time(e)
             tot_ms += ms
@@ -74,7 +74,7 @@ class KernelTimer:
             route[rt][1] += ms
             route[rt][2] += fl
         by_route = {name: {"launches": r[0], "total_ms": r[1], "tflops": (r[2] / (r[1] * 1e-3) / 1e12) if r[1] else 0.0}
-                    for name, r in (("gemm_bf16_kernel", route[0]), ("hipblaslt", route[1]))}
+                    for name, r in (("gemm_bf16_kernel", route[0]), ("hipblaslt", route[1]), ("gemm_f8", route[2]))}
         return {"launches": n, "total_ms": tot_ms, "flops": tot_flops, "by_route": by_route,
                 "avg_ms": tot_ms / max(n, 1), "avg_flops": tot_flops / max(n, 1), "avg_bytes": tot_bytes / max(n, 1)}
 
@@ -111,12 +111,117 @@ def gemm(A, a_kmajor, B, b_kmajor, M, N, K, C, *, lda, ldb, ldc, alpha=1.0, beta
     return C
 
 
+# ------------------------------------------------------------------- fp8 ----
+class Fp8State:
+    """Config 5's fp8 forward (BASELINE configs[4]): when enabled (capk.prepare(...,
+    precision='fp8')), forward Linear / Conv1D products whose weight lives in the model's
+    ParamStore and whose grid fills the chip run as e4m3 x e4m3 scaled-MFMA GEMMs
+    (capk_gemm_f8); the activation is quantised per row on the fly, the weight once per
+    optimizer step (lazily, on first use after `weights_changed`).  Backward products stay
+    bf16 against the bf16 weights and the saved bf16 activations."""
+
+    def __init__(self):
+        self.enabled = False
+        self.epoch = 0
+        self.ranges = []  # (start, end) byte ranges of the ParamStore bf16 shadows
+        self.cache = {}   # (ptr, shape, stride, transposed) -> [epoch, q, scale]
+        self.min_rows = 256  # products with fewer rows (decode steps of small batches) stay bf16
+        self.min_ctas = 96  # 256x256 tiles (x2 for K >= 2048) below which the bf16 kernels run instead
+
+    def enable(self, store):
+        self.ranges = [(b.data_ptr(), b.data_ptr() + b.numel() * b.element_size())
+                       for b in store.bf16.values() if b is not None]
+        self.cache.clear()
+        self.enabled = True
+
+    def disable(self):
+        self.enabled = False
+        self.cache.clear()
+
+    def weights_changed(self):
+        self.epoch += 1
+
+    def is_weight(self, w):
+        p = w.data_ptr()
+        return any(a <= p < b for a, b in self.ranges)
+
+
+FP8 = Fp8State()
+
+
+def quant_fp8(x, *, transpose=False, q=None, scale=None):
+    """e4m3fn rows with E8M0 per-row scales (capk_quant_fp8).  transpose: x [K, N] -> q [N, K]."""
+    _need_gpu(x)
+    rows, cols = (x.shape[1], x.shape[0]) if transpose else x.shape
+    if q is None:
+        q = torch.empty(rows, cols, dtype=torch.uint8, device=x.device)
+    if scale is None:
+        scale = torch.empty(rows, dtype=torch.uint8, device=x.device)
+    check(lib().capk_quant_fp8(dtype_code(x), rows, cols, _p(x), x.stride(0), int(transpose), _p(q), q.stride(0),
+                               _p(scale), _stream()), "capk_quant_fp8")
+    return q, scale
+
+
+def gemm_f8(a, sa, b, sb, C, *, beta=0.0, bias=None, residual=None, act=0, preact=None, drop=NO_DROP):
+    """C = epilogue((2^sa A8) (2^sb B8)^T): A8 [M,K], B8 [N,K] e4m3fn (uint8 storage)."""
+    _need_gpu(a, b, C)
+    L = lib()
+    M, K = a.shape
+    N = b.shape[0]
+    wsb = L.capk_gemm_f8_workspace(M, N, K)
+    ws = _ws(wsb, a.device)
+    timed = GEMM_TIMER.enabled
+    if timed:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    rc = L.capk_gemm_f8(dtype_code(C), M, N, K, _p(a), a.stride(0), _p(sa), _p(b), b.stride(0), _p(sb), _p(C),
+                        C.stride(0), float(beta), _p(bias), _p(residual),
+                        residual.stride(0) if residual is not None else 0, int(act), _p(preact),
+                        preact.stride(0) if preact is not None else 0, float(drop[0]), int(drop[1]) & 0xFFFFFFFF,
+                        _p(ws), wsb if ws is not None else 0, _stream())
+    check(rc, "capk_gemm_f8")
+    if timed:
+        ev1.record()
+        nbytes = M * K + N * K + M + N + C.element_size() * M * N * (2 if beta else 1)
+        GEMM_TIMER.records.append((ev0, ev1, 2.0 * M * N * K, 2, nbytes, 2))
+    return C
+
+
+def _fp8_route(x, w, M, N, K, act, transposed):
+    """(q_w, s_w) when this forward product runs in fp8, else None."""
+    if not FP8.enabled or x.dtype != torch.bfloat16 or (act & ACT_BWD) or K % 128 or N % 8 or M < FP8.min_rows:
+        return None
+    if not FP8.is_weight(w):
+        return None
+    ctas = ((M + 255) // 256) * ((N + 255) // 256)
+    if ctas < FP8.min_ctas and not (K >= 2048 and ctas * 2 >= FP8.min_ctas):
+        return None
+    key = (w.data_ptr(), tuple(w.shape), tuple(w.stride()), transposed)
+    ent = FP8.cache.get(key)
+    if ent is None:
+        ent = FP8.cache[key] = [-1, torch.empty(N, K, dtype=torch.uint8, device=w.device),
+                                torch.empty(N, dtype=torch.uint8, device=w.device)]
+    if ent[0] != FP8.epoch:
+        quant_fp8(w, transpose=transposed, q=ent[1], scale=ent[2])
+        ent[0] = FP8.epoch
+    return ent[1], ent[2]
+
+
+def _linear_f8(x, qw, sw, out, b, residual, act, preact, drop):
+    qx, sx = quant_fp8(x)
+    return gemm_f8(qx, sx, qw, sw, out, bias=b, residual=residual, act=act, preact=preact, drop=drop)
+
+
 def linear(x, w, b=None, *, out=None, residual=None, act=0, preact=None, out_dtype=None, drop=NO_DROP):
     """y = dropout(act(x @ w^T + b)) + residual; x [M,K] (row stride may exceed K), w [N,K] contiguous."""
     M, K = x.shape
     N = w.shape[0]
     if out is None:
         out = torch.empty(M, N, dtype=out_dtype or x.dtype, device=x.device)
+    f8 = _fp8_route(x, w, M, N, K, act, False)
+    if f8 is not None:
+        return _linear_f8(x, f8[0], f8[1], out, b, residual, act, preact, drop)
     gemm(x, True, w, True, M, N, K, out, lda=x.stride(0), ldb=w.stride(0), ldc=out.stride(0), bias=b,
          residual=residual, ldr=residual.stride(0) if residual is not None else 0, act=act, preact=preact,
          ldx=preact.stride(0) if preact is not None else 0, drop=drop)
@@ -342,6 +447,9 @@ def conv1d(x, w, b=None, *, out=None, residual=None, act=0, preact=None, drop=NO
     N = w.shape[1]
     if out is None:
         out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    f8 = _fp8_route(x, w, M, N, K, act, True)
+    if f8 is not None:
+        return _linear_f8(x, f8[0], f8[1], out, b, residual, act, preact, drop)
     gemm(x, True, w, False, M, N, K, out, lda=x.stride(0), ldb=w.stride(0), ldc=out.stride(0), bias=b,
          residual=residual, ldr=residual.stride(0) if residual is not None else 0, act=act, preact=preact,
          ldx=preact.stride(0) if preact is not None else 0, drop=drop)

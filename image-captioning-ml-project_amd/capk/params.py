@@ -180,6 +180,7 @@ class ParamStore:
     def refresh_shadow(self):
         """Re-derive the bf16 shadow after the master weights changed outside the optimizer."""
         from . import ops
+        ops.FP8.weights_changed()
         for g in self.groups:
             if self.bf16[g] is not None and self.master[g].is_cuda:
                 ops.cast(self.master[g], self.bf16[g])

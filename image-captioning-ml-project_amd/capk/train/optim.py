@@ -89,6 +89,7 @@ class CapkAdamW:
                 ops.adamw(st.master[g][s:e], st.grad[g][s:e], self.m[g][s:e], self.v[g][s:e], sh, glr,
                           pg["weight_decay"], self.betas[0], self.betas[1], self.eps, n)
         st.written_optional.clear()
+        ops.FP8.weights_changed()  # fp8 weight copies are re-quantised on their next use
 
     def zero_grad(self, set_to_none=False):
         # capk backward passes overwrite every gradient they produce (no accumulation

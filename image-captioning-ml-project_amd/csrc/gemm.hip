@@ -517,3 +517,68 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
   }
   return CAPK_OK;
 }
+
+// fp8 GEMM (config 5): C = epilogue((diag(2^sa) A8) (diag(2^sb) B8)^T), A8 [M][K], B8 [N][K]
+// e4m3fn, scales E8M0 per row (capk_quant_fp8).  The 256x256 kernel only (F8 variant of
+// gemm8p: 128-deep K-tiles of v_mfma_scale_f32_16x16x128_f8f6f4), split-K as for bf16.
+extern "C" size_t capk_gemm_f8_workspace(int M, int N, int K) {
+  const int s = choose_splits(5, M, N, K / 2);  // 128-deep K-tiles: half as many as bf16's 64
+  return s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
+}
+
+extern "C" int capk_gemm_f8(int out_dtype, int M, int N, int K, const void* A, int64_t lda, const void* a_scale,
+                            const void* B, int64_t ldb, const void* b_scale, void* C, int64_t ldc, float beta,
+                            const float* bias, const void* residual, int64_t ldr, int act, void* preact, int64_t ldx,
+                            float drop_p, uint32_t drop_seed, void* ws, size_t ws_bytes, void* stream) {
+  CAPK_CHECK_ARG(M > 0 && N > 0 && K > 0, "capk_gemm_f8: bad sizes M=%d N=%d K=%d", M, N, K);
+  CAPK_CHECK_ARG(A && B && C && a_scale && b_scale, "capk_gemm_f8: null operand");
+  CAPK_CHECK_ARG(K % 128 == 0, "capk_gemm_f8: K=%d must be a multiple of 128", K);
+  CAPK_CHECK_ARG(N % 8 == 0, "capk_gemm_f8: N=%d must be a multiple of 8", N);
+  CAPK_CHECK_ARG(!(act & CAPK_ACT_BWD), "capk_gemm_f8: forward products only");
+  CAPK_CHECK_ARG(out_dtype == CAPK_BF16 || out_dtype == CAPK_F32, "capk_gemm_f8: unknown out_dtype");
+  CAPK_CHECK_ARG(((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % 16 == 0 && ldb % 16 == 0 &&
+                     lda >= K && ldb >= K,
+                 "capk_gemm_f8: A/B must be 16-B aligned with lda, ldb >= K and %% 16 == 0");
+  const int64_t esz = out_dtype == CAPK_F32 ? 4 : 2;
+  CAPK_CHECK_ARG(((uintptr_t)C % 16 == 0) && (ldc * esz) % 16 == 0, "capk_gemm_f8: C alignment");
+  Epi e{C, ldc, 1.f, beta, bias, residual, ldr, act, preact, nullptr, ldx, M, N, make_drop(drop_p, drop_seed)};
+  hipStream_t st = S(stream);
+  int splits = choose_splits(5, M, N, K / 2);
+  if (!ws || ws_bytes < (size_t)splits * M * N * sizeof(float)) splits = 1;
+  const int grid = tiles_of(5, M, N) * splits;
+  float* slab = splits > 1 ? (float*)ws : nullptr;
+  // activation: plain product (+ bias) into preact / C, then the elementwise pass (as bf16 cfg 5)
+  const bool split = (act & 15) && !(drop_p > 0.f) && !residual && beta == 0.f && out_dtype == CAPK_BF16 &&
+                     splits == 1;
+  const int from_pre = !(act & CAPK_ACT_DERIV) && preact != nullptr;
+  Epi ep = e;
+  if (split) {
+    ep.act = 0;
+    ep.pre = nullptr;
+    if (from_pre) {
+      ep.C = preact;
+      ep.ldc = ldx;
+    }
+  }
+  const int rc = launch_gemm8p_f8(out_dtype == CAPK_F32, grid, A, lda, (const uint8_t*)a_scale, B, ldb,
+                                  (const uint8_t*)b_scale, M, N, K, splits, splits > 1 ? e : ep, slab, st);
+  if (rc != CAPK_OK) return rc;
+  if (split) {
+    const int64_t segs = (int64_t)M * (N / 8);
+    const bool dense = ldc == N && ldx == N && from_pre;
+    const int grid_a = (int)std::min<int64_t>(dense ? cdiv(segs, 512) : cdiv(segs, 256), dense ? (1 << 20) : 8192);
+    hipLaunchKernelGGL(act_pass_kernel<bf16>, dim3(grid_a), dim3(256), 0, st, M, N, (bf16*)C, ldc, (bf16*)preact,
+                       (const bf16*)nullptr, ldx, act, from_pre);
+    CAPK_LAUNCH_CHECK("act_pass_kernel");
+  }
+  if (splits > 1) {
+    const int64_t n8 = (int64_t)M * N / 8;
+    const int g = (int)std::min<int64_t>(2048, (n8 + 255) / 256);
+    if (out_dtype == CAPK_BF16)
+      hipLaunchKernelGGL(splitk_reduce_kernel<bf16>, dim3(g), dim3(256), 0, st, (const float*)ws, splits, e);
+    else
+      hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)ws, splits, e);
+    CAPK_LAUNCH_CHECK("splitk_reduce_kernel");
+  }
+  return CAPK_OK;
+}

@@ -57,12 +57,12 @@ __device__ __forceinline__ void raw_barrier() {
 // row (K-major) / column (MN-major) is row0; k0 = 0.  K-major image [128 rows][64 k]
 // (chunk c of row r at c ^ swz_k<64>(r)); MN-major image [64 k][128 cols] (chunk c of
 // k-row r at c ^ swz_t(r)).
-template <bool KMAJ>
+template <bool KMAJ, int ESZ = 2>
 __device__ __forceinline__ uint32_t piece_voff(int ins, int lane, int row0, int rows, int64_t ld) {
   if constexpr (KMAJ) {
     const int r = ins * 8 + (lane >> 3);
     const int lc = (lane & 7) ^ swz_k<64>(r);
-    return (uint32_t)(((int64_t)(row0 + r) * ld + lc * 8) * 2);
+    return (uint32_t)((int64_t)(row0 + r) * ld * ESZ + lc * 16);
   } else {
     const int kr = ins * 4 + (lane >> 4);
     const int lc = (lane & 15) ^ swz_t(kr);
@@ -96,13 +96,42 @@ __device__ __forceinline__ bf16x8 frag(const char* half, int rbase, int s, int l
   }
 }
 
+// fp8 (F8): one 16x16x128 operand half-fragment -- 16-B chunk 2*(lane>>4) + s of row
+// rbase + (lane&15) of a K-major [128 rows][128 B] image, i.e. the lane's 32 k-bytes
+// 32*(lane>>4) .. +31 split in two (s = 0, 1); the same swizzled image as bf16.
+__device__ __forceinline__ bf16x8 frag8(const char* half, int rbase, int s, int lane) {
+  const int r = rbase + (lane & 15);
+  const int lc = 2 * (lane >> 4) + s;
+  return *(const bf16x8*)(half + r * 128 + ((lc ^ swz_k<64>(r)) << 4));
+}
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x8 cat8(const bf16x8& lo, const bf16x8& hi) {
+  const i32x4 a = __builtin_bit_cast(i32x4, lo), b = __builtin_bit_cast(i32x4, hi);
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+// E8M0 scale bytes of 4 fragment rows row0 + 16*i + (lane & 15), i = 0..3, packed (byte i);
+// rows past `rows` take the last row's code (their data read as zero)
+__device__ __forceinline__ uint32_t scale_word(const uint8_t* sc, int row0, int rows, int lane) {
+  uint32_t w = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = row0 + 16 * i + (lane & 15);
+    w |= (uint32_t)sc[r < rows ? r : rows - 1] << (8 * i);
+  }
+  return w;
+}
+
 __device__ __forceinline__ void pin(const Raw8<bf16>& r) { asm volatile("" ::"v"(r.v)); }
 __device__ __forceinline__ void pin(const Raw8<float>& r) { asm volatile("" ::"v"(r.a), "v"(r.b)); }
 
-template <bool AK, bool BK, typename OutT>
-__global__ __launch_bounds__(512) void gemm8p_kernel(const bf16* __restrict__ A, int64_t lda,
-                                                     const bf16* __restrict__ B, int64_t ldb, int M, int N, int K,
-                                                     int splits, Epi e, float* __restrict__ ws) {
+template <bool AK, bool BK, typename OutT, bool F8 = false>
+__global__ __launch_bounds__(512) void gemm8p_kernel(const void* __restrict__ A, int64_t lda,
+                                                     const void* __restrict__ B, int64_t ldb, int M, int N, int K,
+                                                     int splits, Epi e, float* __restrict__ ws,
+                                                     const uint8_t* __restrict__ scA, const uint8_t* __restrict__ scB) {
+  static_assert(!F8 || (AK && BK), "fp8 operands are K-major");
+  constexpr int ESZ = F8 ? 1 : 2, BKE = F8 ? 128 : 64;  // element bytes, K elements per K-tile
   constexpr int HALF = 128 * 64 * 2, STAGE = 4 * HALF;
   constexpr int EPI_LD = 256 + 4;
   constexpr int SMEM = (2 * STAGE > 128 * EPI_LD * 4) ? 2 * STAGE : 128 * EPI_LD * 4;
@@ -114,13 +143,13 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(const bf16* __restrict__ A,
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int split = wg / ntiles, tile = wg % ntiles;
   const int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 256;
-  const int nk_all = (K + 63) / 64;
+  const int nk_all = (K + BKE - 1) / BKE;
   const int kt_per = (nk_all + splits - 1) / splits;
   const int kt0 = split * kt_per;
   const int nk = max(0, min(nk_all, kt0 + kt_per) - kt0);
   // descriptor ranges: K-major operands end at row M (N); MN-major ones at k row K
-  const int bytesA = (int)((AK ? (int64_t)M * lda : (int64_t)K * lda) * 2);
-  const int bytesB = (int)((BK ? (int64_t)N * ldb : (int64_t)K * ldb) * 2);
+  const int bytesA = (int)((AK ? (int64_t)M * lda : (int64_t)K * lda) * ESZ);
+  const int bytesB = (int)((BK ? (int64_t)N * ldb : (int64_t)K * ldb) * ESZ);
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, bytesA, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, bytesB, 0x00020000);
   // per-lane offsets of this wave's two pieces in each half (k0 = 0); h: 0 = A0, 1 = A1,
@@ -128,10 +157,10 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(const bf16* __restrict__ A,
   uint32_t vo[4][2];
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
-    vo[0][p] = piece_voff<AK>(wave * 2 + p, lane, m0, M, lda);
-    vo[1][p] = piece_voff<AK>(wave * 2 + p, lane, m0 + 128, M, lda);
-    vo[2][p] = piece_voff<BK>(wave * 2 + p, lane, n0, N, ldb);
-    vo[3][p] = piece_voff<BK>(wave * 2 + p, lane, n0 + 128, N, ldb);
+    vo[0][p] = piece_voff<AK, ESZ>(wave * 2 + p, lane, m0, M, lda);
+    vo[1][p] = piece_voff<AK, ESZ>(wave * 2 + p, lane, m0 + 128, M, lda);
+    vo[2][p] = piece_voff<BK, ESZ>(wave * 2 + p, lane, n0, N, ldb);
+    vo[3][p] = piece_voff<BK, ESZ>(wave * 2 + p, lane, n0 + 128, N, ldb);
   }
   // byte step of one K-tile: 64 k along a K-major row, 64 k rows of an MN-major operand
   const uint32_t kstepA = AK ? 128u : (uint32_t)(64 * lda * 2);
@@ -198,14 +227,20 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(const bf16* __restrict__ A,
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) f[s][i] = frag<AK>(base, wm * 64 + i * 16, s, lane);
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (F8) f[s][i] = frag8(base, wm * 64 + i * 16, s, lane);
+        else f[s][i] = frag<AK>(base, wm * 64 + i * 16, s, lane);
+      }
   };
   auto readB = [&](bf16x8 (&f)[2][2], int t, int h) {
     const char* base = half(t, h);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) f[s][j] = frag<BK>(base, wn * 32 + j * 16, s, lane);
+      for (int j = 0; j < 2; ++j) {
+        if constexpr (F8) f[s][j] = frag8(base, wn * 32 + j * 16, s, lane);
+        else f[s][j] = frag<BK>(base, wn * 32 + j * 16, s, lane);
+      }
   };
   f32x4 acc[2][2][4][2];
 #pragma unroll
@@ -216,7 +251,18 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(const bf16* __restrict__ A,
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[a][b][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  auto mma = [&](const bf16x8 (&fa)[2][4], const bf16x8 (&fb)[2][2], f32x4 (&c)[4][2]) {
+  // fp8: E8M0 row scales of this wave's fragment rows, applied inside the scaled MFMA
+  // (byte i of sa[qm]: A rows qm*128 + wm*64 + 16i + (lane&15); byte 2qn+j of sb: B rows
+  // qn*128 + wn*32 + 16j + (lane&15))
+  uint32_t sa[2] = {0u, 0u}, sb = 0u;
+  if constexpr (F8) {
+    sa[0] = scale_word(scA, m0 + wm * 64, M, lane);
+    sa[1] = scale_word(scA, m0 + 128 + wm * 64, M, lane);
+    const uint32_t b0 = scale_word(scB, n0 + wn * 32, N, lane), b1 = scale_word(scB, n0 + 128 + wn * 32, N, lane);
+    sb = (b0 & 0xFFFFu) | (b1 << 16);
+  }
+  auto mma = [&](const bf16x8 (&fa)[2][4], const bf16x8 (&fb)[2][2], f32x4 (&c)[4][2], auto qmc, auto qnc) {
+    constexpr int QM = decltype(qmc)::value, QN = decltype(qnc)::value;
 #if !defined(CAPK_V_NOPRIO) && !defined(CAPK_V_STATICPRIO)
     __builtin_amdgcn_s_setprio(1);
 #endif
@@ -228,12 +274,22 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(const bf16* __restrict__ A,
 #pragma unroll
         for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(fa[s][i]), "v"(fb[s][j]));
 #else
+    if constexpr (F8) {
+      const int sA = (int)sa[QM], sB = (int)sb;
+#define F8MMA(I, J)                                                                                              \
+  c[I][J] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(cat8(fa[0][I], fa[1][I]), cat8(fb[0][J], fb[1][J]), \
+                                                             c[I][J], 0, 0, I, sA, 2 * QN + J, sB)
+      F8MMA(0, 0); F8MMA(0, 1); F8MMA(1, 0); F8MMA(1, 1);
+      F8MMA(2, 0); F8MMA(2, 1); F8MMA(3, 0); F8MMA(3, 1);
+#undef F8MMA
+    } else {
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+      for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s][i], fb[s][j], c[i][j], 0, 0, 0);
+          for (int j = 0; j < 2; ++j) c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s][i], fb[s][j], c[i][j], 0, 0, 0);
+    }
 #endif
 #if !defined(CAPK_V_NOPRIO) && !defined(CAPK_V_STATICPRIO)
     __builtin_amdgcn_s_setprio(0);
@@ -250,6 +306,8 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(const bf16* __restrict__ A,
     fence();
   };
 
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
   bf16x8 fa[2][4], fb0[2][2], fb1[2][2];
   // prologue: K-tiles 0 and 1 in the order the steady-state phases -3 .. -1 would issue
   // them (A0/B0/B1(0), A1(0), A0/B0/B1(1)), then wait for A0/B0/B1(0) (read in phase 0)
@@ -274,8 +332,8 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(const bf16* __restrict__ A,
     issue(ph);
     lds_done();
     bar();
-    mma(fa, fb0, acc[0][0]);
-    mma(fa, fb1, acc[0][1]);
+    mma(fa, fb0, acc[0][0], I0{}, I0{});
+    mma(fa, fb1, acc[0][1], I0{}, I1{});
     bar();
     // Q2: quadrants (1,1), (1,0).  L: read A1(u); wait A0/B0/B1(u+1) (phase 2u-1)
     readA(fa, u, 1);
@@ -283,8 +341,8 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(const bf16* __restrict__ A,
     issue(ph + 1);
     lds_done();
     bar();
-    mma(fa, fb1, acc[1][1]);
-    mma(fa, fb0, acc[1][0]);
+    mma(fa, fb1, acc[1][1], I1{}, I1{});
+    mma(fa, fb0, acc[1][0], I1{}, I0{});
     bar();
   }
 #if !defined(CAPK_V_NOSTAGGER)
@@ -351,8 +409,8 @@ int launch_gemm8p(bool a_kmajor, bool b_kmajor, bool out_f32, int grid, const vo
                      (b_kmajor ? (int64_t)N * ldb : (int64_t)K * ldb) * 2 < (1ll << 31),
                  "capk_gemm(bf16, 256x256): operand larger than 2 GiB");
 #define L8(AK, BKM, OT)                                                                                            \
-  hipLaunchKernelGGL((gemm8p_kernel<AK, BKM, OT>), dim3(grid), dim3(512), 0, st, (const bf16*)A, lda, (const bf16*)B, \
-                     ldb, M, N, K, splits, e, slab)
+  hipLaunchKernelGGL((gemm8p_kernel<AK, BKM, OT>), dim3(grid), dim3(512), 0, st, A, lda, B, ldb, M, N, K, splits, \
+                     e, slab, nullptr, nullptr)
 #define L8D(OT)                                  \
   if (a_kmajor && b_kmajor) L8(true, true, OT);   \
   else if (a_kmajor) L8(true, false, OT);         \
@@ -362,6 +420,21 @@ int launch_gemm8p(bool a_kmajor, bool b_kmajor, bool out_f32, int grid, const vo
 #undef L8D
 #undef L8
   CAPK_LAUNCH_CHECK("gemm8p_kernel");
+  return CAPK_OK;
+}
+
+int launch_gemm8p_f8(bool out_f32, int grid, const void* A, int64_t lda, const uint8_t* scA, const void* B,
+                     int64_t ldb, const uint8_t* scB, int M, int N, int K, int splits, const Epi& e, float* slab,
+                     hipStream_t st) {
+  CAPK_CHECK_ARG((int64_t)M * lda < (1ll << 31) && (int64_t)N * ldb < (1ll << 31),
+                 "capk_gemm_f8: operand larger than 2 GiB");
+  if (out_f32)
+    hipLaunchKernelGGL((gemm8p_kernel<true, true, float, true>), dim3(grid), dim3(512), 0, st, A, lda, B, ldb, M, N, K,
+                       splits, e, slab, scA, scB);
+  else
+    hipLaunchKernelGGL((gemm8p_kernel<true, true, bf16, true>), dim3(grid), dim3(512), 0, st, A, lda, B, ldb, M, N, K,
+                       splits, e, slab, scA, scB);
+  CAPK_LAUNCH_CHECK("gemm8p_kernel<f8>");
   return CAPK_OK;
 }
 

@@ -268,5 +268,9 @@ __device__ __forceinline__ void wait_vm() {
 // gemm8p.hip: launch the 256x256 phased kernel (grid = tiles * splits)
 int launch_gemm8p(bool a_kmajor, bool b_kmajor, bool out_f32, int grid, const void* A, int64_t lda, const void* B,
                   int64_t ldb, int M, int N, int K, int splits, const Epi& e, float* slab, hipStream_t st);
+// fp8 e4m3 x e4m3 (both K-major, K % 128 == 0) with per-row E8M0 scales (gemm8p.hip)
+int launch_gemm8p_f8(bool out_f32, int grid, const void* A, int64_t lda, const uint8_t* scA, const void* B,
+                     int64_t ldb, const uint8_t* scB, int M, int N, int K, int splits, const Epi& e, float* slab,
+                     hipStream_t st);
 
 }  // namespace capk

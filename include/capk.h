@@ -92,6 +92,30 @@ int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K,
               float drop_p, uint32_t drop_seed,
               void* ws, size_t ws_bytes, void* stream);
 
+/* ------------------------------------------------- fp8 (config 5) --------
+ * The forward Linear / Conv1D products of BASELINE config 5 ("fp8 MFMA") on OCP e4m3fn
+ * operands with one power-of-two scale per row, stored as its E8M0 code (2^(code-127)):
+ * the code format v_mfma_scale_f32_16x16x128_f8f6f4 applies per lane, so scaling costs
+ * nothing in the GEMM.  Replaces the fp16-autocast nn.Linear / Conv1D forward of the
+ * reference's CLIP (modeling_clip.py:273-276,322-325) and GPT-2 (modeling_gpt2.py:
+ * 267,281,559-561, pytorch_utils.Conv1D) under src/train/trainer.py:224-226 autocast.
+ *
+ * capk_quant_fp8: q = RNE_e4m3(x * 2^-e) per output row, e the smallest exponent with
+ *   amax(row) * 2^-e <= 448; scale[row] = e + 127 (0x7F for an all-zero row).
+ *   transpose = 0: x [rows][cols] (ldx >= cols, cols % 8 == 0);
+ *   transpose = 1: x [cols][rows] (ldx >= rows; a Conv1D weight [in][out]), q [rows][cols].
+ *   q [rows][ldq] bytes, ldq % 8 == 0 (rows) / % 16 == 0 (transpose).  in_dtype CAPK_F32 or CAPK_BF16.
+ * capk_gemm_f8: C[M,N] = epilogue(sum_k A[m,k] 2^sa[m] * B[n,k] 2^sb[n]) with fp32
+ *   accumulation; A [M][lda], B [N][ldb] e4m3fn K-major, K % 128 == 0; same epilogue
+ *   arguments and meaning as capk_gemm (forward activations only). */
+int capk_quant_fp8(int in_dtype, int rows, int cols, const void* x, int64_t ldx, int transpose,
+                   void* q, int64_t ldq, void* scale, void* stream);
+size_t capk_gemm_f8_workspace(int M, int N, int K);
+int capk_gemm_f8(int out_dtype, int M, int N, int K, const void* A, int64_t lda, const void* a_scale,
+                 const void* B, int64_t ldb, const void* b_scale, void* C, int64_t ldc, float beta,
+                 const float* bias, const void* residual, int64_t ldr, int act, void* preact, int64_t ldx,
+                 float drop_p, uint32_t drop_seed, void* ws, size_t ws_bytes, void* stream);
+
 /* -------------------------------------------------------- LayerNorm -------
  * y = (x - mean) * rstd * w + b over the last `cols` elements of each row;
  * mean/rstd (fp32, [rows]) saved for backward.  LN eps 1e-12 (ViT), 1e-5

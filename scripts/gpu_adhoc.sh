@@ -1,9 +1,8 @@
 set -u
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -rf --timeout 240 --timeout-method thread > gpurun_out/tests.log 2>&1
-rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/tests.log
-[ $rc -le 1 ] || exit $rc
-timeout -k 10 400 python bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/bench.log 2>&1
-rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench.log | cut -c1-400
+timeout -k 10 300 python -u -m pytest tests/test_gpu_fp8.py -x -v -rf --timeout 120 --timeout-method thread > gpurun_out/fp8_tests.log 2>&1
+rc=$?; echo "fp8 tests rc=$rc"; tail -5 gpurun_out/fp8_tests.log
 [ $rc -eq 0 ] || exit $rc
-PROF_TAG=prof_r2 PROF_SECS=300 PROF_CMD="bench.py --steps 3 --warmup 2 --no-cpu-baseline --beam-batch 0" bash scripts/gpu_profile.sh
+GEMM_ONLY=f8_clip_qkv,f8_clip_fc1,f8_clip_fc2,f8_gpt2_fc1,f8_lm_head,f8_lm_head_beam5,f8_big,bf16_big,f8_quant_x,vit_qkv_fwd,lm_head_fwd \
+  timeout -k 10 300 python -u tools/gemm_bench.py > gpurun_out/gemm_f8.log 2>&1
+rc=$?; echo "gemm rc=$rc"; cat gpurun_out/gemm_f8.log

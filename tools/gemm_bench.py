@@ -23,13 +23,29 @@ SHAPES = [  # name, M, N, K, kind
     ("vit_fc1_fwd_bias_res", T, 3072, 768, "fwd_res"),
     # the model's forms: GELU with CAPK_ACT_DERIV (kept act'(pre); backward multiplies by it)
     ("vit_fc1_fwd_gelu_deriv", T, 3072, 768, "fwd_gelu_deriv"), ("vit_fc2_dx_gelu_deriv", T, 3072, 768, "dx_gelu_deriv"),
+    # config 5 (fp8 forward): CLIP-B/32 rows 256*50, GPT-2 rows 256*20, decode LM heads
+    ("f8_clip_qkv", 12800, 2304, 768, "f8"), ("f8_clip_fc1", 12800, 3072, 768, "f8"),
+    ("f8_clip_fc2", 12800, 768, 3072, "f8"), ("f8_gpt2_fc1", 5120, 3072, 768, "f8"),
+    ("f8_lm_head", 5120, 50304, 768, "f8"), ("f8_lm_head_beam5", 1280, 50304, 768, "f8"),
+    ("f8_big", 16384, 16384, 8192, "f8"), ("bf16_big", 16384, 16384, 8192, "fwd"),
+    ("f8_quant_x", 12800, 3072, 768, "quant"),
 ]
 
 
 def run(name, M, N, K, kind, iters=20):
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(0)
-    if kind.startswith("fwd"):
+    if kind == "f8":
+        qa, sa = ops.quant_fp8(torch.randn(M, K, device=dev, generator=g).bfloat16())
+        qb, sb = ops.quant_fp8(torch.randn(N, K, device=dev, generator=g) * 0.02)
+        C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        fn = lambda: ops.gemm_f8(qa, sa, qb, sb, C)
+    elif kind == "quant":  # activation quantisation alone: [M, N] bf16 -> fp8
+        x = torch.randn(M, N, device=dev, generator=g).bfloat16()
+        q = torch.empty(M, N, device=dev, dtype=torch.uint8)
+        sc = torch.empty(M, device=dev, dtype=torch.uint8)
+        fn = lambda: ops.quant_fp8(x, q=q, scale=sc)
+    elif kind.startswith("fwd"):
         x = torch.randn(M, K, device=dev, generator=g).bfloat16()
         w = (torch.randn(N, K, device=dev, generator=g) * 0.02).bfloat16()
         b = torch.zeros(N, device=dev)
@@ -59,6 +75,10 @@ def run(name, M, N, K, kind, iters=20):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / iters
     tf = 2.0 * M * N * K / (ms * 1e-3) / 1e12
+    if kind == "quant":
+        print(f"{name:18s} M={M:6d} N={N:6d}  {ms * 1e3:8.1f} us  {3.0 * M * N / (ms * 1e-3) / 1e9:7.1f} GB/s",
+              flush=True)
+        return 0.0
     print(f"{name:18s} M={M:6d} N={N:6d} K={K:6d}  {ms * 1e3:8.1f} us  {tf:7.1f} TFLOP/s", flush=True)
     return tf
 
