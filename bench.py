@@ -25,6 +25,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
+PEAK_FP8_TFLOPS = 5000.0   # MI355X dense fp8 MFMA (same table; the 2:1-sparse figure is never used)
 FLOP_PER_IMAGE = 120.7e9  # config-3 fwd+bwd algorithmic FLOPs per image
 FLOP_PER_CAPTION = 54e9   # beam-5 caption (ViT fwd + memory K/V + 19 KV-cached steps x 5 beams)
 
@@ -184,6 +185,135 @@ def throughput(per_rank_batch, world, steps, elapsed):
     return per_rank_batch * world * steps / elapsed
 
 
+# ------------------------------------------------------------------ config 5 ----
+def flops_config5(max_length=20, enc_tokens=50, d=768, layers=12, ff=3072, vocab=50304, beams=4, patch_k=3072):
+    """Algorithmic GEMM FLOPs per image of one config-5 SCST update (dense products only):
+    CLIP-B/32 forward + backward, GPT-2 sampling (KV-cached, max_length-1 steps), beam-4
+    baseline, teacher-forced GPT-2 forward + backward over the sampled caption."""
+    per_tok = 2 * d * (3 * d + d + 2 * ff) * layers  # QKV, O, FC1, FC2 of every block
+    clip_fwd = enc_tokens * per_tok + 2 * (enc_tokens - 1) * patch_k * d
+    steps = max_length - 1
+    dec_tok = per_tok + 2 * d * vocab  # one GPT-2 position incl. the LM head
+    sample = steps * dec_tok
+    baseline = beams * steps * dec_tok
+    tf_fwd = max_length * dec_tok
+    return 3 * clip_fwd + sample + baseline + 3 * tf_fwd
+
+
+def build_config5(device, precision="fp8"):
+    """BASELINE configs[4]: CLIP-ViT-B/32 + GPT-2 (+ AoA attention config, unused by the
+    GPT-2 decoder as in the reference) with SCST; fp8 forward products (capk.prepare 'fp8')."""
+    import capk
+    from capk import config as C
+    from capk.models import captioning_model as cm
+    from capk.train import CapkAdamW
+    torch.manual_seed(42)
+    cfg = C.Config()
+    cfg.model.encoder = C.EncoderConfig(encoder_type="clip", pretrained_model_name="openai/clip-vit-base-patch32")
+    cfg.model.decoder = C.DecoderConfig(decoder_type="gpt2", pretrained_model_name="gpt2")
+    cfg.model.attention = C.AttentionConfig(attention_type="aoa")
+    cfg.model.vocab_size, cfg.model.pad_token_id = 50257, 50256
+    cfg.model.bos_token_id = cfg.model.eos_token_id = 50256
+    model = cm.ImageCaptioningModel(cfg)
+    cpu_sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    store = capk.prepare(model, device, precision)
+    opt = CapkAdamW(store, lr=cfg.training.learning_rate, weight_decay=cfg.training.weight_decay)
+    return cfg, model, store, opt, cpu_sd
+
+
+def run_config5(args, world, rank, device):
+    """One step = one SCST update at bs=args.batch per GPU (capk.train.scst.scst_step:
+    CLIP forward, 19-step sampling, GPT-2 beam-4 baseline, host CIDEr-D rewards,
+    teacher-forced forward + backward, DP gradient all-reduce, AdamW); then beam-5
+    captions/s.  Random-init GPT-2 never emits EOS: every decode runs all 19 steps."""
+    from capk import ops
+    from capk.train.dp import GradBucketer
+    from capk.train.scst import scst_step
+    cfg, model, store, opt, cpu_sd = build_config5(device, args.precision)
+    B = args.batch
+    g = torch.Generator(device=device).manual_seed(5 + 1000 * rank)
+    images = torch.randn(B, 3, 224, 224, device=device, generator=g)
+    gh = torch.Generator().manual_seed(6 + 1000 * rank)
+    refs = [[torch.randint(0, 50256, (int(torch.randint(8, 17, (1,), generator=gh)),), generator=gh).tolist()
+             for _ in range(5)] for _ in range(B)]
+    bucketer = GradBucketer(store, exchange=args.grad_exchange) if world > 1 else None
+    model.train()
+    upd = [0]
+    last = [None]
+
+    def step():
+        last[0] = scst_step(model, images, refs, opt, lr=cfg.training.learning_rate, seed=0x5C57 + upd[0],
+                            max_length=20, baseline_kwargs={"num_beams": 4}, bucketer=bucketer)
+        upd[0] += 1
+
+    for _ in range(args.warmup):
+        step()
+    ops.GEMM_TIMER.start()
+    elapsed = timed_steps(step, args.steps, 0, world, torch.cuda.synchronize, device)
+    ops.GEMM_TIMER.stop()
+    gem = ops.GEMM_TIMER.summary()
+    beam = None
+    if args.beam_batch > 0:
+        bdt, bgem, blen = beam_bench(model, args.beam_batch, args.beam_reps, device, rank)
+        if world > 1:
+            t = torch.tensor([bdt], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            bdt = float(t)
+        beam = (bdt, bgem, blen)
+    if rank != 0:
+        return None
+    ms = elapsed / args.steps * 1e3
+    value = throughput(B, world, args.steps, elapsed)
+    f8 = gem["by_route"]["gemm_f8"]
+    bf = gem["by_route"]["gemm_bf16_kernel"]
+    fpi = flops_config5()
+    loss, rs, rb = last[0]
+    rec = {
+        "metric": "images/sec SCST train (CLIP-ViT + GPT-2, --use_rl) + beam-5 captions/sec, fp8 MFMA",
+        "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp8" if args.precision == "fp8" else args.precision,
+        "data": "synthetic (randn 224x224x3 images, 5 random reference captions of 8-16 tokens per image), "
+                "random-init weights",
+        "config": {"workload": "config 5: CLIP-ViT-B/32 + GPT-2 + aoa, SCST update (sample 19 steps + beam-4 "
+                               "baseline + CIDEr-D + teacher-forced fwd/bwd + AdamW)",
+                   "global_batch": B * world, "per_gpu_batch": B, "seq_len": 20, "image_tokens": 50, "vocab": 50257,
+                   "parallelism": f"dp{world}", "precision": args.precision,
+                   "grad_exchange": args.grad_exchange if world > 1 else None},
+        "roofline": {"bound": "mfma", "kernel": "fp8 GEMM (gemm8p F8: v_mfma_scale_f32_16x16x128_f8f6f4), every "
+                                                "capk_gemm_f8 launch in the timed steps",
+                     "achieved": round(f8["tflops"], 1), "peak": PEAK_FP8_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(f8["tflops"] / PEAK_FP8_TFLOPS, 4), "traffic": None,
+                     "traffic_source": "not collected for config 5",
+                     "launches": f8["launches"], "ms": round(f8["total_ms"], 2),
+                     "bf16_gemm": {"launches": bf["launches"], "ms": round(bf["total_ms"], 2),
+                                   "tflops": round(bf["tflops"], 1), "frac_of_bf16_peak": round(bf["tflops"] / PEAK_BF16_TFLOPS, 4)},
+                     "gemm_share_of_step": round(gem["total_ms"] / (elapsed * 1e3), 3)},
+        "model_flops": {"per_image": fpi, "tflops": round(fpi * value / world / 1e12, 1)},
+        "final_loss": round(float(loss), 5), "reward_sample": round(rs, 4), "reward_baseline": round(rb, 4),
+    }
+    if beam is not None:
+        bdt, bgem, blen = beam
+        cps = args.beam_batch * world * args.beam_reps / bdt
+        rec["beam5"] = {"metric": "beam-5 captions/sec", "value": round(cps, 2), "unit": "captions/s",
+                        "per_gpu_batch": args.beam_batch, "reps": args.beam_reps,
+                        "ms_per_batch": round(bdt / args.beam_reps * 1e3, 3), "num_beams": 5, "max_length": 20,
+                        "output_length": blen, "dtype": rec["dtype"],
+                        "workload": "CLIP-ViT-B/32 fwd + KV-cached GPT-2 beam-5 decode (HF semantics)",
+                        "gemm": {k: {"launches": v["launches"], "ms": round(v["total_ms"], 2),
+                                     "tflops": round(v["tflops"], 1)} for k, v in bgem["by_route"].items()}}
+    if world == 1 and not args.no_cpu_baseline:
+        from oracle.step import time_cpu_scst
+        threads, hinfo = host_cpus()
+        ips, dt = time_cpu_scst(cpu_sd, images=args.cpu_batch_scst, threads=threads)
+        rec["cpu_baseline"] = {"value": round(ips, 4), "unit": "images/s", "cores": threads, "kind": "port",
+                               "host": hinfo,
+                               "sample": f"oracle fp32 CPU SCST update (CLIP fwd/bwd, sampling and beam-4 re-running "
+                                         f"GPT-2 on each prefix, CIDEr-D, AdamW), {args.cpu_batch_scst} images "
+                                         f"({dt:.1f} s)"}
+    return rec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -198,11 +328,22 @@ def main():
     ap.add_argument("--cpu-beam-images", type=int, default=24)
     ap.add_argument("--grad-exchange", choices=["fp32", "bf16"], default="bf16",
                     help="DP gradient all-reduce precision (fp32 master weights either way)")
+    ap.add_argument("--workload", choices=["config3", "config5"], default="config3",
+                    help="config3 (headline: ViT+Transformer CE) or config5 (CLIP+GPT-2 SCST, fp8)")
+    ap.add_argument("--precision", choices=["fp8", "bf16"], default="fp8", help="config5 forward precision")
+    ap.add_argument("--cpu-batch-scst", type=int, default=4)
     args = ap.parse_args()
 
     world, rank, local = dist_init("nccl")
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
+    if args.workload == "config5":
+        rec = run_config5(args, world, rank, device)
+        if rank == 0:
+            print(json.dumps(rec), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     from capk import ops
     from capk.train.dp import GradBucketer

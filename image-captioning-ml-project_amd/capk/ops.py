@@ -157,8 +157,11 @@ def quant_fp8(x, *, transpose=False, q=None, scale=None):
         q = torch.empty(rows, cols, dtype=torch.uint8, device=x.device)
     if scale is None:
         scale = torch.empty(rows, dtype=torch.uint8, device=x.device)
-    check(lib().capk_quant_fp8(dtype_code(x), rows, cols, _p(x), x.stride(0), int(transpose), _p(q), q.stride(0),
-                               _p(scale), _stream()), "capk_quant_fp8")
+    L = lib()
+    wsb = L.capk_quant_fp8_workspace(rows, cols, int(transpose))
+    ws = _ws(wsb, x.device)
+    check(L.capk_quant_fp8(dtype_code(x), rows, cols, _p(x), x.stride(0), int(transpose), _p(q), q.stride(0),
+                           _p(scale), _p(ws), wsb, _stream()), "capk_quant_fp8")
     return q, scale
 
 

@@ -53,6 +53,25 @@ __device__ __forceinline__ bool full_kb(const AttnArgs& a, int kb) {
 }
 constexpr float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
 
+// Compile-time launch modes of the bf16 kernels: MODE bit 0 = probability dropout, bit 1 =
+// causal / key-padding masks.  The common ViT / cross-attention launch (mode 0) has no
+// per-score branches: only the last key block is tested, against Nk.
+constexpr int AM_DROP = 1, AM_MASK = 2;
+template <int MODE>
+__device__ __forceinline__ bool kok(const AttnArgs& a, int b, int key, int q) {
+  if constexpr (MODE & AM_MASK) return key_ok(a, b, key, q);
+  else return key < a.Nk;
+}
+template <int MODE>
+__device__ __forceinline__ bool fullk(const AttnArgs& a, int kb) {
+  if constexpr (MODE & AM_MASK) return full_kb(a, kb);
+  else return (kb + 1) * 16 <= a.Nk;
+}
+template <int MODE>
+constexpr bool dropm() { return (MODE & AM_DROP) != 0; }
+// v_exp_f32 directly: arguments are <= 0 or -inf (-> 0); no denormal range reduction
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ bf16x8 ld8(const bf16* p) { return *(const bf16x8*)p; }
 __device__ __forceinline__ bf16x8 zero8() {
   bf16x8 z;
@@ -88,6 +107,29 @@ __device__ __forceinline__ bf16x8 tr_read8(const bf16* img, int st, int r0, int 
   return r;
 }
 
+// Swizzled head image (forward kernel, HDP 64): unpadded 128-B rows, 16-B chunk c of row r
+// stored at chunk c ^ ((r >> 1) & 7) -- conflict-free for the 16-row b128 fragment reads and
+// the 4-row transposed reads (the GEMM's K-major swizzle), and 12 % less LDS than 8-element
+// padding: with 16-row granularity a ViT head's K/V take 52 KiB, three workgroups per CU.
+__device__ __forceinline__ int swz_off(int r, int col) {
+  return r * 64 + ((((col >> 3) ^ ((r >> 1) & 7))) << 3) + (col & 7);
+}
+__device__ __forceinline__ bf16x4 tr_read_sw(const bf16* img, int r0, int c0, int lane) {
+  const int i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, img + swz_off(r0 + q, c0 + 4 * p)));
+}
+// tr_read8 on a swizzled image; hi = false: the upper 16 rows lie past the image (zeros)
+__device__ __forceinline__ bf16x8 tr_read8_sw(const bf16* img, int r0, int c0, int lane, bool hi) {
+  const int g = lane >> 4;
+  bf16x4 x0 = tr_read_sw(img, r0 + 4 * g, c0, lane);
+  bf16x4 x1 = {(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+  if (hi) x1 = tr_read_sw(img, r0 + 16 + 4 * g, c0, lane);
+  bf16x8 r;
+  r[0] = x0[0]; r[1] = x0[1]; r[2] = x0[2]; r[3] = x0[3];
+  r[4] = x1[0]; r[5] = x1[1]; r[6] = x1[2]; r[7] = x1[3];
+  return r;
+}
+
 // Stage up to NIMG row-major [NP x HDP] head images into LDS (row stride HDP+8).
 // Every global load of every image is issued before the first LDS write, so a
 // workgroup pays one memory round trip for its whole staging, not one per chunk.
@@ -97,8 +139,9 @@ struct StageSrc {
   int64_t rs;
   int n, NP;
 };
-template <int HDP, int NIMG, int MINTHR>
+template <int HDP, int NIMG, int MINTHR, bool SWZ = false>
 __device__ __forceinline__ void stage_images(const StageSrc (&S)[NIMG], int hd) {
+  static_assert(!SWZ || HDP == 64, "swizzled images are 64 wide");
   constexpr int NCH = HDP / 8;
   constexpr int ST = HDP + 8;
   constexpr int MAXIT = (256 * NCH + MINTHR - 1) / MINTHR;  // NP <= 256
@@ -117,8 +160,37 @@ __device__ __forceinline__ void stage_images(const StageSrc (&S)[NIMG], int hd) 
     for (int it = 0; it < MAXIT; ++it) {
       const int c = threadIdx.x + it * blockDim.x;
       const int r = c / NCH, dc = c % NCH;
-      if (r < S[im].NP) *(bf16x8*)(S[im].img + r * ST + dc * 8) = v[im][it];
+      if (r < S[im].NP) *(bf16x8*)(S[im].img + (SWZ ? swz_off(r, dc * 8) : r * ST + dc * 8)) = v[im][it];
     }
+}
+
+// stage_images for any blockDim: rounds of R 16-B chunks per image per thread (all loads
+// of a round issued before its LDS writes).
+template <int HDP, int NIMG, bool SWZ>
+__device__ __forceinline__ void stage_images_rt(const StageSrc (&S)[NIMG], int hd) {
+  constexpr int NCH = HDP / 8, ST = HDP + 8, R = 4;
+  int total = 0;
+#pragma unroll
+  for (int im = 0; im < NIMG; ++im) total = max(total, S[im].NP * NCH);
+  for (int base = 0; base < total; base += R * (int)blockDim.x) {
+    bf16x8 v[NIMG][R];
+#pragma unroll
+    for (int im = 0; im < NIMG; ++im)
+#pragma unroll
+      for (int it = 0; it < R; ++it) {
+        const int c = base + threadIdx.x + it * blockDim.x;
+        const int r = c / NCH, dc = c % NCH;
+        v[im][it] = (r < S[im].n && dc * 8 < hd) ? ld8(S[im].src + (int64_t)r * S[im].rs + dc * 8) : zero8();
+      }
+#pragma unroll
+    for (int im = 0; im < NIMG; ++im)
+#pragma unroll
+      for (int it = 0; it < R; ++it) {
+        const int c = base + threadIdx.x + it * blockDim.x;
+        const int r = c / NCH, dc = c % NCH;
+        if (r < S[im].NP) *(bf16x8*)(S[im].img + (SWZ ? swz_off(r, dc * 8) : r * ST + dc * 8)) = v[im][it];
+      }
+  }
 }
 
 template <int HDP>
@@ -131,13 +203,19 @@ __device__ __forceinline__ void load_q_frags(const AttnArgs& a, const bf16* qsrc
   }
 }
 
-template <int HDP>
-__global__ __launch_bounds__(512) void attn_fwd_bf16(AttnArgs a) {
+// 8 waves over the 16-query tiles; HDP 64 is held to 80 VGPRs so that three workgroups
+// (52 KiB of swizzled K/V each) share a CU.  (Measured: one wave per tile -- 13-wave
+// workgroups, two per CU -- 130 us vs 101 us on the ViT layer: fewer, longer-staging
+// workgroups overlap less.)
+template <int HDP, int MODE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HDP == 64 ? 6 : 1))) void attn_fwd_bf16(
+    AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
-  const int NKP = (a.Nk + 31) & ~31;
-  constexpr int ST = HDP + 8;
+  constexpr bool SW = HDP == 64;  // swizzled 16-row-granular images (swz_off)
+  const int NKP = SW ? (a.Nk + 15) & ~15 : (a.Nk + 31) & ~31;
+  constexpr int ST = SW ? 64 : HDP + 8;
   bf16* Ks = (bf16*)smem;
   bf16* Vs = Ks + NKP * ST;
   const int hoff = h * a.hd;
@@ -148,7 +226,7 @@ __global__ __launch_bounds__(512) void attn_fwd_bf16(AttnArgs a) {
   {
     const StageSrc S[2] = {{Ks, (const bf16*)a.k + (int64_t)b * a.k_bs + hoff, a.k_rs, a.Nk, NKP},
                            {Vs, (const bf16*)a.v + (int64_t)b * a.v_bs + hoff, a.v_rs, a.Nk, NKP}};
-    stage_images<HDP, 2, 512>(S, a.hd);
+    stage_images_rt<HDP, 2, SW>(S, a.hd);
   }
   __syncthreads();
 
@@ -159,52 +237,67 @@ __global__ __launch_bounds__(512) void attn_fwd_bf16(AttnArgs a) {
   for (int qt = wave; qt * 16 < a.Nq; qt += nwaves) {
     if (qt != wave) load_q_frags<HDP>(a, qsrc, qt, lane, qf);
     const int qi = qt * 16 + (lane & 15);
-    float m = -INFINITY, l = 0.f;  // running max (per query, reduced over the lane group), lane-partial sum
+    // m: the reference maximum of the query's raw scores (reduced over the lane group); the
+    // exponent base is m*sl2.  Lazy rescale: the reference only moves when a chunk's max
+    // exceeds it by more than 2^8 in p (wave-uniform test), otherwise p <= 256 is kept
+    // against the old reference -- same O / LSE, no o *= alpha on most chunks.
+    float m = -INFINITY, l = 0.f;
+    float mref = 0.f;  // m * sl2 (0 while nothing is unmasked: p = 0, no NaN)
     f32x4 o[HDP / 16];
 #pragma unroll
     for (int db = 0; db < HDP / 16; ++db) o[db] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    for (int t = 0; t < NKP / 32; ++t) {
+    for (int t = 0; t * 32 < NKP; ++t) {
       f32x4 sc[2];
       float cm = -INFINITY;
+      const bool hi = (2 * t + 1) * 16 < NKP;  // the chunk's upper 16 keys are staged
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int kb = 2 * t + c;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        if (c == 0 || hi) {
 #pragma unroll
-        for (int s = 0; s < HDP / 32; ++s) {
-          bf16x8 kf = *(const bf16x8*)(Ks + (kb * 16 + (lane & 15)) * ST + s * 32 + 8 * (lane >> 4));
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s], acc, 0, 0, 0);
+          for (int s = 0; s < HDP / 32; ++s) {
+            const int row = kb * 16 + (lane & 15), col = s * 32 + 8 * (lane >> 4);
+            bf16x8 kf = *(const bf16x8*)(Ks + (SW ? swz_off(row, col) : row * ST + col));
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s], acc, 0, 0, 0);
+          }
         }
-        const bool full = full_kb(a, kb);
+        if (!fullk<MODE>(a, kb)) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = kb * 16 + (lane >> 4) * 4 + r;
-          acc[r] = (full || key_ok(a, b, key, qi)) ? acc[r] * sl2 : -INFINITY;
-          cm = fmaxf(cm, acc[r]);
+          for (int r = 0; r < 4; ++r) {
+            const int key = kb * 16 + (lane >> 4) * 4 + r;
+            acc[r] = kok<MODE>(a, b, key, qi) ? acc[r] : -INFINITY;
+          }
         }
+        cm = fmaxf(fmaxf(cm, fmaxf(acc[0], acc[1])), fmaxf(acc[2], acc[3]));
         sc[c] = acc;
       }
       cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
       cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
-      const float mn = fmaxf(m, cm);
-      const float mref = mn == -INFINITY ? 0.f : mn;  // nothing unmasked yet: p = 0, no NaN
-      const float alpha = exp2f(m - mref);
-      m = mn;
-      l *= alpha;
+      const bool move = cm > m && (m == -INFINITY || (cm - m) * sl2 > 8.f);
+      if (__builtin_amdgcn_ballot_w64(move)) {
+        const float mn = move ? cm : m;
+        const float nref = mn == -INFINITY ? 0.f : mn * sl2;
+        const float alpha = move ? fexp2(mref - nref) : 1.f;
+        m = mn;
+        mref = nref;
+        l *= alpha;
 #pragma unroll
-      for (int db = 0; db < HDP / 16; ++db) o[db] *= alpha;
+        for (int db = 0; db < HDP / 16; ++db) o[db] *= alpha;
+      }
 #pragma unroll
       for (int c = 0; c < 2; ++c)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(sc[c][r] - mref);
+          const float p = fexp2(fmaf(sc[c][r], sl2, -mref));
           l += p;  // the normaliser excludes dropout
-          sc[c][r] = a.drop.on() ? p * pdrop(a, b, h, qi, (2 * t + c) * 16 + (lane >> 4) * 4 + r) : p;
+          sc[c][r] = dropm<MODE>() ? p * pdrop(a, b, h, qi, (2 * t + c) * 16 + (lane >> 4) * 4 + r) : p;
         }
       const bf16x8 pb = pack8(sc[0], sc[1]);
 #pragma unroll
       for (int db = 0; db < HDP / 16; ++db)  // O^T += V^T P^T, V^T fragments by transposed LDS reads
-        o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_read8(Vs, ST, 32 * t, db * 16, lane), pb, o[db], 0, 0, 0);
+        o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            SW ? tr_read8_sw(Vs, 32 * t, db * 16, lane, hi) : tr_read8(Vs, ST, 32 * t, db * 16, lane), pb, o[db], 0, 0, 0);
     }
     l += __shfl_xor(l, 16, 64);
     l += __shfl_xor(l, 32, 64);
@@ -216,12 +309,12 @@ __global__ __launch_bounds__(512) void attn_fwd_bf16(AttnArgs a) {
         const int d0 = db * 16 + (lane >> 4) * 4;
         if (d0 < a.hd) store4(orow + d0, o[db], inv);
       }
-      if ((lane >> 4) == 0) a.lse[((int64_t)b * a.H + h) * a.Nq + qi] = (m + __log2f(l)) * kLn2;
+      if ((lane >> 4) == 0) a.lse[((int64_t)b * a.H + h) * a.Nq + qi] = (mref + __log2f(l)) * kLn2;
     }
   }
 }
 
-template <int HDP>
+template <int HDP, int MODE>
 __global__ __launch_bounds__(512) void attn_bwd_bf16(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
@@ -293,9 +386,9 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16(AttnArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int q = t * 32 + c * 16 + (lane >> 4) * 4 + r;
-          const bool ok = q < a.Nq && (full_kb(a, kb) || key_ok(a, b, keyl, q));
-          const float pv = ok ? exp2f(s_acc[r] * sl2 - lse_s[q]) : 0.f;
-          const float mk = a.drop.on() && q < a.Nq ? pdrop(a, b, h, q, keyl) : 1.f;
+          const bool ok = q < a.Nq && (fullk<MODE>(a, kb) || kok<MODE>(a, b, keyl, q));
+          const float pv = ok ? fexp2(s_acc[r] * sl2 - lse_s[q]) : 0.f;
+          const float mk = dropm<MODE>() && q < a.Nq ? pdrop(a, b, h, q, keyl) : 1.f;
           p[c][r] = pv * mk;
           ds[c][r] = pv * (dp_acc[r] * mk - del_s[q]);
         }
@@ -345,9 +438,9 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16(AttnArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = t * 32 + c * 16 + (lane >> 4) * 4 + r;
-          const bool ok = ql < a.Nq && (full_kb(a, 2 * t + c) || key_ok(a, b, key, ql));
-          const float pv = ok ? exp2f(s_acc[r] * sl2 - lq) : 0.f;
-          const float mk = a.drop.on() && ok ? pdrop(a, b, h, ql, key) : 1.f;
+          const bool ok = ql < a.Nq && (fullk<MODE>(a, 2 * t + c) || kok<MODE>(a, b, key, ql));
+          const float pv = ok ? fexp2(s_acc[r] * sl2 - lq) : 0.f;
+          const float mk = dropm<MODE>() && ok ? pdrop(a, b, h, ql, key) : 1.f;
           ds[c][r] = pv * (dp_acc[r] * mk - dq_del);
         }
       }
@@ -372,7 +465,7 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16(AttnArgs a) {
 // in registers; dQ with K, V staged and the wave's own Q/dO rows in registers.  Same
 // arithmetic as attn_bwd_bf16 phases A and B (which remains for reference shapes that
 // do not fit this split's launch checks).
-template <int HDP, int WPE>
+template <int HDP, int WPE, int MODE>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void attn_bwd_kv_bf16(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
@@ -443,9 +536,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int q = t * 32 + c * 16 + (lane >> 4) * 4 + r;
-          const bool ok = q < a.Nq && (full_kb(a, kb) || key_ok(a, b, keyl, q));
-          const float pv = ok ? exp2f(s_acc[r] * sl2 - lse_s[q]) : 0.f;
-          const float mk = a.drop.on() && q < a.Nq ? pdrop(a, b, h, q, keyl) : 1.f;
+          const bool ok = q < a.Nq && (fullk<MODE>(a, kb) || kok<MODE>(a, b, keyl, q));
+          const float pv = ok ? fexp2(s_acc[r] * sl2 - lse_s[q]) : 0.f;
+          const float mk = dropm<MODE>() && q < a.Nq ? pdrop(a, b, h, q, keyl) : 1.f;
           p[c][r] = pv * mk;
           ds[c][r] = pv * (dp_acc[r] * mk - del_s[q]);
         }
@@ -472,7 +565,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
 }
 
-template <int HDP>
+template <int HDP, int MODE>
 __global__ __launch_bounds__(512) void attn_bwd_q_bf16(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
@@ -527,9 +620,9 @@ __global__ __launch_bounds__(512) void attn_bwd_q_bf16(AttnArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = t * 32 + c * 16 + (lane >> 4) * 4 + r;
-          const bool ok = ql < a.Nq && (full_kb(a, 2 * t + c) || key_ok(a, b, key, ql));
-          const float pv = ok ? exp2f(s_acc[r] * sl2 - lq) : 0.f;
-          const float mk = a.drop.on() && ok ? pdrop(a, b, h, ql, key) : 1.f;
+          const bool ok = ql < a.Nq && (fullk<MODE>(a, 2 * t + c) || kok<MODE>(a, b, key, ql));
+          const float pv = ok ? fexp2(s_acc[r] * sl2 - lq) : 0.f;
+          const float mk = dropm<MODE>() && ok ? pdrop(a, b, h, ql, key) : 1.f;
           ds[c][r] = pv * (dp_acc[r] * mk - dd);
         }
       }
@@ -664,6 +757,11 @@ __global__ __launch_bounds__(64) void attn_bwd_dkv_f32(AttnArgs a) {
 static size_t fwd_smem(int Nk, int hdp) {
   const int NKP = (Nk + 31) & ~31;
   return (size_t)2 * NKP * (hdp + 8) * 2;
+}
+// attn_fwd_bf16: hdp 64 uses swizzled unpadded images at 16-row granularity
+static size_t fwd_kernel_smem(int Nk, int hdp) {
+  if (hdp != 64) return fwd_smem(Nk, hdp);
+  return (size_t)2 * ((Nk + 15) & ~15) * 64 * 2;
 }
 static size_t bwd_kv_smem(int Nq, int hdp) {
   const int NQP = (Nq + 31) & ~31;
@@ -875,14 +973,23 @@ extern "C" int capk_attention_fwd(int dtype, int B, int H, int Nq, int Nk, int h
     return CAPK_OK;
   }
   const int hdp = hdp_of(hd);
-  const size_t shm = fwd_smem(Nk, hdp);
+  const size_t shm = fwd_kernel_smem(Nk, hdp);
   const dim3 grid(B * H), block(512);
-  switch (hdp) {
-    case 32: return launch_dyn(attn_fwd_bf16<32>, grid, block, shm, st, a, "attn_fwd_bf16");
-    case 64: return launch_dyn(attn_fwd_bf16<64>, grid, block, shm, st, a, "attn_fwd_bf16");
-    case 96: return launch_dyn(attn_fwd_bf16<96>, grid, block, shm, st, a, "attn_fwd_bf16");
-    default: return launch_dyn(attn_fwd_bf16<128>, grid, block, shm, st, a, "attn_fwd_bf16");
+  const int mode = (drop_p > 0.f ? AM_DROP : 0) | ((causal || key_pad) ? AM_MASK : 0);
+#define FWD_M(HD)                                                                                        \
+  switch (mode) {                                                                                        \
+    case 0: return launch_dyn(attn_fwd_bf16<HD, 0>, grid, block, shm, st, a, "attn_fwd_bf16");           \
+    case 1: return launch_dyn(attn_fwd_bf16<HD, 1>, grid, block, shm, st, a, "attn_fwd_bf16");           \
+    case 2: return launch_dyn(attn_fwd_bf16<HD, 2>, grid, block, shm, st, a, "attn_fwd_bf16");           \
+    default: return launch_dyn(attn_fwd_bf16<HD, 3>, grid, block, shm, st, a, "attn_fwd_bf16");          \
   }
+  switch (hdp) {
+    case 32: FWD_M(32)
+    case 64: FWD_M(64)
+    case 96: FWD_M(96)
+    default: FWD_M(128)
+  }
+#undef FWD_M
 }
 
 extern "C" int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int hd, float scale, int causal,
@@ -920,43 +1027,58 @@ extern "C" int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int h
                  "capk_attention_bwd(bf16): strides must allow vector access");
   const int hdp = hdp_of(hd);
   const dim3 grid(B * H), block(512);
+  const int mode = (drop_p > 0.f ? AM_DROP : 0) | ((causal || key_pad) ? AM_MASK : 0);
+#define BY_MODE(CALL)        \
+  switch (mode) {            \
+    case 0: CALL(0); break;  \
+    case 1: CALL(1); break;  \
+    case 2: CALL(2); break;  \
+    default: CALL(3); break; \
+  }
+#define BY_HDP(CALL2, M)          \
+  switch (hdp) {                  \
+    case 32: CALL2(32, M); break; \
+    case 64: CALL2(64, M); break; \
+    case 96: CALL2(96, M); break; \
+    default: CALL2(128, M); break; \
+  }
+  int rc2 = CAPK_OK;
   {
     // split backward: dK/dV kernel, then dQ kernel (two head images in LDS each)
     const size_t s1 = bwd_kv_smem(Nq, hdp), s2 = fwd_smem(Nk, hdp);
     // (measured: ViT N=197 bwd 554 -> 460 us; for Nq <= 32 the second launch costs more than it saves)
     if (Nq > 32 && s1 <= 80 * 1024 && s2 <= 80 * 1024) {
-      int rc2;
       static const int wpe = [] { const char* e = getenv("CAPK_ATTN_WPE"); return e ? atoi(e) : 4; }();
+#define KV4(HD, M) rc2 = launch_dyn(attn_bwd_kv_bf16<HD, 4, M>, grid, block, s1, st, a, "attn_bwd_kv_bf16")
+#define KV2(HD, M) rc2 = launch_dyn(attn_bwd_kv_bf16<HD, 2, M>, grid, block, s1, st, a, "attn_bwd_kv_bf16")
+#define QK(HD, M) rc2 = launch_dyn(attn_bwd_q_bf16<HD, M>, grid, block, s2, st, a, "attn_bwd_q_bf16")
+#define KV4M(M) BY_HDP(KV4, M)
+#define KV2M(M) BY_HDP(KV2, M)
+#define QKM(M) BY_HDP(QK, M)
       if (wpe == 4) {  // <= 128 VGPRs: two workgroups per CU
-        switch (hdp) {
-          case 32: rc2 = launch_dyn(attn_bwd_kv_bf16<32, 4>, grid, block, s1, st, a, "attn_bwd_kv_bf16"); break;
-          case 64: rc2 = launch_dyn(attn_bwd_kv_bf16<64, 4>, grid, block, s1, st, a, "attn_bwd_kv_bf16"); break;
-          case 96: rc2 = launch_dyn(attn_bwd_kv_bf16<96, 4>, grid, block, s1, st, a, "attn_bwd_kv_bf16"); break;
-          default: rc2 = launch_dyn(attn_bwd_kv_bf16<128, 4>, grid, block, s1, st, a, "attn_bwd_kv_bf16"); break;
-        }
+        BY_MODE(KV4M)
       } else {
-        switch (hdp) {
-          case 32: rc2 = launch_dyn(attn_bwd_kv_bf16<32, 2>, grid, block, s1, st, a, "attn_bwd_kv_bf16"); break;
-          case 64: rc2 = launch_dyn(attn_bwd_kv_bf16<64, 2>, grid, block, s1, st, a, "attn_bwd_kv_bf16"); break;
-          case 96: rc2 = launch_dyn(attn_bwd_kv_bf16<96, 2>, grid, block, s1, st, a, "attn_bwd_kv_bf16"); break;
-          default: rc2 = launch_dyn(attn_bwd_kv_bf16<128, 2>, grid, block, s1, st, a, "attn_bwd_kv_bf16"); break;
-        }
+        BY_MODE(KV2M)
       }
       if (rc2) return rc2;
-      switch (hdp) {
-        case 32: return launch_dyn(attn_bwd_q_bf16<32>, grid, block, s2, st, a, "attn_bwd_q_bf16");
-        case 64: return launch_dyn(attn_bwd_q_bf16<64>, grid, block, s2, st, a, "attn_bwd_q_bf16");
-        case 96: return launch_dyn(attn_bwd_q_bf16<96>, grid, block, s2, st, a, "attn_bwd_q_bf16");
-        default: return launch_dyn(attn_bwd_q_bf16<128>, grid, block, s2, st, a, "attn_bwd_q_bf16");
-      }
+      BY_MODE(QKM)
+      return rc2;
     }
   }
   const size_t shm = bwd_smem(Nq, Nk, hdp);
   CAPK_CHECK_ARG(shm <= 160 * 1024, "capk_attention_bwd: LDS %zu > 160 KiB", shm);
-  switch (hdp) {
-    case 32: return launch_dyn(attn_bwd_bf16<32>, grid, block, shm, st, a, "attn_bwd_bf16");
-    case 64: return launch_dyn(attn_bwd_bf16<64>, grid, block, shm, st, a, "attn_bwd_bf16");
-    case 96: return launch_dyn(attn_bwd_bf16<96>, grid, block, shm, st, a, "attn_bwd_bf16");
-    default: return launch_dyn(attn_bwd_bf16<128>, grid, block, shm, st, a, "attn_bwd_bf16");
-  }
+#define FB(HD, M) rc2 = launch_dyn(attn_bwd_bf16<HD, M>, grid, block, shm, st, a, "attn_bwd_bf16")
+#define FBM(M) BY_HDP(FB, M)
+  BY_MODE(FBM)
+  return rc2;
+#undef FB
+#undef FBM
+#undef KV4
+#undef KV2
+#undef QK
+#undef KV4M
+#undef KV2M
+#undef QKM
+#undef BY_HDP
+#undef BY_MODE
 }

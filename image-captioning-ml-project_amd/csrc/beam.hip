@@ -515,6 +515,57 @@ __global__ __launch_bounds__(256) void sample_rows_kernel_f32(const float* __res
   }
 }
 
+// bf16 rows up to SAMPLE_LDS_MAX elements: the same arithmetic (per-thread contiguous chunks
+// summed in order) on a row staged once in LDS with coalesced 16-B loads -- the chunk-owner
+// layout reads global memory 197 elements apart per lane, and three passes re-read it.
+constexpr int SAMPLE_LDS_MAX = 65536;  // 128 KiB of LDS
+__global__ __launch_bounds__(256) void sample_rows_lds_kernel(const bf16* __restrict__ x0, int64_t ld, int V,
+                                                              uint32_t seed, int step, int64_t* __restrict__ out,
+                                                              int64_t out_stride, float* __restrict__ logp) {
+  extern __shared__ __attribute__((aligned(16))) char dyn[];
+  bf16* row = (bf16*)dyn;
+  const int r = blockIdx.x, tid = threadIdx.x;
+  const bf16* xr = x0 + (int64_t)r * ld;
+  const int v8 = V & ~7;
+  for (int i = tid * 8; i < v8; i += 256 * 8) *(bf16x8*)(row + i) = *(const bf16x8*)(xr + i);
+  for (int i = v8 + tid; i < V; i += 256) row[i] = xr[i];
+  __syncthreads();
+  const int chunk = (V + 255) / 256;
+  const int lo = tid * chunk, hi = min(V, lo + chunk);
+  __shared__ float red[4];
+  __shared__ float pre[257];
+  float m = -INFINITY;
+  for (int i = lo; i < hi; ++i) m = fmaxf(m, (float)row[i]);
+  m = wave_max(m);
+  if ((tid & 63) == 0) red[tid >> 6] = m;
+  __syncthreads();
+  const float M = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float sl = 0.f;
+  for (int i = lo; i < hi; ++i) sl += __expf((float)row[i] - M);
+  pre[tid + 1] = sl;
+  __syncthreads();
+  if (tid == 0) {
+    pre[0] = 0.f;
+    for (int t = 1; t <= 256; ++t) pre[t] += pre[t - 1];
+  }
+  __syncthreads();
+  const float S = pre[256];
+  const uint32_t h = drop_hash(seed, ((uint64_t)(uint32_t)step << 32) | (uint32_t)r);
+  const float target = (float)(h >> 8) * (1.0f / 16777216.0f) * S;
+  const bool own = (pre[tid] <= target && target < pre[tid + 1]) ||
+                   (tid == min(255, (V - 1) / chunk) && target >= pre[tid + 1]);
+  if (own && lo < hi) {
+    float cum = pre[tid];
+    int tok = hi - 1;
+    for (int i = lo; i < hi; ++i) {
+      cum += __expf((float)row[i] - M);
+      if (cum > target) { tok = i; break; }
+    }
+    out[(int64_t)r * out_stride] = tok;
+    if (logp) logp[r] = ((float)row[tok] - M) - logf(S);
+  }
+}
+
 static int grid_of(int64_t work) {
   int64_t g = (work + 255) / 256;
   return (int)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
@@ -635,8 +686,18 @@ extern "C" int capk_sample_rows(int dtype, int rows, int V, int64_t ld, const vo
                                 int64_t* out, int64_t out_stride, float* logp, void* stream) {
   CAPK_CHECK_ARG(rows > 0 && V > 0 && ld >= V && (dtype == CAPK_F32 || dtype == CAPK_BF16),
                  "capk_sample_rows: bad arguments");
-  hipLaunchKernelGGL(sample_rows_kernel_f32, dim3(rows), dim3(256), 0, S(stream), (const float*)logits, ld, V, seed,
-                     step, out, out_stride, logp, dtype == CAPK_BF16 ? 1 : 0);
+  if (dtype == CAPK_BF16 && V <= SAMPLE_LDS_MAX && ld % 8 == 0 && (uintptr_t)logits % 16 == 0) {
+    const size_t lds = (size_t)((V + 7) & ~7) * sizeof(bf16);
+    static const hipError_t attr = hipFuncSetAttribute((const void*)sample_rows_lds_kernel,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       SAMPLE_LDS_MAX * (int)sizeof(bf16));
+    if (attr != hipSuccess) return hip_status(attr, "capk_sample_rows: hipFuncSetAttribute");
+    hipLaunchKernelGGL(sample_rows_lds_kernel, dim3(rows), dim3(256), lds, S(stream), (const bf16*)logits, ld, V, seed,
+                       step, out, out_stride, logp);
+  } else {
+    hipLaunchKernelGGL(sample_rows_kernel_f32, dim3(rows), dim3(256), 0, S(stream), (const float*)logits, ld, V, seed,
+                       step, out, out_stride, logp, dtype == CAPK_BF16 ? 1 : 0);
+  }
   CAPK_LAUNCH_CHECK("sample_rows_kernel");
   return CAPK_OK;
 }

@@ -8,7 +8,8 @@
 //
 //   rows mode       x [rows][cols] (ldx)      -> q [rows][cols] (ldq), one wave per row
 //   transpose mode  x [cols][rows] (ldx)      -> q [rows][cols]: a Conv1D weight [in, out]
-//                   (GPT-2) becomes the K-major [out][in] operand, through 64x64 LDS tiles.
+//                   (GPT-2) becomes the K-major [out][in] operand: column maxima (atomic max
+//                   into the caller's workspace), then 64x64 tiles transposed through LDS.
 //
 // HBM-bound: reads 2 (bf16) or 4 (fp32) bytes and writes 1 byte per element.
 #include "common.h"
@@ -70,53 +71,59 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(int rows, int cols, con
   if (lane == 0) scale[row] = (uint8_t)code;
 }
 
-// transpose mode: block = 64 output rows (input columns) x all cols (input rows).
-// 256 threads; pass 1: per-column amax (thread = column c&63, row group c>>6); pass 2:
-// 64x64 tiles staged in LDS, written K-contiguous (each thread 16 bytes = 16 k of one row).
+// transpose mode, pass 1: column maxima.  grid (ceil(rows/256), ceil(cols/64)); thread =
+// one input column n (coalesced rows), 64 input rows; partial maxima combined with an
+// atomic max on the fp32 bit pattern (non-negative floats order like their bits).
+template <typename T>
+__global__ __launch_bounds__(256) void amax_cols_kernel(int rows, int cols, const T* __restrict__ x, int64_t ldx,
+                                                        uint32_t* __restrict__ amax) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= rows) return;
+  const int k0 = blockIdx.y * 64, k1 = min(cols, k0 + 64);
+  float m = 0.f;
+#pragma unroll 8
+  for (int k = k0; k < k1; ++k) m = fmaxf(m, fabsf(to_f32(x[(int64_t)k * ldx + n])));
+  atomicMax(amax + n, __float_as_uint(m));
+}
+
+// transpose mode, pass 2: one 64 (output rows) x 64 (k) tile per block, grid
+// (ceil(rows/64), ceil(cols/64)); staged through LDS and written K-contiguous (each thread
+// 16 bytes = 16 k of one output row).
 template <typename T>
 __global__ __launch_bounds__(256) void quant_trans_kernel(int rows, int cols, const T* __restrict__ x, int64_t ldx,
-                                                          uint8_t* __restrict__ q, int64_t ldq,
-                                                          uint8_t* __restrict__ scale) {
-  __shared__ float red[4][64];
+                                                          const uint32_t* __restrict__ amax, uint8_t* __restrict__ q,
+                                                          int64_t ldq, uint8_t* __restrict__ scale) {
   __shared__ float tile[64][65];
   __shared__ float sinv[64];
   const int tid = threadIdx.x, cl = tid & 63, rg = tid >> 6;
   const int r0 = blockIdx.x * 64;  // first output row = input column
+  const int k0 = blockIdx.y * 64;
   const int n = r0 + cl;
-  float amax = 0.f;
-  if (n < rows)
-    for (int k = rg; k < cols; k += 4) amax = fmaxf(amax, fabsf(to_f32(x[(int64_t)k * ldx + n])));
-  red[rg][cl] = amax;
-  __syncthreads();
   if (tid < 64) {
-    const float a = fmaxf(fmaxf(red[0][tid], red[1][tid]), fmaxf(red[2][tid], red[3][tid]));
-    const int code = scale_code(a);
+    const int code = scale_code(r0 + tid < rows ? __uint_as_float(amax[r0 + tid]) : 0.f);
     sinv[tid] = inv_scale(code);
-    if (r0 + tid < rows) scale[r0 + tid] = (uint8_t)code;
+    if (blockIdx.y == 0 && r0 + tid < rows) scale[r0 + tid] = (uint8_t)code;
   }
   __syncthreads();
-  for (int k0 = 0; k0 < cols; k0 += 64) {
-    // load x[k0 + kk][r0 + cl] for kk = rg, rg+4, ...  (coalesced along n)
-    for (int kk = rg; kk < 64; kk += 4) {
-      const int k = k0 + kk;
-      tile[kk][cl] = (k < cols && n < rows) ? to_f32(x[(int64_t)k * ldx + n]) * sinv[cl] : 0.f;
-    }
-    __syncthreads();
-    // write q[r0 + rr][k0 + 16*c4 .. +16]: thread = (rr = tid >> 2, c4 = tid & 3)
-    const int rr = tid >> 2, c4 = tid & 3;
-    const int kb = k0 + c4 * 16;
-    if (r0 + rr < rows && kb < cols) {
-      uint4 w;
-      float v[16];
+  // load x[k0 + kk][r0 + cl] for kk = rg, rg+4, ...  (coalesced along n)
+#pragma unroll 4
+  for (int kk = rg; kk < 64; kk += 4) {
+    const int k = k0 + kk;
+    tile[kk][cl] = (k < cols && n < rows) ? to_f32(x[(int64_t)k * ldx + n]) * sinv[cl] : 0.f;
+  }
+  __syncthreads();
+  const int rr = tid >> 2, c4 = tid & 3;
+  const int kb = k0 + c4 * 16;
+  if (r0 + rr < rows && kb < cols) {
+    uint4 w;
+    float v[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = tile[c4 * 16 + i][rr];
-      w.x = pack4(v[0], v[1], v[2], v[3]);
-      w.y = pack4(v[4], v[5], v[6], v[7]);
-      w.z = pack4(v[8], v[9], v[10], v[11]);
-      w.w = pack4(v[12], v[13], v[14], v[15]);
-      *(uint4*)(q + (int64_t)(r0 + rr) * ldq + kb) = w;
-    }
-    __syncthreads();
+    for (int i = 0; i < 16; ++i) v[i] = tile[c4 * 16 + i][rr];
+    w.x = pack4(v[0], v[1], v[2], v[3]);
+    w.y = pack4(v[4], v[5], v[6], v[7]);
+    w.z = pack4(v[8], v[9], v[10], v[11]);
+    w.w = pack4(v[12], v[13], v[14], v[15]);
+    *(uint4*)(q + (int64_t)(r0 + rr) * ldq + kb) = w;
   }
 }
 
@@ -125,8 +132,13 @@ __global__ __launch_bounds__(256) void quant_trans_kernel(int rows, int cols, co
 
 using namespace capk;
 
+extern "C" size_t capk_quant_fp8_workspace(int rows, int cols, int transpose) {
+  (void)cols;
+  return transpose ? (size_t)rows * sizeof(uint32_t) : 0;
+}
+
 extern "C" int capk_quant_fp8(int in_dtype, int rows, int cols, const void* x, int64_t ldx, int transpose, void* q,
-                              int64_t ldq, void* scale, void* stream) {
+                              int64_t ldq, void* scale, void* ws, size_t ws_bytes, void* stream) {
   CAPK_CHECK_ARG(rows > 0 && cols > 0 && x && q && scale, "capk_quant_fp8: bad arguments");
   CAPK_CHECK_ARG(in_dtype == CAPK_BF16 || in_dtype == CAPK_F32, "capk_quant_fp8: in_dtype must be f32 or bf16");
   // rows mode stores 8 bytes per lane, transpose mode 16
@@ -148,13 +160,21 @@ extern "C" int capk_quant_fp8(int in_dtype, int rows, int cols, const void* x, i
                          (uint8_t*)q, ldq, (uint8_t*)scale);
   } else {
     CAPK_CHECK_ARG(cols % 16 == 0 && ldx >= rows, "capk_quant_fp8(transpose): cols %% 16 == 0, ldx >= rows");
-    const int grid = (rows + 63) / 64;
-    if (in_dtype == CAPK_F32)
-      hipLaunchKernelGGL(quant_trans_kernel<float>, dim3(grid), dim3(256), 0, st, rows, cols, (const float*)x, ldx,
+    CAPK_CHECK_ARG(ws && ws_bytes >= (size_t)rows * 4 && (uintptr_t)ws % 4 == 0,
+                   "capk_quant_fp8(transpose): workspace of capk_quant_fp8_workspace() bytes required");
+    uint32_t* amax = (uint32_t*)ws;
+    const hipError_t me = hipMemsetAsync(amax, 0, (size_t)rows * 4, st);
+    if (me != hipSuccess) return hip_status(me, "capk_quant_fp8: hipMemsetAsync");
+    const dim3 g1((rows + 255) / 256, (cols + 63) / 64), g2((rows + 63) / 64, (cols + 63) / 64);
+    if (in_dtype == CAPK_F32) {
+      hipLaunchKernelGGL(amax_cols_kernel<float>, g1, dim3(256), 0, st, rows, cols, (const float*)x, ldx, amax);
+      hipLaunchKernelGGL(quant_trans_kernel<float>, g2, dim3(256), 0, st, rows, cols, (const float*)x, ldx, amax,
                          (uint8_t*)q, ldq, (uint8_t*)scale);
-    else
-      hipLaunchKernelGGL(quant_trans_kernel<bf16>, dim3(grid), dim3(256), 0, st, rows, cols, (const bf16*)x, ldx,
+    } else {
+      hipLaunchKernelGGL(amax_cols_kernel<bf16>, g1, dim3(256), 0, st, rows, cols, (const bf16*)x, ldx, amax);
+      hipLaunchKernelGGL(quant_trans_kernel<bf16>, g2, dim3(256), 0, st, rows, cols, (const bf16*)x, ldx, amax,
                          (uint8_t*)q, ldq, (uint8_t*)scale);
+    }
   }
   CAPK_LAUNCH_CHECK("capk_quant_fp8");
   return CAPK_OK;

@@ -108,8 +108,9 @@ int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K,
  * capk_gemm_f8: C[M,N] = epilogue(sum_k A[m,k] 2^sa[m] * B[n,k] 2^sb[n]) with fp32
  *   accumulation; A [M][lda], B [N][ldb] e4m3fn K-major, K % 128 == 0; same epilogue
  *   arguments and meaning as capk_gemm (forward activations only). */
+size_t capk_quant_fp8_workspace(int rows, int cols, int transpose); /* transpose: rows * 4 bytes */
 int capk_quant_fp8(int in_dtype, int rows, int cols, const void* x, int64_t ldx, int transpose,
-                   void* q, int64_t ldq, void* scale, void* stream);
+                   void* q, int64_t ldq, void* scale, void* ws, size_t ws_bytes, void* stream);
 size_t capk_gemm_f8_workspace(int M, int N, int K);
 int capk_gemm_f8(int out_dtype, int M, int N, int K, const void* A, int64_t lda, const void* a_scale,
                  const void* B, int64_t ldb, const void* b_scale, void* C, int64_t ldc, float beta,

@@ -76,3 +76,71 @@ def time_cpu_beam(state_dict, images=2, num_beams=5, max_length=20, threads=None
                     bos=eos, eos=eos, pad=eos)
     dt = time.perf_counter() - t0
     return images / dt, dt
+
+
+def time_cpu_scst(state_dict, images=2, max_length=20, threads=None, eos=50256, refs_per_image=5):
+    """Images/s of the oracle CPU SCST update for config 5 (CLIP-ViT-B/32 + GPT-2) on a
+    bounded sample -- CaptioningTrainer._train_reinforcement_learning (src/train/
+    trainer.py:338-381) with the SURVEY D7/D8/D9 restatements: CLIP forward (with grad),
+    sampled captions (softmax sampling, the decoder re-run on each prefix as the reference's
+    _sample_captions does, trainer.py:383-438), the GPT-2 baseline beam-4 generate
+    (decoders.py:645-654 -> oracle/beam.py), CIDEr-D rewards (oracle/cider.py), the
+    policy-gradient loss over a teacher-forced re-run, backward, AdamW."""
+    from .beam import beam_search
+    from .cider import cider_d
+    if threads:
+        torch.set_num_threads(threads)
+    params = make_params(state_dict)
+    enc_p, dec_p = _sub(params, "encoder.model."), _sub(params, "decoder.")
+    g = torch.Generator().manual_seed(11)
+    img = torch.randn(images, 3, 224, 224, generator=g)
+    refs = [[torch.randint(0, eos, (int(torch.randint(8, 17, (1,), generator=g)),), generator=g).tolist()
+             for _ in range(refs_per_image)] for _ in range(images)]
+
+    def strip(seq):
+        out = []
+        for t in seq[1:]:
+            if t == eos:
+                break
+            out.append(int(t))
+        return out
+
+    t0 = time.perf_counter()
+    for p in params.values():
+        p.grad = None
+    enc = oenc.clip_encoder(enc_p, img, 12, 12, 32)
+    pooled = enc["pooled_features"]
+    with torch.no_grad():
+        dp = {k: v.detach() for k, v in dec_p.items()}
+        pd = pooled.detach()
+        seqs = torch.full((images, 1), eos, dtype=torch.long)
+        for _ in range(max_length - 1):
+            last = odec.gpt2_decoder(dp, pd, seqs, 12, 12, eos, use_pad_mask=False)[:, -1]
+            nxt = torch.distributions.Categorical(logits=last).sample()
+            seqs = torch.cat([seqs, nxt[:, None]], 1)
+            if bool((nxt == eos).all()):
+                break
+        pr = pd.repeat_interleave(4, 0)
+        base = beam_search(lambda s: odec.gpt2_decoder(dp, pr, s, 12, 12, eos, use_pad_mask=False)[:, -1], images, 4,
+                           max_length, bos=eos, eos=eos, pad=eos)["sequences"]
+    r_s = cider_d([strip(s) for s in seqs.tolist()], refs)
+    r_b = cider_d([strip(s) for s in base.tolist()], refs)
+    adv = torch.tensor([a - b for a, b in zip(r_s, r_b)], dtype=torch.float32)
+    logits = odec.gpt2_decoder(dec_p, pooled, seqs, 12, 12, eos, use_pad_mask=False)
+    logp = torch.log_softmax(logits[:, :-1], -1).gather(2, seqs[:, 1:, None])[..., 0]
+    keep = torch.ones_like(logp, dtype=torch.bool)
+    for b in range(images):  # tokens up to and including the first EOS (D8)
+        row = seqs[b, 1:].tolist()
+        if eos in row:
+            keep[b, row.index(eos) + 1:] = False
+    loss = -(logp * adv[:, None] * keep).sum() / keep.sum()
+    loss.backward()
+    with torch.no_grad():
+        opt_state = {}
+        for n, p in params.items():
+            if p.grad is None:
+                continue
+            m, v = opt_state.setdefault(n, (torch.zeros_like(p), torch.zeros_like(p)))
+            otrain.adamw_step(p, p.grad, m, v, 1, 5e-5, 0.0 if otrain.no_decay(n) else 0.01)
+    dt = time.perf_counter() - t0
+    return images / dt, dt

@@ -137,11 +137,20 @@ def _attn_ref(q, k, v, scale, causal, key_pad):
 
 @cuda
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("case", ["vit", "dec_self", "dec_cross_gap", "clip"])
+@pytest.mark.parametrize("case", ["vit", "dec_self", "dec_cross_gap", "clip", "vit_stream", "pad_stream",
+                                  "causal_stream"])
 def test_attention_fwd_bwd(ops, dtype, case):
+    """*_stream cases have >= 1024 (batch, head) pairs: the bf16 forward runs the persistent
+    streaming kernel (attn_fwd_stream_bf16); the others the per-head kernel."""
     from capk.ops import HeadView
     g = torch.Generator(device="cuda").manual_seed(5)
-    if case == "vit":
+    if case == "vit_stream":
+        B, H, Nq, Nk, hd, causal, gap = 96, 12, 197, 197, 64, False, 0
+    elif case == "pad_stream":
+        B, H, Nq, Nk, hd, causal, gap = 128, 8, 50, 50, 64, False, 1
+    elif case == "causal_stream":
+        B, H, Nq, Nk, hd, causal, gap = 128, 8, 40, 40, 64, True, 0
+    elif case == "vit":
         B, H, Nq, Nk, hd, causal, gap = 3, 4, 197, 197, 64, False, 0
     elif case == "dec_self":
         B, H, Nq, Nk, hd, causal, gap = 4, 8, 20, 20, 96, True, 0
@@ -155,10 +164,12 @@ def test_attention_fwd_bwd(ops, dtype, case):
     kv = torch.randn(kvrows, 2 * D, device="cuda", generator=g).to(dtype)
     do = torch.randn(B * Nq, D, device="cuda", generator=g).to(dtype)
     key_pad = None
-    if case == "dec_self":
+    if case in ("dec_self", "pad_stream"):
         key_pad = torch.zeros(B, Nk, dtype=torch.bool, device="cuda")
         key_pad[1, 15:] = True
         key_pad[3, 19] = True
+        if case == "pad_stream":
+            key_pad[7:, 33:] = True
     o = torch.empty(B * Nq, D, device="cuda", dtype=dtype)
     qv = HeadView(q, 0, Nq * D, D)
     kview = HeadView(kv, 0, (Nk + gap) * 2 * D, 2 * D)

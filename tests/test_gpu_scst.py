@@ -18,14 +18,18 @@ GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 @cuda
 @pytest.mark.parametrize("V,scale", [(50257, 3.0), (61, 1.0)])
-def test_sample_rows_vs_oracle(V, scale):
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_sample_rows_vs_oracle(V, scale, dtype):
+    """fp32 rows: the chunk-owner kernel; bf16 rows: the LDS-staged kernel (same arithmetic
+    on the bf16 values, which the oracle receives exactly)."""
     from capk import ops
     g = torch.Generator().manual_seed(V)
     R = 48
-    x = torch.randn(R, V, generator=g) * scale
+    x = (torch.randn(R, V, generator=g) * scale).to(dtype).float()
     ld = (V + 63) // 64 * 64
     xp = torch.full((R, ld), 1e4)
     xp[:, :V] = x
+    xp = xp.to(dtype)
     out = torch.empty(R, dtype=torch.long, device="cuda")
     logp = torch.empty(R, dtype=torch.float32, device="cuda")
     for step in (0, 7):
