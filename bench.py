@@ -314,6 +314,95 @@ def run_config5(args, world, rank, device):
     return rec
 
 
+# ------------------------------------------------------------------ config 2 ----
+def build_config2(device):
+    """BASELINE configs[1]: ResNet-101 + LSTM (768 hidden, 6 layers) + soft attention, bf16."""
+    import capk
+    from capk import config as C
+    from capk.models import captioning_model as cm
+    from capk.train import CapkAdamW, CombinedLoss
+    torch.manual_seed(42)
+    cfg = C.Config()
+    cfg.model.encoder = C.EncoderConfig(encoder_type="resnet", pretrained_model_name="microsoft/resnet-101")
+    cfg.model.decoder = C.DecoderConfig(decoder_type="lstm", hidden_dim=768, num_layers=6, num_heads=1)
+    cfg.model.attention = C.AttentionConfig(attention_type="soft", num_heads=1)
+    cfg.model.vocab_size, cfg.model.pad_token_id = 50257, 50256
+    cfg.model.bos_token_id = cfg.model.eos_token_id = 50256
+    model = cm.ImageCaptioningModel(cfg)
+    cpu_sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    store = capk.prepare(model, device, "bf16")
+    opt = CapkAdamW(store, lr=cfg.training.learning_rate, weight_decay=cfg.training.weight_decay)
+    return cfg, model, store, opt, CombinedLoss(cfg.model.pad_token_id), cpu_sd
+
+
+def run_config2(args, world, rank, device):
+    """One step = the CE train step of config 2 at bs=args.batch per GPU (128 by default for
+    this workload): ResNet-101 forward (train-mode BatchNorm) + LSTM/soft-attention decoder
+    over 20 tokens + CE + backward + (DP all-reduce) + AdamW."""
+    from capk import ops
+    from capk.train.dp import GradBucketer
+    from capk.train.optim import cosine_schedule_with_warmup
+    cfg, model, store, opt, loss_fn, cpu_sd = build_config2(device)
+    B = args.batch
+    g = torch.Generator(device=device).manual_seed(0 + 1000 * rank)
+    images = torch.randn(B, 3, 224, 224, device=device, generator=g)
+    captions = torch.randint(0, 50256, (B, 20), device=device, generator=g)
+    bucketer = GradBucketer(store, exchange=args.grad_exchange) if world > 1 else None
+    model.train()
+    step_no = [0]
+    last = [None]
+
+    def step():
+        out = model(images=images, captions=captions, caption_lengths=None)
+        loss = loss_fn(logits=out["logits"], targets=captions)["total_loss"]
+        loss.backward()
+        if bucketer is not None:
+            bucketer.finish()
+        opt.step(lr=cosine_schedule_with_warmup(step_no[0], cfg.training.learning_rate, cfg.training.warmup_steps,
+                                                10_000))
+        step_no[0] += 1
+        last[0] = loss
+
+    for _ in range(args.warmup):
+        step()
+    ops.GEMM_TIMER.start()
+    elapsed = timed_steps(step, args.steps, 0, world, torch.cuda.synchronize, device)
+    ops.GEMM_TIMER.stop()
+    gem = ops.GEMM_TIMER.summary()
+    if rank != 0:
+        return None
+    value = throughput(B, world, args.steps, elapsed)
+    bf = gem["by_route"]["gemm_bf16_kernel"]
+    rec = {
+        "metric": "images/sec train (ResNet-101 + LSTM + soft attention, CE)", "value": round(value, 2),
+        "unit": "images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (randn 224x224x3 images, randint 20-token captions), random-init weights",
+        "config": {"workload": "config 2: ResNet-101 + LSTM(768, 6 layers) + soft attention, CE train step",
+                   "global_batch": B * world, "per_gpu_batch": B, "seq_len": 20, "image_tokens": 49,
+                   "vocab": 50257, "parallelism": f"dp{world}",
+                   "grad_exchange": args.grad_exchange if world > 1 else None},
+        "roofline": {"bound": "mfma", "kernel": "bf16 GEMM family (convolutions as implicit GEMMs, LSTM / "
+                                                "attention / vocabulary projections): every capk_gemm launch",
+                     "achieved": round(bf["tflops"], 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(bf["tflops"] / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "traffic_source": "not collected for config 2", "launches": bf["launches"],
+                     "gemm_share_of_step": round(gem["total_ms"] / (elapsed * 1e3), 3)},
+        "final_loss": round(float(last[0]), 4),
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        from oracle.step import time_cpu_config2
+        threads, hinfo = host_cpus()
+        ips, dt = time_cpu_config2(cpu_sd, batch=2, steps=1, threads=threads)
+        rec["cpu_baseline"] = {"value": round(ips, 4), "unit": "images/s", "cores": threads, "kind": "port",
+                               "host": hinfo,
+                               "sample": f"oracle fp32 CPU train step (ResNet-101 train-mode BN + LSTM 6x768 + soft "
+                                         f"attention, torch CPU autograd + AdamW), batch 2, 1 timed step after 1 "
+                                         f"warm-up ({dt:.1f} s)"}
+    return rec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -328,8 +417,9 @@ def main():
     ap.add_argument("--cpu-beam-images", type=int, default=24)
     ap.add_argument("--grad-exchange", choices=["fp32", "bf16"], default="bf16",
                     help="DP gradient all-reduce precision (fp32 master weights either way)")
-    ap.add_argument("--workload", choices=["config3", "config5"], default="config3",
-                    help="config3 (headline: ViT+Transformer CE) or config5 (CLIP+GPT-2 SCST, fp8)")
+    ap.add_argument("--workload", choices=["config3", "config2", "config5"], default="config3",
+                    help="config3 (headline: ViT+Transformer CE), config2 (ResNet-101+LSTM CE, bs 128) or "
+                         "config5 (CLIP+GPT-2 SCST, fp8)")
     ap.add_argument("--precision", choices=["fp8", "bf16"], default="fp8", help="config5 forward precision")
     ap.add_argument("--cpu-batch-scst", type=int, default=4)
     args = ap.parse_args()
@@ -337,8 +427,10 @@ def main():
     world, rank, local = dist_init("nccl")
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
-    if args.workload == "config5":
-        rec = run_config5(args, world, rank, device)
+    if args.workload in ("config2", "config5"):
+        if args.workload == "config2" and args.batch == 256:
+            args.batch = 128  # BASELINE configs[1]: bs=128
+        rec = (run_config2 if args.workload == "config2" else run_config5)(args, world, rank, device)
         if rank == 0:
             print(json.dumps(rec), flush=True)
         if world > 1:

@@ -508,9 +508,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
   const float sl2 = a.scale * kLog2e;
   const bf16* kbase = (const bf16*)a.k + (int64_t)b * a.k_bs + hoff;
   const bf16* vbase = (const bf16*)a.v + (int64_t)b * a.v_bs + hoff;
-  for (int kb = wave; kb < NKP / 16; kb += nwaves) {
+  // the wave's own K / V rows; the next key block's are loaded while this one computes
+  auto load_rows = [&](int kb, bf16x8 (&kf)[HDP / 32], bf16x8 (&vf)[HDP / 32]) {
     const int keyl = kb * 16 + (lane & 15);
-    bf16x8 kf[HDP / 32], vf[HDP / 32];
 #pragma unroll
     for (int s = 0; s < HDP / 32; ++s) {
       const int d = s * 32 + 8 * (lane >> 4);
@@ -518,6 +518,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
       kf[s] = in ? ld8(kbase + (int64_t)keyl * a.k_rs + d) : zero8();
       vf[s] = in ? ld8(vbase + (int64_t)keyl * a.v_rs + d) : zero8();
     }
+  };
+  bf16x8 kf[HDP / 32], vf[HDP / 32];
+  if (wave < NKP / 16) load_rows(wave, kf, vf);
+  for (int kb = wave; kb < NKP / 16; kb += nwaves) {
+    const int keyl = kb * 16 + (lane & 15);
+    bf16x8 kn[HDP / 32], vn[HDP / 32];
+    if (kb + nwaves < NKP / 16) load_rows(kb + nwaves, kn, vn);
     f32x4 dvt[HDP / 16], dkt[HDP / 16];
 #pragma unroll
     for (int db = 0; db < HDP / 16; ++db) dvt[db] = dkt[db] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -562,23 +569,32 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
       }
     }
+#pragma unroll
+    for (int s = 0; s < HDP / 32; ++s) {
+      kf[s] = kn[s];
+      vf[s] = vn[s];
+    }
   }
 }
 
+// dQ kernel; HDP 64: swizzled 16-row K/V images and <= 80 VGPRs (three workgroups per CU),
+// as the forward kernel.
 template <int HDP, int MODE>
-__global__ __launch_bounds__(512) void attn_bwd_q_bf16(AttnArgs a) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HDP == 64 ? 6 : 1))) void attn_bwd_q_bf16(
+    AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
-  const int NQP = (a.Nq + 31) & ~31, NKP = (a.Nk + 31) & ~31;
-  constexpr int ST = HDP + 8;
+  constexpr bool SW = HDP == 64;
+  const int NQP = (a.Nq + 31) & ~31, NKP = SW ? (a.Nk + 15) & ~15 : (a.Nk + 31) & ~31;
+  constexpr int ST = SW ? 64 : HDP + 8;
   bf16* Ks = (bf16*)smem;
   bf16* Vs = Ks + NKP * ST;
   const int hoff = h * a.hd;
   {
     const StageSrc S[2] = {{Ks, (const bf16*)a.k + (int64_t)b * a.k_bs + hoff, a.k_rs, a.Nk, NKP},
                            {Vs, (const bf16*)a.v + (int64_t)b * a.v_bs + hoff, a.v_rs, a.Nk, NKP}};
-    stage_images<HDP, 2, 512>(S, a.hd);
+    stage_images_rt<HDP, 2, SW>(S, a.hd);
   }
   __syncthreads();
   const float sl2 = a.scale * kLog2e;
@@ -605,17 +621,21 @@ __global__ __launch_bounds__(512) void attn_bwd_q_bf16(AttnArgs a) {
     f32x4 dqt[HDP / 16];
 #pragma unroll
     for (int db = 0; db < HDP / 16; ++db) dqt[db] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    for (int t = 0; t < NKP / 32; ++t) {
+    for (int t = 0; t * 32 < NKP; ++t) {
       f32x4 ds[2];
+      const bool hi = (2 * t + 1) * 16 < NKP;  // the chunk's upper 16 keys are staged
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int ka = t * 32 + c * 16 + (lane & 15);
         f32x4 s_acc = {0.f, 0.f, 0.f, 0.f}, dp_acc = {0.f, 0.f, 0.f, 0.f};
+        if (c == 0 || hi) {
 #pragma unroll
-        for (int s = 0; s < HDP / 32; ++s) {
-          const int d = s * 32 + 8 * (lane >> 4);
-          s_acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(Ks + ka * ST + d), qf[s], s_acc, 0, 0, 0);
-          dp_acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(Vs + ka * ST + d), dof[s], dp_acc, 0, 0, 0);
+          for (int s = 0; s < HDP / 32; ++s) {
+            const int d = s * 32 + 8 * (lane >> 4);
+            const int ko = SW ? swz_off(ka, d) : ka * ST + d;
+            s_acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(Ks + ko), qf[s], s_acc, 0, 0, 0);
+            dp_acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(Vs + ko), dof[s], dp_acc, 0, 0, 0);
+          }
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -629,7 +649,8 @@ __global__ __launch_bounds__(512) void attn_bwd_q_bf16(AttnArgs a) {
       const bf16x8 dsb = pack8(ds[0], ds[1]);
 #pragma unroll
       for (int db = 0; db < HDP / 16; ++db)
-        dqt[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_read8(Ks, ST, t * 32, db * 16, lane), dsb, dqt[db], 0, 0, 0);
+        dqt[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            SW ? tr_read8_sw(Ks, t * 32, db * 16, lane, hi) : tr_read8(Ks, ST, t * 32, db * 16, lane), dsb, dqt[db], 0, 0, 0);
     }
     if (ql < a.Nq) {
       bf16* dqrow = (bf16*)a.dq + (int64_t)b * a.dq_bs + (int64_t)ql * a.dq_rs + hoff;
@@ -1045,7 +1066,7 @@ extern "C" int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int h
   int rc2 = CAPK_OK;
   {
     // split backward: dK/dV kernel, then dQ kernel (two head images in LDS each)
-    const size_t s1 = bwd_kv_smem(Nq, hdp), s2 = fwd_smem(Nk, hdp);
+    const size_t s1 = bwd_kv_smem(Nq, hdp), s2 = fwd_kernel_smem(Nk, hdp);
     // (measured: ViT N=197 bwd 554 -> 460 us; for Nq <= 32 the second launch costs more than it saves)
     if (Nq > 32 && s1 <= 80 * 1024 && s2 <= 80 * 1024) {
       static const int wpe = [] { const char* e = getenv("CAPK_ATTN_WPE"); return e ? atoi(e) : 4; }();

@@ -144,3 +144,42 @@ def time_cpu_scst(state_dict, images=2, max_length=20, threads=None, eos=50256, 
             otrain.adamw_step(p, p.grad, m, v, 1, 5e-5, 0.0 if otrain.no_decay(n) else 0.01)
     dt = time.perf_counter() - t0
     return images / dt, dt
+
+
+def time_cpu_config2(state_dict, batch=2, steps=1, warmup=1, pad=50256, threads=None):
+    """Images/s of the oracle CPU CE train step for config 2 (ResNet-101 + LSTM(768, 6 layers)
+    + soft attention, train-mode BatchNorm) on a bounded sample -- the same
+    _train_epoch body as time_cpu_baseline (src/train/trainer.py:218-289)."""
+    from . import lstm as olstm
+    if threads:
+        torch.set_num_threads(threads)
+    params = make_params(state_dict)
+    state = {k: v.detach().clone() for k, v in state_dict.items()}
+    opt_state = {}
+    g = torch.Generator().manual_seed(0)
+    images = torch.randn(batch, 3, 224, 224, generator=g)
+    caps = torch.randint(0, pad, (batch, 20), generator=torch.Generator().manual_seed(1))
+
+    def one(step):
+        for p in params.values():
+            p.grad = None
+        enc = oenc.resnet_encoder(_sub(params, "encoder."), images, [256, 512, 1024, 2048], [3, 4, 23, 3],
+                                  training=True, state=_sub(state, "encoder."))
+        logits, _ = olstm.lstm_decoder(_sub(params, "decoder."), enc["features"], enc["pooled_features"], caps, 6,
+                                       "soft")
+        loss = otrain.shifted_ce(logits, caps, pad)
+        loss.backward()
+        with torch.no_grad():
+            for n, p in params.items():
+                if p.grad is None:
+                    continue
+                m, v = opt_state.setdefault(n, (torch.zeros_like(p), torch.zeros_like(p)))
+                otrain.adamw_step(p, p.grad, m, v, step, 5e-5, 0.0 if otrain.no_decay(n) else 0.01)
+
+    for i in range(warmup):
+        one(i + 1)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        one(warmup + i + 1)
+    dt = time.perf_counter() - t0
+    return batch * steps / dt, dt

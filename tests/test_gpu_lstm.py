@@ -124,3 +124,63 @@ def test_lstm_bf16_close_and_trains(name):
         opt.step(lr=3e-3)
         losses.append(float(loss))
     assert all(np.isfinite(losses)) and losses[-1] < losses[0] * 0.9, losses
+
+
+def _full_lstm(precision, kind="soft", heads=1, seed=21):
+    """Config-2 decoder geometry: LSTM 768 hidden x 6 layers (DecoderConfig defaults),
+    soft attention over the 49 ResNet feature keys, GPT-2 vocabulary."""
+    import capk
+    from capk import config as C
+    from capk.models.decoders import build_decoder
+    torch.manual_seed(seed)
+    V, pad = 50257, 50256
+    dec = build_decoder(C.DecoderConfig(decoder_type="lstm", hidden_dim=768, num_layers=6, num_heads=heads),
+                        C.AttentionConfig(attention_type=kind, num_heads=heads), V, pad, pad, pad)
+    sd = {k: v.detach().clone() for k, v in dec.state_dict().items()}
+    capk.prepare(dec, "cuda", precision)
+    dec.eval()
+    return dec, sd
+
+
+@cuda
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-3), ("bf16", 3e-2)])
+def test_lstm_full_size_vs_oracle(precision, tol):
+    """768 hidden, 6 layers, 49 keys, batch 8, 20 tokens vs oracle/lstm.py (fp32 CPU):
+    logits and attention weights within the north-star 1e-3 (fp32) / 3e-2 (bf16) relative;
+    fp32 gradients of features, pooled and the LSTM / attention weights within 1e-3."""
+    from oracle import lstm as olstm
+    from capk.train import CombinedLoss
+    dec, sd = _full_lstm(precision)
+    B, T, S, D = 8, 20, 49, 768
+    g = torch.Generator().manual_seed(2)
+    feats = torch.randn(B, S, D, generator=g)
+    pooled = torch.randn(B, D, generator=g)
+    caps = torch.randint(0, 50256, (B, T), generator=g)
+    dt = torch.float32 if precision == "fp32" else torch.bfloat16
+    fg = feats.cuda().to(dt).requires_grad_(True)
+    pg = pooled.cuda().to(dt).requires_grad_(True)
+    out = dec({"features": fg, "pooled_features": pg, "attention_mask": None}, caps.cuda())
+    p = {k: v.float().requires_grad_(True) for k, v in sd.items()}
+    fr = fg.detach().float().cpu().requires_grad_(True)
+    pr = pg.detach().float().cpu().requires_grad_(True)
+    ref_logits, ref_w = olstm.lstm_decoder(p, fr, pr, caps, 6, "soft")
+
+    def rel(a, b):
+        return float((a.detach().float().cpu() - b.detach()).norm() / b.detach().norm())
+
+    assert rel(out["logits"], ref_logits) < tol
+    assert rel(out["attention_weights"], ref_w) < tol
+    if precision == "fp32":
+        loss = CombinedLoss(50256)(logits=out["logits"], targets=caps.cuda())["total_loss"]
+        loss.backward()
+        from oracle.train import shifted_ce
+        ref_loss = shifted_ce(ref_logits, caps, 50256)
+        ref_loss.backward()
+        assert abs(float(loss) - float(ref_loss)) < 1e-4 * abs(float(ref_loss))
+        assert rel(fg.grad, fr.grad) < 1e-3 and rel(pg.grad, pr.grad) < 1e-3
+        for n, prm in dec.named_parameters():
+            if p[n].grad is not None:  # (the attention energy bias shifts every key equally: its
+                # true gradient is 0 and both sides hold rounding noise -> absolute floor)
+                ref = p[n].grad
+                err = float((prm._capk_grad.float().cpu() - ref).norm())
+                assert err <= 1e-3 * float(ref.norm()) + 1e-6, (n, err, float(ref.norm()))

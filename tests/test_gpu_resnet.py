@@ -326,3 +326,44 @@ def test_resnet_lstm_bf16_train_steps_reduce_loss():
         opt.step()
         losses.append(float(loss.detach()))
     assert all(np.isfinite(losses)) and losses[-1] < losses[0], losses
+
+
+@cuda
+def test_resnet101_bf16_every_bottleneck_local_vs_oracle():
+    """bf16 local check of all 33 ResNet-101 bottlenecks (+ the stem): each capk block gets
+    the fp32 oracle's input to that block (rounded to bf16) and its output is compared with
+    the oracle block on the same input -- the per-block bf16 error, free of the drift that
+    train-mode BatchNorm amplifies across a random-init network (stated tolerance 3e-2)."""
+    from capk.models import resnet as R
+    from oracle import encoders as oenc
+    torch.manual_seed(11)
+    arch = R.RESNET_ARCHS["microsoft/resnet-101"]
+    m = R.CapkResNetModel(arch)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    import capk
+    capk.prepare(m, "cuda", "bf16")
+    m.train()
+    B = 2
+    images = torch.randn(B, 3, 224, 224)
+    st = {k: v.clone() for k, v in sd.items()}
+    errs = []
+    with torch.no_grad():
+        x, H, W = m.embedder(images.cuda())
+        r = F.max_pool2d(oenc._conv_bn(sd, "embedder.embedder.", images, 2, True, True, st), 3, 2, 1)
+        errs.append(("stem", _rel(x, _nhwc(r))))
+        for si, depth in enumerate([3, 4, 23, 3]):
+            for li in range(depth):
+                H, W = r.shape[2], r.shape[3]
+                xin = _nhwc(r).cuda().bfloat16()
+                y, _, _ = m.encoder.stages[si].layers[li](xin, B, H, W)
+                pre = f"encoder.stages.{si}.layers.{li}."
+                stride = (2 if si > 0 else 1) if li == 0 else 1
+                h = oenc._conv_bn(sd, pre + "layer.0.", r, 1, True, True, st)
+                h = oenc._conv_bn(sd, pre + "layer.1.", h, stride, True, True, st)
+                h = oenc._conv_bn(sd, pre + "layer.2.", h, 1, True, False, st)
+                rr = oenc._conv_bn(sd, pre + "shortcut.", r, stride, True, False, st) if li == 0 else r
+                r = F.relu(h + rr)
+                errs.append((pre, _rel(y, _nhwc(r))))
+    assert len(errs) == 34
+    bad = [(n, e) for n, e in errs if not e < 3e-2]
+    assert not bad, bad
