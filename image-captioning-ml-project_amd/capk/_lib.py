@@ -94,6 +94,7 @@ SIGNATURES = {
     "capk_beam_finalize": (_i, [_i, _i, _i, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "capk_argmax_rows": (_i, [_i, _i, _i, _i64, _c_p, _c_p, _i64, _c_p]),
     "capk_sample_rows": (_i, [_i, _i, _i, _i64, _c_p, _u32, _i, _c_p, _i64, _c_p, _c_p]),
+    "capk_sample_rows_dev": (_i, [_i, _i, _i, _i64, _c_p, _c_p, _i, _c_p, _i64, _c_p, _c_p]),
     "capk_gather_rows": (_i, [_i, _i, _i, _i, _c_p, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p]),
     "capk_im2col": (_i, [_i, _i, _i, _i, _i, _i, _i64, _i64, _i64, _i64, _i, _i, _i, _i, _i, _i, _i, _c_p, _c_p,
                          _c_p]),

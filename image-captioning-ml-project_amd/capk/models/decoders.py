@@ -61,13 +61,20 @@ class TransformerDecoder(TransformerDecoderCore, CaptionDecoder):
         feats = encoder_features["features"]
         B = feats.shape[0]
         if num_beams > 1:
+            from .. import graphs
             from ..beam import beam_search
-            from .transformer import KVDecodeRunner
-            runner = KVDecodeRunner(self, feats, num_beams, max_length)
+            from .transformer import KVDecodeRunner, _mem_geometry
             prompt = torch.full((B,), self.bos_token_id, dtype=torch.long, device=feats.device)
-            out = beam_search(runner.step, B, num_beams, max_length, prompt, self.eos_token_id,
-                              pad_token_id=self.pad_token_id, length_penalty=length_penalty,
-                              early_stopping=early_stopping, vocab_size=self.vocab_size)
+            kw = dict(pad_token_id=self.pad_token_id, length_penalty=length_penalty, early_stopping=early_stopping,
+                      vocab_size=self.vocab_size)
+            if graphs.active():  # cached runner, steps replayed as HIP graphs (capk/graphs.py)
+                key = ("tdec", tuple(feats.shape), _mem_geometry(feats)[1], feats.dtype, num_beams, max_length)
+                runner = graphs.runner_for(self, key, lambda: KVDecodeRunner(self, feats, num_beams, max_length))
+                runner.load(feats)
+                out = graphs.beam_generate(runner, B, num_beams, max_length, prompt, self.eos_token_id, **kw)
+            else:
+                runner = KVDecodeRunner(self, feats, num_beams, max_length)
+                out = beam_search(runner.step, B, num_beams, max_length, prompt, self.eos_token_id, **kw)
             return out["sequences"], {"sequences_scores": out["sequences_scores"],
                                       "beam_indices": out["beam_indices"]}
         # greedy on the KV-cached decode step: the same per-position arithmetic as the
@@ -140,15 +147,22 @@ class GPT2Decoder(GPT2DecoderCore, CaptionDecoder):
         if num_beams < 2:
             raise NotImplementedError("capk GPT2Decoder.generate: greedy (num_beams=1) is not on the hot path; "
                                       "the reference always beam-searches (decoders.py:623)")
+        from .. import graphs
         from ..beam import beam_search
         from .gpt2 import GPT2KVRunner
         pooled = encoder_features["pooled_features"]
         B = pooled.shape[0]
-        runner = GPT2KVRunner(self, pooled, num_beams, max_length)
         prompt = torch.full((B,), self.bos_token_id, dtype=torch.long, device=pooled.device)
-        out = beam_search(runner.step, B, num_beams, max_length, prompt, self.eos_token_id,
-                          pad_token_id=self.pad_token_id, length_penalty=length_penalty,
-                          early_stopping=early_stopping, vocab_size=self.vocab_size)
+        kw = dict(pad_token_id=self.pad_token_id, length_penalty=length_penalty, early_stopping=early_stopping,
+                  vocab_size=self.vocab_size)
+        if graphs.active():  # cached runner, steps replayed as HIP graphs (capk/graphs.py)
+            key = ("gpt2", B, pooled.dtype, num_beams, max_length)
+            runner = graphs.runner_for(self, key, lambda: GPT2KVRunner(self, pooled, num_beams, max_length))
+            runner.load(pooled)
+            out = graphs.beam_generate(runner, B, num_beams, max_length, prompt, self.eos_token_id, **kw)
+        else:
+            runner = GPT2KVRunner(self, pooled, num_beams, max_length)
+            out = beam_search(runner.step, B, num_beams, max_length, prompt, self.eos_token_id, **kw)
         return out["sequences"], {"sequences_scores": out["sequences_scores"], "beam_indices": out["beam_indices"]}
 
 

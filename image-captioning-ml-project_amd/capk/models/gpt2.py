@@ -323,27 +323,37 @@ class GPT2KVRunner:
         self.P, self.Lc = P, P + max_length
         if P + max_length > c.n_positions:
             raise ValueError(f"capk GPT2 generate: 10 + max_length exceeds n_positions {c.n_positions}")
-        if pooled.dtype != dt:
-            raise TypeError(f"capk GPT2Decoder: pooled dtype {pooled.dtype} != compute dtype {dt}")
         dev = pooled.device
-        itp = m.image_to_prefix
-        prefix = ops.linear(pooled.contiguous(), W(itp.weight, dt), itp.bias.detach())  # [B, P*D]
         R = B * num_beams
         self.R = R
-        rep_idx = torch.arange(R, dtype=torch.int32, device=dev) // num_beams
-        pref_rep = torch.empty(R, P * D, dtype=dt, device=dev)
-        ops.gather_rows(prefix, rep_idx, pref_rep, 1, R, P * D, P * D, 0, P * D, 0)
-        nl = c.n_layer
-        shape = (nl, R, self.Lc, 3 * D)
-        self.cache = torch.empty(shape, dtype=dt, device=dev)
-        self.spare = torch.empty(shape, dtype=dt, device=dev)
-        idxP = _arange_i32(P, dev)
-        Lc3 = self.Lc * 3 * D
-        for li in range(nl):
-            for slot in (1, 2):  # K and V slots of the prefix rows
-                ops.gather_rows(pref_rep, idxP, self.cache[li], R, P, D, D, P * D, 3 * D, Lc3, y_off=slot * D)
+        shape = (c.n_layer, R, self.Lc, 3 * D)
+        self._bufs = (torch.empty(shape, dtype=dt, device=dev), torch.empty(shape, dtype=dt, device=dev))
+        self.pref_rep = torch.empty(R, P * D, dtype=dt, device=dev)
+        self.rep_idx = torch.arange(R, dtype=torch.int32, device=dev) // num_beams
         wte = m.model.transformer.wte.weight
         self.wout = wte._capk_pad_bf16 if dt == torch.bfloat16 else wte._capk_pad_master
+        self.load(pooled)
+
+    def load(self, pooled):
+        """Per-call state, written in place (a runner reused by capk.graphs keeps its buffers):
+        the image prefix into the K/V slots of the first 10 rows of every layer's cache."""
+        m, dt, P, D, R = self.m, self.dt, self.P, self.D, self.R
+        if pooled.dtype != dt:
+            raise TypeError(f"capk GPT2Decoder: pooled dtype {pooled.dtype} != compute dtype {dt}")
+        if pooled.shape[0] != self.B:
+            raise ValueError("capk GPT2KVRunner.load: batch size differs from the runner's")
+        itp = m.image_to_prefix
+        prefix = ops.linear(pooled.contiguous(), W(itp.weight, dt), itp.bias.detach())  # [B, P*D]
+        ops.gather_rows(prefix, self.rep_idx, self.pref_rep, 1, R, P * D, P * D, 0, P * D, 0)
+        self.reset()
+        idxP = _arange_i32(P, pooled.device)
+        Lc3 = self.Lc * 3 * D
+        for li in range(self.cache.shape[0]):
+            for slot in (1, 2):  # K and V slots of the prefix rows
+                ops.gather_rows(self.pref_rep, idxP, self.cache[li], R, P, D, D, P * D, 3 * D, Lc3, y_off=slot * D)
+
+    def reset(self):
+        self.cache, self.spare = self._bufs
 
     def step(self, cur_len, ids, reorder_idx):
         m, dt, D, H, hd, R, P = self.m, self.dt, self.D, self.H, self.hd, self.R, self.P

@@ -314,24 +314,37 @@ class KVDecodeRunner:
         self.H = m.num_heads
         self.hd = D // self.H
         self.scale = 1.0 / math.sqrt(self.hd)
-        if features.dtype != dt:
-            raise TypeError(f"capk TransformerDecoder: features dtype {features.dtype} != compute dtype {dt}")
         feat_mem, self.rpb, _ = _mem_geometry(features)
-        vp = m.visual_projection
-        mem = ops.linear(feat_mem, W(vp.weight, dt), vp.bias.detach())
-        self.mem_kv = []
-        for L in m.transformer_decoder.layers:
-            ca = L.multihead_attn
-            self.mem_kv.append(ops.linear(mem, W(ca.in_proj_weight, dt)[D:], ca.in_proj_bias.detach()[D:]))
         nl = len(m.transformer_decoder.layers)
+        dev = features.device
+        self.mem_kv = [torch.empty(feat_mem.shape[0], 2 * D, dtype=dt, device=dev) for _ in range(nl)]
         R = B * num_beams
         self.R = R
         shape = (nl, R, max_length, 3 * D)
-        self.cache = torch.empty(shape, dtype=dt, device=features.device)
-        self.spare = torch.empty(shape, dtype=dt, device=features.device)
+        self._bufs = (torch.empty(shape, dtype=dt, device=dev), torch.empty(shape, dtype=dt, device=dev))
         ol = m.output_layer
         self.wout = ol.weight._capk_pad_bf16 if dt == torch.bfloat16 else ol.weight._capk_pad_master
         self.bout = _pad_bias(ol)
+        self.load(features)
+
+    def load(self, features):
+        """Per-call state, written in place (a runner reused by capk.graphs keeps its
+        buffers): the memory side -- visual projection and every layer's cross K/V."""
+        m, dt, D = self.m, self.dt, self.D
+        if features.dtype != dt:
+            raise TypeError(f"capk TransformerDecoder: features dtype {features.dtype} != compute dtype {dt}")
+        feat_mem, rpb, _ = _mem_geometry(features)
+        if tuple(features.shape) != (self.B, self.S, D) or rpb != self.rpb:
+            raise ValueError("capk KVDecodeRunner.load: feature geometry differs from the runner's")
+        vp = m.visual_projection
+        mem = ops.linear(feat_mem, W(vp.weight, dt), vp.bias.detach())
+        for li, L in enumerate(m.transformer_decoder.layers):
+            ca = L.multihead_attn
+            ops.linear(mem, W(ca.in_proj_weight, dt)[D:], ca.in_proj_bias.detach()[D:], out=self.mem_kv[li])
+        self.reset()
+
+    def reset(self):
+        self.cache, self.spare = self._bufs
 
     def reorder(self, idx, t):
         """Rows r <- idx[r] for cache positions [0, t) of every layer (one launch)."""

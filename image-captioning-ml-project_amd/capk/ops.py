@@ -93,7 +93,7 @@ def gemm(A, a_kmajor, B, b_kmajor, M, N, K, C, *, lda, ldb, ldc, alpha=1.0, beta
     it, ot = dtype_code(A), dtype_code(C)
     wsb = L.capk_gemm_workspace(it, ot, M, N, K)
     ws = _ws(wsb, A.device)
-    timed = GEMM_TIMER.enabled
+    timed = GEMM_TIMER.enabled and not torch.cuda.is_current_stream_capturing()
     if timed:
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
@@ -141,6 +141,16 @@ class Fp8State:
     def weights_changed(self):
         self.epoch += 1
 
+    def refresh(self):
+        """Re-quantise every cached weight copy that is stale (before a graph replay: a
+        captured graph holds the copies' addresses, never the quantisation itself)."""
+        if not self.enabled:
+            return
+        for key, ent in self.cache.items():  # ent = [epoch, q, scale, bf16 weight view]
+            if ent[0] != self.epoch:
+                quant_fp8(ent[3], transpose=key[3], q=ent[1], scale=ent[2])
+                ent[0] = self.epoch
+
     def is_weight(self, w):
         p = w.data_ptr()
         return any(a <= p < b for a, b in self.ranges)
@@ -173,7 +183,7 @@ def gemm_f8(a, sa, b, sb, C, *, beta=0.0, bias=None, residual=None, act=0, preac
     N = b.shape[0]
     wsb = L.capk_gemm_f8_workspace(M, N, K)
     ws = _ws(wsb, a.device)
-    timed = GEMM_TIMER.enabled
+    timed = GEMM_TIMER.enabled and not torch.cuda.is_current_stream_capturing()
     if timed:
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
@@ -203,9 +213,13 @@ def _fp8_route(x, w, M, N, K, act, transposed):
     key = (w.data_ptr(), tuple(w.shape), tuple(w.stride()), transposed)
     ent = FP8.cache.get(key)
     if ent is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise _lib.CapkError("capk fp8: weight copy created inside a graph capture (warm the path eagerly first)")
         ent = FP8.cache[key] = [-1, torch.empty(N, K, dtype=torch.uint8, device=w.device),
-                                torch.empty(N, dtype=torch.uint8, device=w.device)]
+                                torch.empty(N, dtype=torch.uint8, device=w.device), w]
     if ent[0] != FP8.epoch:
+        if torch.cuda.is_current_stream_capturing():
+            raise _lib.CapkError("capk fp8: stale weight copy inside a graph capture (call FP8.refresh() first)")
         quant_fp8(w, transpose=transposed, q=ent[1], scale=ent[2])
         ent[0] = FP8.epoch
     return ent[1], ent[2]
@@ -394,7 +408,14 @@ def shifted_ce(logits2d, targets, B, T, V, ignore_index, *, want_loss=True, dlog
 
 
 def sample_rows(logits, V, seed, step, out, logp=None):
-    """out[r] (int64 view, any stride) ~ Categorical(softmax(logits[r, :V])) with the counter-based uniform."""
+    """out[r] (int64 view, any stride) ~ Categorical(softmax(logits[r, :V])) with the counter-based uniform.
+    seed: an int, or a 1-element int32 device tensor read by the kernel (graph replay)."""
+    if torch.is_tensor(seed):
+        _need_gpu(seed)
+        check(lib().capk_sample_rows_dev(dtype_code(logits), logits.shape[0], V, logits.stride(0), _p(logits),
+                                         _p(seed), int(step), _p(out), out.stride(0), _p(logp), _stream()),
+              "capk_sample_rows_dev")
+        return out
     check(lib().capk_sample_rows(dtype_code(logits), logits.shape[0], V, logits.stride(0), _p(logits),
                                  int(seed) & 0xFFFFFFFF, int(step), _p(out), out.stride(0), _p(logp), _stream()),
           "capk_sample_rows")

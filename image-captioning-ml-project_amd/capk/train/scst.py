@@ -98,19 +98,32 @@ def sample_captions(decoder, encoder_features, max_length, seed, check_every=EOS
     the host only every `check_every` steps: the uniforms are counter-based per
     (seed, step, row), so steps sampled past the stop are simply cut off and the result
     equals a per-step check, without a host sync per token."""
+    from .. import graphs
     from ..models.decoders import GPT2Decoder, TransformerDecoder
     if isinstance(decoder, TransformerDecoder):
-        from ..models.transformer import KVDecodeRunner
+        from ..models.transformer import KVDecodeRunner, _mem_geometry
         feats = encoder_features["features"]
-        runner = KVDecodeRunner(decoder, feats, 1, max_length)
-        B, dev = feats.shape[0], feats.device
+        make = lambda: KVDecodeRunner(decoder, feats, 1, max_length)  # noqa: E731
+        key = ("tdec", tuple(feats.shape), _mem_geometry(feats)[1], feats.dtype, 1, max_length)
+        src = feats
     elif isinstance(decoder, GPT2Decoder):
         from ..models.gpt2 import GPT2KVRunner
         pooled = encoder_features["pooled_features"]
-        runner = GPT2KVRunner(decoder, pooled, 1, max_length)
-        B, dev = pooled.shape[0], pooled.device
+        make = lambda: GPT2KVRunner(decoder, pooled, 1, max_length)  # noqa: E731
+        key = ("gpt2", pooled.shape[0], pooled.dtype, 1, max_length)
+        src = pooled
     else:
         raise NotImplementedError(f"capk SCST sampler: {type(decoder).__name__} (Transformer / GPT-2 decoders)")
+    if graphs.active():  # cached runner, chunks of steps replayed as HIP graphs (capk/graphs.py)
+        runner = graphs.runner_for(decoder, ("sample",) + key, make)
+        runner.load(src)
+        if runner.warm:
+            ids, logp, steps = graphs.sample_generate(runner, decoder, max_length, seed, check_every)
+            return ids[:, :steps + 1].clone(), logp[:steps].t().clone()
+        runner.warm = True
+    else:
+        runner = make()
+    B, dev = src.shape[0], src.device
     ids = torch.empty(B, max_length, dtype=torch.long, device=dev)
     ids[:, 0] = decoder.bos_token_id
     logp = torch.empty(max_length - 1, B, dtype=torch.float32, device=dev)

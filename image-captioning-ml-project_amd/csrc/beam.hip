@@ -137,9 +137,16 @@ __device__ __forceinline__ int wave_compact(uint64_t* wb, int cnt, int K2, int l
 template <typename T>
 __global__ __launch_bounds__(ROWS_THREADS) void beam_rows_kernel(const T* __restrict__ logits, int64_t ld, int V,
                                                                  int K2, int* flags, float* cand_val, int* cand_tok,
-                                                                 float* row_max, float* row_logsum) {
+                                                                 float* row_max, float* row_logsum, int cur_len,
+                                                                 int early_true) {
   const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (r == 0 && tid < 4) flags[tid] = 0;
+  if (r == 0 && tid == 0) {
+    // HF's batch-global stopping rule on the previous step's flags, made sticky in flags[3]:
+    // a replayed chunk of steps (capk/graphs.py) that runs past the host's stop point then
+    // leaves the search state untouched (beam_update_kernel returns at once).
+    if (cur_len > 1 && !(flags[0] && !(early_true && !flags[1]) && flags[2])) flags[3] = 1;
+    flags[0] = flags[1] = flags[2] = 0;
+  }
   const T* x = logits + (int64_t)r * ld;
   __shared__ uint64_t wbuf[4][WAVE_CAP];
   __shared__ float sm[4], ss[4];
@@ -241,6 +248,7 @@ __global__ __launch_bounds__(64) void beam_update_kernel(BeamState st, int k, in
                                                          const float* __restrict__ row_logsum, int* reorder,
                                                          int64_t* next_ids) {
   const int b = blockIdx.x, lane = threadIdx.x;
+  if (st.flags[3]) return;  // the search already stopped (see beam_rows_kernel)
   const int K2 = 2 * k, Lb = L - 1;
   extern __shared__ int sh[];
   int* o_rseq = sh;                       // [k][L]
@@ -395,6 +403,7 @@ __global__ __launch_bounds__(64) void beam_update_kernel(BeamState st, int k, in
 
 __global__ void beam_init_kernel(BeamState st, int B, int k, int L, const int64_t* prompt, int fill) {
   const int64_t n = (int64_t)B * k * L;
+  if (blockIdx.x == 0 && threadIdx.x < 4) st.flags[threadIdx.x] = 0;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
     const int p = (int)(e % L);
     const int b = (int)(e / ((int64_t)k * L));
@@ -473,7 +482,8 @@ __global__ __launch_bounds__(256) void argmax_rows_kernel(const T* __restrict__ 
 __global__ __launch_bounds__(256) void sample_rows_kernel_f32(const float* __restrict__ x0, int64_t ld, int V,
                                                               uint32_t seed, int step, int64_t* __restrict__ out,
                                                               int64_t out_stride, float* __restrict__ logp,
-                                                              int is_bf16) {
+                                                              int is_bf16, const uint32_t* __restrict__ seedp) {
+  if (seedp) seed = *seedp;
   const int r = blockIdx.x, tid = threadIdx.x;
   const int chunk = (V + 255) / 256;
   const int lo = tid * chunk, hi = min(V, lo + chunk);
@@ -521,7 +531,9 @@ __global__ __launch_bounds__(256) void sample_rows_kernel_f32(const float* __res
 constexpr int SAMPLE_LDS_MAX = 65536;  // 128 KiB of LDS
 __global__ __launch_bounds__(256) void sample_rows_lds_kernel(const bf16* __restrict__ x0, int64_t ld, int V,
                                                               uint32_t seed, int step, int64_t* __restrict__ out,
-                                                              int64_t out_stride, float* __restrict__ logp) {
+                                                              int64_t out_stride, float* __restrict__ logp,
+                                                              const uint32_t* __restrict__ seedp) {
+  if (seedp) seed = *seedp;
   extern __shared__ __attribute__((aligned(16))) char dyn[];
   bf16* row = (bf16*)dyn;
   const int r = blockIdx.x, tid = threadIdx.x;
@@ -619,10 +631,12 @@ extern "C" int capk_beam_step(int dtype, int B, int num_beams, int max_length, i
   hipStream_t s = S(stream);
   if (dtype == CAPK_F32)
     hipLaunchKernelGGL(beam_rows_kernel<float>, dim3((unsigned)Bk), dim3(ROWS_THREADS), 0, s, (const float*)logits,
-                       ld, V, 2 * k, st.flags, cand_val, cand_tok, row_max, row_logsum);
+                       ld, V, 2 * k, st.flags, cand_val, cand_tok, row_max, row_logsum, cur_len,
+                       early_stopping == 1 ? 1 : 0);
   else
     hipLaunchKernelGGL(beam_rows_kernel<bf16>, dim3((unsigned)Bk), dim3(ROWS_THREADS), 0, s, (const bf16*)logits,
-                       ld, V, 2 * k, st.flags, cand_val, cand_tok, row_max, row_logsum);
+                       ld, V, 2 * k, st.flags, cand_val, cand_tok, row_max, row_logsum, cur_len,
+                       early_stopping == 1 ? 1 : 0);
   CAPK_LAUNCH_CHECK("beam_rows_kernel");
   const size_t lds = (size_t)(2 * k * L + 2 * k * (L - 1)) * sizeof(int);
   hipLaunchKernelGGL(beam_update_kernel, dim3(B), dim3(64), lds, s, st, k, L, V, cur_len, (int)eos, fin_div,
@@ -682,8 +696,9 @@ extern "C" int capk_argmax_rows(int dtype, int rows, int V, int64_t ld, const vo
   return CAPK_OK;
 }
 
-extern "C" int capk_sample_rows(int dtype, int rows, int V, int64_t ld, const void* logits, uint32_t seed, int step,
-                                int64_t* out, int64_t out_stride, float* logp, void* stream) {
+static int sample_rows_launch(int dtype, int rows, int V, int64_t ld, const void* logits, uint32_t seed,
+                              const uint32_t* seedp, int step, int64_t* out, int64_t out_stride, float* logp,
+                              void* stream) {
   CAPK_CHECK_ARG(rows > 0 && V > 0 && ld >= V && (dtype == CAPK_F32 || dtype == CAPK_BF16),
                  "capk_sample_rows: bad arguments");
   if (dtype == CAPK_BF16 && V <= SAMPLE_LDS_MAX && ld % 8 == 0 && (uintptr_t)logits % 16 == 0) {
@@ -693,11 +708,22 @@ extern "C" int capk_sample_rows(int dtype, int rows, int V, int64_t ld, const vo
                                                        SAMPLE_LDS_MAX * (int)sizeof(bf16));
     if (attr != hipSuccess) return hip_status(attr, "capk_sample_rows: hipFuncSetAttribute");
     hipLaunchKernelGGL(sample_rows_lds_kernel, dim3(rows), dim3(256), lds, S(stream), (const bf16*)logits, ld, V, seed,
-                       step, out, out_stride, logp);
+                       step, out, out_stride, logp, seedp);
   } else {
     hipLaunchKernelGGL(sample_rows_kernel_f32, dim3(rows), dim3(256), 0, S(stream), (const float*)logits, ld, V, seed,
-                       step, out, out_stride, logp, dtype == CAPK_BF16 ? 1 : 0);
+                       step, out, out_stride, logp, dtype == CAPK_BF16 ? 1 : 0, seedp);
   }
   CAPK_LAUNCH_CHECK("sample_rows_kernel");
   return CAPK_OK;
+}
+
+extern "C" int capk_sample_rows(int dtype, int rows, int V, int64_t ld, const void* logits, uint32_t seed, int step,
+                                int64_t* out, int64_t out_stride, float* logp, void* stream) {
+  return sample_rows_launch(dtype, rows, V, ld, logits, seed, nullptr, step, out, out_stride, logp, stream);
+}
+
+extern "C" int capk_sample_rows_dev(int dtype, int rows, int V, int64_t ld, const void* logits, const uint32_t* seed,
+                                    int step, int64_t* out, int64_t out_stride, float* logp, void* stream) {
+  CAPK_CHECK_ARG(seed != nullptr, "capk_sample_rows_dev: null seed");
+  return sample_rows_launch(dtype, rows, V, ld, logits, 0u, seed, step, out, out_stride, logp, stream);
 }

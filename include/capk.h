@@ -290,6 +290,10 @@ int capk_argmax_rows(int dtype, int rows, int V, int64_t ld, const void* x, int6
  * = token, logp[r] (optional) = its log-probability.  SCST sampler (trainer.py:383-438). */
 int capk_sample_rows(int dtype, int rows, int V, int64_t ld, const void* logits, uint32_t seed, int step,
                      int64_t* out, int64_t out_stride, float* logp, void* stream);
+/* capk_sample_rows with the seed read from device memory (a replayed HIP graph of the
+ * sampling loop keeps its kernel arguments; capk/graphs.py writes the seed before replay). */
+int capk_sample_rows_dev(int dtype, int rows, int V, int64_t ld, const void* logits, const uint32_t* seed,
+                         int step, int64_t* out, int64_t out_stride, float* logp, void* stream);
 /* y[g][r] = x[g][idx[r]] row gather over G groups (KV-cache reorder after a beam
  * step, all layers in one launch; HF Cache.reorder_cache = index_select on dim 0). */
 int capk_gather_rows(int dtype, int groups, int rows, int cols, const int32_t* idx, const void* x, int64_t ldx,
