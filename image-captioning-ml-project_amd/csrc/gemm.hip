@@ -329,18 +329,26 @@ static int choose_cfg(int M, int N, int K, int a_kmajor, int b_kmajor, int act) 
       return 5;
     }
   }
-  if (act && (a_kmajor || b_kmajor) && K % 32 == 0) return 4;
+  // (decode-step rows, M < 2048: the 2-WG/CU BK-64 ring measured faster with an activation too)
+  if (act && (a_kmajor || b_kmajor) && K % 32 == 0 && M >= 2048) return 4;
   if (!a_kmajor && !b_kmajor && tiles_of(4, M, N) < slots_of(4)) return 1;  // split-K dW (cfg 4 measured slower)
   return 1;
 }
 // Split-K factor: fill one round of resident workgroups when the tile grid alone cannot
 // (any integer factor; every split keeps >= 4 K-tiles).
 static int choose_splits(int cfg, int M, int N, int K) {
+  static const int max_split = [] {  // A/B control (tools/gemm_bench.py): CAPK_GEMM_MAXSPLIT=1 disables split-K
+    const char* v = getenv("CAPK_GEMM_MAXSPLIT");
+    return v ? std::max(1, atoi(v)) : 16;
+  }();
   const int bk = (cfg == 3 || cfg == 4) ? 32 : 64;
   const int tiles = tiles_of(cfg, M, N), slots = slots_of(cfg);
   const int nk = cdiv(K, bk);
   if (2 * tiles >= slots) return 1;
-  int s = std::min(16, slots / tiles);
+  // decode-step shapes (tools/gemm_bench.py dec*, graph-timed): with >= 128 tiles, or >= 48
+  // on a short K, the separate reduce launch costs more than the split saves
+  if (tiles >= 128 || (K < 2048 && tiles > 48)) return 1;
+  int s = std::min(max_split, slots / tiles);
   s = std::min(s, std::max(1, nk / 4));
   return std::max(1, s);
 }

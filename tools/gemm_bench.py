@@ -29,6 +29,13 @@ SHAPES = [  # name, M, N, K, kind
     ("f8_lm_head", 5120, 50304, 768, "f8"), ("f8_lm_head_beam5", 1280, 50304, 768, "f8"),
     ("f8_big", 16384, 16384, 8192, "f8"), ("bf16_big", 16384, 16384, 8192, "fwd"),
     ("f8_quant_x", 12800, 3072, 768, "quant"),
+    # decode steps (GPT-2 Conv1D weights N-major: "c1d"): rows = beams in flight
+    ("dec256_cattn", 256, 2304, 768, "c1d"), ("dec256_cproj", 256, 768, 768, "c1d"),
+    ("dec256_fc", 256, 3072, 768, "c1d_gelu"), ("dec256_proj2", 256, 768, 3072, "c1d"),
+    ("dec1280_cattn", 1280, 2304, 768, "c1d"), ("dec1280_cproj", 1280, 768, 768, "c1d"),
+    ("dec1280_fc", 1280, 3072, 768, "c1d_gelu"), ("dec1280_proj2", 1280, 768, 3072, "c1d"),
+    ("tdec1280_qkv", 1280, 2304, 768, "fwd"), ("tdec1280_fc1", 1280, 3072, 768, "fwd_gelu"),
+    ("tdec1280_fc2", 1280, 768, 3072, "fwd"),
 ]
 
 
@@ -45,6 +52,13 @@ def run(name, M, N, K, kind, iters=20):
         q = torch.empty(M, N, device=dev, dtype=torch.uint8)
         sc = torch.empty(M, device=dev, dtype=torch.uint8)
         fn = lambda: ops.quant_fp8(x, q=q, scale=sc)
+    elif kind.startswith("c1d"):  # GPT-2 Conv1D: y = x @ W, W [K, N] (N-major B)
+        from capk._lib import ACT_GELU_TANH
+        x = torch.randn(M, K, device=dev, generator=g).bfloat16()
+        w = (torch.randn(K, N, device=dev, generator=g) * 0.02).bfloat16()
+        b = torch.zeros(N, device=dev)
+        act = ACT_GELU_TANH if "gelu" in kind else 0
+        fn = lambda: ops.conv1d(x, w, b, act=act)
     elif kind.startswith("fwd"):
         x = torch.randn(M, K, device=dev, generator=g).bfloat16()
         w = (torch.randn(N, K, device=dev, generator=g) * 0.02).bfloat16()
@@ -68,10 +82,21 @@ def run(name, M, N, K, kind, iters=20):
         fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(iters):
-        fn()
-    e1.record()
+    if os.environ.get("GEMM_GRAPH") == "1":  # GPU time only: the iterations replayed as one HIP graph
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            for _ in range(iters):
+                fn()
+        gr.replay()
+        torch.cuda.synchronize()
+        e0.record()
+        gr.replay()
+        e1.record()
+    else:
+        e0.record()
+        for _ in range(iters):
+            fn()
+        e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / iters
     tf = 2.0 * M * N * K / (ms * 1e-3) / 1e12
