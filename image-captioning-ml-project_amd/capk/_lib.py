@@ -35,6 +35,8 @@ SIGNATURES = {
     "capk_gemm_last_route": (_i, []),
     "capk_gemm_last_config": (_i, []),
     "capk_gemm_force_config": (_i, [_i, _i]),
+    "capk_image_desc_bytes": (_sz, []),
+    "capk_resize_normalize": (_i, [_i, _i, _i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "capk_quant_fp8_workspace": (_sz, [_i, _i, _i]),
     "capk_quant_fp8": (_i, [_i, _i, _i, _c_p, _i64, _i, _c_p, _i64, _c_p, _c_p, _sz, _c_p]),
     "capk_gemm_f8_workspace": (_sz, [_i, _i, _i]),
