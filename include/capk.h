@@ -290,6 +290,17 @@ int capk_argmax_rows(int dtype, int rows, int V, int64_t ld, const void* x, int6
  * = token, logp[r] (optional) = its log-probability.  SCST sampler (trainer.py:383-438). */
 int capk_sample_rows(int dtype, int rows, int V, int64_t ld, const void* logits, uint32_t seed, int step,
                      int64_t* out, int64_t out_stride, float* logp, void* stream);
+/* ------------------------------------------------------ input pipeline -----
+ * The reference's torchvision transforms on PIL images (src/main.py:139-153;
+ * src/data/dataset.py:105-112): per image of a packed uint8 RGB HWC buffer, crop
+ * (cy, cx, ch, cw) -> Pillow-exact antialiased bilinear resize to (rh, rw) -> the size x size
+ * window at (oy, ox) -> optional horizontal flip -> x / 255 -> (x - mean) / std, written
+ * [B, 3, size, size] (out_dtype CAPK_F32 / CAPK_BF16).  desc = B packed descriptors
+ * {int64 offset; int32 H, W, cy, cx, ch, cw, rh, rw, oy, ox, flip} of
+ * capk_image_desc_bytes() bytes each; downscale per axis <= 31x. */
+size_t capk_image_desc_bytes(void);
+int capk_resize_normalize(int out_dtype, int B, int size, const void* images, const void* desc,
+                          const float* mean, const float* stdv, void* out, void* stream);
 /* capk_sample_rows with the seed read from device memory (a replayed HIP graph of the
  * sampling loop keeps its kernel arguments; capk/graphs.py writes the seed before replay). */
 int capk_sample_rows_dev(int dtype, int rows, int V, int64_t ld, const void* logits, const uint32_t* seed,
