@@ -161,3 +161,44 @@ def resnet_encoder(p, images, hidden_sizes, depths, training=True, state=None):
 
 def _strip(p, prefix):
     return {k[len(prefix):]: v for k, v in p.items() if k.startswith(prefix)}
+
+
+# ------------------------------------------------------------------- QFormer ----
+def qformer(p, features, num_layers, num_heads, eps=1e-5):
+    """QFormer.forward (src/models/captioning_model.py:202-245) in eval mode: the learnable
+    queries through `num_layers` norm_first nn.TransformerEncoderLayer blocks
+    (x += SA(LN1 x); x += W2 GELU(W1 LN2 x)), then `num_layers` norm_first
+    nn.TransformerDecoderLayer blocks cross-attending the (vision_proj-ed) features
+    (x += SA(LN1 x); x += MHA(LN2 x, mem); x += FFN(LN3 x)); torch's layer math
+    (torch/nn/modules/transformer.py) with packed in_proj weights.  The encoders' all-ones
+    mask becomes an additive 0 key mask (no masking)."""
+    from .decoders import mha_packed
+    B = features.shape[0]
+    D = p["query_tokens"].shape[-1]
+    x = p["query_tokens"].expand(B, -1, -1)
+    mem = F.linear(features, p["vision_proj.weight"], p["vision_proj.bias"]) if "vision_proj.weight" in p \
+        else features
+
+    def ln(t, pre):
+        return F.layer_norm(t, (D,), p[pre + ".weight"], p[pre + ".bias"], eps)
+
+    def ffn(t, pre):
+        return F.linear(F.gelu(F.linear(t, p[pre + "linear1.weight"], p[pre + "linear1.bias"])),
+                        p[pre + "linear2.weight"], p[pre + "linear2.bias"])
+
+    def mha(q, kv, pre):
+        return mha_packed(q, kv, p[pre + "in_proj_weight"], p[pre + "in_proj_bias"], p[pre + "out_proj.weight"],
+                          p[pre + "out_proj.bias"], num_heads)
+
+    for i in range(num_layers):
+        pre = f"encoder.layers.{i}."
+        h = ln(x, pre + "norm1")
+        x = x + mha(h, h, pre + "self_attn.")
+        x = x + ffn(ln(x, pre + "norm2"), pre)
+    for i in range(num_layers):
+        pre = f"decoder.layers.{i}."
+        h = ln(x, pre + "norm1")
+        x = x + mha(h, h, pre + "self_attn.")
+        x = x + mha(ln(x, pre + "norm2"), mem, pre + "multihead_attn.")
+        x = x + ffn(ln(x, pre + "norm3"), pre)
+    return x

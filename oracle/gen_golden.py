@@ -406,7 +406,29 @@ def case_legacy_decoder(R):
     return arrs
 
 
-CASES = {"vit_transformer_step": case_vit_transformer, "clip_gpt2_step": case_clip_gpt2,
+def case_qformer(R):
+    """The reference's BLIP-2 style QFormer (src/models/captioning_model.py:153-245): two
+    norm_first nn.TransformerEncoder layers over the learnable queries, then two
+    nn.TransformerDecoder layers cross-attending the vision features; eval mode (dropout
+    off), with the all-ones vision mask the encoders return (-> additive 0 key mask)."""
+    torch.manual_seed(77)
+    D, Q, H, S, B = 32, 4, 4, 6, 2
+    qf = R.cap.QFormer(query_dim=D, vision_dim=D, num_queries=Q, num_layers=2, num_heads=H, dropout=0.1)
+    qf.eval()
+    feats = torch.randn(B, S, D, requires_grad=True)
+    mask = torch.ones(B, S)
+    out = qf(feats, mask)["queries"]
+    g = torch.randn_like(out)
+    (out * g).sum().backward()
+    arrs = {"meta/dims": np.array([D, Q, H, S, B], dtype=np.int64), "in/features": _np(feats),
+            "in/grad_out": _np(g), "out/queries": _np(out), "out/dfeatures": _np(feats.grad)}
+    for n, p in qf.named_parameters():
+        arrs["p0/" + n] = _np(p)
+        arrs["grad/" + n] = _np(p.grad)
+    return arrs
+
+
+CASES = {"vit_transformer_step": case_vit_transformer, "qformer_step": case_qformer, "clip_gpt2_step": case_clip_gpt2,
          "lstm_attention": case_lstm_attention, "resnet_lstm_step": case_resnet_lstm,
          "legacy_decoder_step": case_legacy_decoder}
 

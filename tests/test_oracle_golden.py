@@ -258,3 +258,20 @@ def test_legacy_decoder_step_matches_reference(golden_dir):
     p1 = oleg.clamp_adam_step({n: t.detach() for n, t in p.items()}, {n: t.grad for n, t in p.items()})
     for n, t in p1.items():
         _check_digest(z, "p1/" + n, t, 1e-5, 1e-6)
+
+
+def test_qformer_matches_reference(golden_dir):
+    """oracle/encoders.py qformer vs the reference QFormer (captioning_model.py:153-245):
+    queries and every parameter / feature gradient (eval mode)."""
+    z = _load(golden_dir, "qformer_step")
+    D, Q, H, S, B = [int(x) for x in z["meta/dims"]]
+    p = {k: v.requires_grad_(True) for k, v in _params(z, "p0").items()}
+    feats = torch.from_numpy(z["in/features"]).requires_grad_(True)
+    out = oenc.qformer(p, feats, 2, H)
+    np.testing.assert_allclose(out.detach().numpy(), z["out/queries"], rtol=1e-5, atol=1e-6)
+    (out * torch.from_numpy(z["in/grad_out"])).sum().backward()
+    np.testing.assert_allclose(feats.grad.numpy(), z["out/dfeatures"], rtol=1e-4, atol=1e-6)
+    for n, t in p.items():
+        ref = z["grad/" + n]
+        np.testing.assert_allclose(t.grad.numpy(), ref, rtol=1e-4, atol=1e-6 * max(1.0, float(np.abs(ref).max())),
+                                   err_msg=n)
