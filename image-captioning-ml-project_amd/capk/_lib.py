@@ -98,6 +98,11 @@ SIGNATURES = {
     "capk_sample_rows": (_i, [_i, _i, _i, _i64, _c_p, _u32, _i, _c_p, _i64, _c_p, _c_p]),
     "capk_sample_rows_dev": (_i, [_i, _i, _i, _i64, _c_p, _c_p, _i, _c_p, _i64, _c_p, _c_p]),
     "capk_gather_rows": (_i, [_i, _i, _i, _i, _c_p, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p]),
+    "capk_window_attn_fwd": (_i, [_i, _i, _i, _i, _i, _i, _f, _c_p, _i64, _i, _c_p, _c_p, _c_p, _i64, _c_p, _c_p]),
+    "capk_window_attn_bwd_workspace": (_sz, [_i, _i, _i]),
+    "capk_window_attn_bwd": (_i, [_i, _i, _i, _i, _i, _i, _f, _c_p, _i64, _i, _c_p, _c_p, _c_p, _i64, _c_p, _i64,
+                                  _c_p, _c_p, _i64, _c_p, _i, _c_p, _sz, _c_p]),
+    "capk_rowscale_add": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i, _c_p, _i64, _c_p, _i64, _c_p]),
     "capk_im2col": (_i, [_i, _i, _i, _i, _i, _i, _i64, _i64, _i64, _i64, _i, _i, _i, _i, _i, _i, _i, _c_p, _c_p,
                          _c_p]),
     "capk_col2im": (_i, [_i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _c_p, _c_p, _f, _c_p]),

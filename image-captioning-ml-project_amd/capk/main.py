@@ -61,14 +61,17 @@ def build_parser():
 
 
 _FAMILY_DEFAULT_ENCODER = {EncoderType.VIT: "google/vit-base-patch16-224", EncoderType.RESNET: "microsoft/resnet-50",
-                           EncoderType.CLIP: "openai/clip-vit-base-patch32"}
+                           EncoderType.CLIP: "openai/clip-vit-base-patch32",
+                           EncoderType.SWIN: "microsoft/swin-base-patch4-window7-224"}
 
 
 def _known_encoder_archs(et):
     from .models.clip import CLIP_ARCHS
     from .models.resnet import RESNET_ARCHS
+    from .models.swin import SWIN_ARCHS
     from .models.vit import VIT_ARCHS
-    return {EncoderType.VIT: VIT_ARCHS, EncoderType.RESNET: RESNET_ARCHS, EncoderType.CLIP: CLIP_ARCHS}.get(et, {})
+    return {EncoderType.VIT: VIT_ARCHS, EncoderType.RESNET: RESNET_ARCHS, EncoderType.CLIP: CLIP_ARCHS,
+            EncoderType.SWIN: SWIN_ARCHS}.get(et, {})
 
 
 def update_config_from_args(config, args):

@@ -16,6 +16,7 @@ from ..config import EncoderConfig, EncoderType
 from .clip import CLIP_ARCHS, CapkCLIPVisionModel
 from .common import CapkModule
 from .resnet import RESNET_ARCHS, CapkResNetModel, _ResNetHeadFn
+from .swin import SWIN_ARCHS, CapkSwinModel, SwinHeadFn
 from .vit import VIT_ARCHS, CapkViTModel
 
 
@@ -118,6 +119,35 @@ class ResNetEncoder(ImageEncoder, CapkModule):
         return {"features": features, "pooled_features": pooled, "attention_mask": mask}
 
 
+class SwinEncoder(ImageEncoder):
+    """encoders.py:140-182 on libcapk kernels: features = proj(SwinModel
+    last_hidden_state) (proj = Linear when hidden_size != feature_dim, encoders.py:153-158),
+    pooled = features.mean(dim=1) (encoders.py:172), all-valid mask (D4 restatement)."""
+
+    def __init__(self, config: EncoderConfig, arch=None):
+        super().__init__()
+        name = config.pretrained_model_name or "microsoft/swin-base-patch4-window7-224"  # encoders.py:145-147
+        if arch is None:
+            if name not in SWIN_ARCHS:
+                raise ValueError(f"capk SwinEncoder: unknown architecture '{name}' (known: {sorted(SWIN_ARCHS)})")
+            arch = SWIN_ARCHS[name]
+        self.model = CapkSwinModel(arch)
+        self.feature_dim = config.feature_dim
+        hidden = self.model.num_features
+        self.proj = nn.Linear(hidden, self.feature_dim) if hidden != self.feature_dim else nn.Identity()
+        if config.freeze:
+            for p in self.model.parameters():
+                p.requires_grad = False
+
+    def forward(self, images):
+        x, (B, H, W) = self.model(images)
+        proj = self.proj if isinstance(self.proj, nn.Linear) else None
+        feats, pooled = SwinHeadFn.apply(x, self.model.layernorm.weight, self.model, proj, B, H * W)
+        features = feats.view(B, H * W, feats.shape[1])
+        mask = torch.ones(B, H * W, dtype=torch.bool, device=images.device)  # D4 restatement
+        return {"features": features, "pooled_features": pooled, "attention_mask": mask}
+
+
 def build_encoder(config: EncoderConfig) -> ImageEncoder:
     """encoders.py:299-312 (with D2: string types accepted)."""
     et = config.encoder_type if isinstance(config.encoder_type, EncoderType) else EncoderType(config.encoder_type)
@@ -128,5 +158,5 @@ def build_encoder(config: EncoderConfig) -> ImageEncoder:
     if et == EncoderType.RESNET:
         return ResNetEncoder(config)
     if et == EncoderType.SWIN:
-        raise NotImplementedError("capk: Swin is out of the hot-path scope (SURVEY §2, §8f-4)")
+        return SwinEncoder(config)
     raise ValueError(f"Unsupported encoder type: {config.encoder_type}")

@@ -498,6 +498,42 @@ def gather_rows(x, idx, y, groups, rows, cols, ldx, gsx, ldy, gsy, x_off=0, y_of
                                  y.data_ptr() + y_off * y.element_size(), ldy, gsy, _stream()), "capk_gather_rows")
 
 
+# ------------------------------------------------------------------ Swin ----
+def window_attn_fwd(qkv, C, H, ws, nw_img, scale, table, labels, out):
+    """Swin window attention over window-ordered rows (capk.h); returns lse [nwin, H, N]."""
+    _need_gpu(qkv, table, out)
+    N = ws * ws
+    nwin = qkv.shape[0] // N
+    lse = torch.empty(nwin, H, N, dtype=torch.float32, device=qkv.device)
+    check(lib().capk_window_attn_fwd(dtype_code(qkv), nwin, nw_img, ws, H, C // H, float(scale), _p(qkv),
+                                     qkv.stride(0), C, _p(table), _p(labels), _p(out), out.stride(0), _p(lse),
+                                     _stream()), "capk_window_attn_fwd")
+    return lse
+
+
+def window_attn_bwd(qkv, C, H, ws, nw_img, scale, table, labels, out, dout, lse, dqkv, dtable, accumulate=False):
+    L = lib()
+    N = ws * ws
+    nwin = qkv.shape[0] // N
+    wsb = L.capk_window_attn_bwd_workspace(nwin, ws, H)
+    ws_t = _ws(wsb, qkv.device)
+    check(L.capk_window_attn_bwd(dtype_code(qkv), nwin, nw_img, ws, H, C // H, float(scale), _p(qkv), qkv.stride(0),
+                                 C, _p(table), _p(labels), _p(out), out.stride(0), _p(dout), dout.stride(0), _p(lse),
+                                 _p(dqkv), dqkv.stride(0), _p(dtable), int(accumulate), _p(ws_t), wsb, _stream()),
+          "capk_window_attn_bwd")
+
+
+def rowscale_add(x, scale, group_rows, res=None, out=None):
+    """out = res + x * scale[row // group_rows] (SwinDropPath's per-sample factor)."""
+    rows, cols = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    check(lib().capk_rowscale_add(dtype_code(x), rows, cols, _p(x), x.stride(0), _p(scale), int(group_rows),
+                                  _p(res), res.stride(0) if res is not None else 0, _p(out), out.stride(0),
+                                  _stream()), "capk_rowscale_add")
+    return out
+
+
 def dropout_apply(x, drop, out=None):
     """x * mask (GEMM-epilogue mask convention, index r*cols + c)."""
     if drop[0] <= 0:

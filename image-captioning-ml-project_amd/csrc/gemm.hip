@@ -315,6 +315,8 @@ static int tiles_of(int cfg, int M, int N) {
 static int choose_splits(int cfg, int M, int N, int K);
 static int choose_cfg(int M, int N, int K, int a_kmajor, int b_kmajor, int act) {
   int o = cfg_override();
+  // K-major operands with K % 64 != 0 (e.g. Swin-T/S, C = 96): only the BK-32 rings apply
+  if ((a_kmajor || b_kmajor) && K % 64) return o == 3 ? 3 : 4;
   if ((o == 2 || big_tile(o)) && M < 256) o = 1;
   if ((o == 3 || o == 4) && (a_kmajor || b_kmajor) && K % 32) o = 1;
   if (o >= 1 && o <= 5) return o;
@@ -407,8 +409,8 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
   }
   CAPK_CHECK_ARG(in_dtype == CAPK_BF16, "capk_gemm: unknown in_dtype %d", in_dtype);
   CAPK_CHECK_ARG(out_dtype == CAPK_BF16 || out_dtype == CAPK_F32, "capk_gemm: unknown out_dtype");
-  CAPK_CHECK_ARG(!(a_kmajor || b_kmajor) || K % BKT == 0,
-                 "capk_gemm(bf16): K=%d must be a multiple of %d when an operand is K-major", K, BKT);
+  CAPK_CHECK_ARG(!(a_kmajor || b_kmajor) || K % 32 == 0,
+                 "capk_gemm(bf16): K=%d must be a multiple of 32 when an operand is K-major", K);
   CAPK_CHECK_ARG(N % 8 == 0, "capk_gemm(bf16): N=%d must be a multiple of 8", N);
   CAPK_CHECK_ARG(a_kmajor || (M % 8 == 0 && M >= 8), "capk_gemm(bf16): M-major A needs M %% 8 == 0");
   CAPK_CHECK_ARG(b_kmajor || (N % 8 == 0 && N >= 8), "capk_gemm(bf16): N-major B needs N %% 8 == 0");

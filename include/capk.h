@@ -437,6 +437,31 @@ int capk_clamp(int64_t n, float* x, float lo, float hi, void* stream);
 int capk_mask_rows_by_length(int dtype, int B, int T, int cols, void* x, int64_t ld, int64_t bs, const int32_t* len,
                              void* stream);
 
+/* ------------------------------------------------- Swin encoder (§8f-4) ----
+ * Window attention of transformers SwinAttention (modeling_swin.py:401-468, reached from
+ * SwinEncoder.forward, src/models/encoders.py:165-182), rows in window order: window w
+ * (= b*nw_img + window-in-image) owns rows [w*N, (w+1)*N), N = ws*ws <= 64, token
+ * t = r*ws + c.  q / k / v of head h are columns h*hd, C + h*hd, 2C + h*hd of qkv
+ * (row stride ldq); hd = 32.  s_ij = scale*q_i.k_j + table[idx(i,j)*H + h]
+ * (+ -100 where labels[w % nw_img][i] != labels[..][j]; labels = null for an unshifted
+ * block), idx(i,j) = (r_i-r_j+ws-1)*(2ws-1) + (c_i-c_j+ws-1) (SwinRelativePositionBias);
+ * out = softmax(s) v per head into columns h*hd of out; lse [nwin, H, N] fp32.
+ * capk_window_attn_bwd: dq/dk/dv into the same column layout of dqkv (every element of
+ * the 3C columns written); dtable [(2ws-1)^2, H] fp32 (+)= sum over windows of dS binned
+ * by idx (fixed-order reduction through the caller's workspace).
+ * capk_rowscale_add: y[r, :] = res[r, :] + x[r, :] * scale[r / group_rows] (res may be
+ * null) -- SwinDropPath's per-sample keep/(1-p) factor (modeling_swin.py:42-60). */
+int capk_window_attn_fwd(int dtype, int nwin, int nw_img, int ws, int H, int hd, float scale, const void* qkv,
+                         int64_t ldq, int C, const float* table, const int32_t* labels, void* out, int64_t ldo,
+                         float* lse, void* stream);
+size_t capk_window_attn_bwd_workspace(int nwin, int ws, int H);
+int capk_window_attn_bwd(int dtype, int nwin, int nw_img, int ws, int H, int hd, float scale, const void* qkv,
+                         int64_t ldq, int C, const float* table, const int32_t* labels, const void* out, int64_t ldo,
+                         const void* dout, int64_t lddo, const float* lse, void* dqkv, int64_t lddq, float* dtable,
+                         int accumulate, void* work, size_t work_bytes, void* stream);
+int capk_rowscale_add(int dtype, int rows, int cols, const void* x, int64_t ldx, const float* scale, int group_rows,
+                      const void* res, int64_t ldr, void* y, int64_t ldy, void* stream);
+
 /* ------------------------------------------------------ CIDEr-D (host) ----
  * SCST reward: replaces src/evaluate/metrics.py:46-110 (pycocoevalcap
  * CiderD, via CaptioningTrainer._calculate_rewards, src/train/trainer.py:440-484) with a

@@ -202,3 +202,125 @@ def qformer(p, features, num_layers, num_heads, eps=1e-5):
         x = x + mha(ln(x, pre + "norm2"), mem, pre + "multihead_attn.")
         x = x + ffn(ln(x, pre + "norm3"), pre)
     return x
+
+
+# ---------------------------------------------------------------------- Swin ----
+def _swin_rel_index(ws):
+    """SwinRelativePositionBias._create_relative_position_index (modeling_swin.py:350-365):
+    (r_i - r_j + ws - 1) * (2ws - 1) + (c_i - c_j + ws - 1) for window tokens i, j."""
+    r = torch.arange(ws).repeat_interleave(ws)
+    c = torch.arange(ws).repeat(ws)
+    return (r[:, None] - r[None, :] + ws - 1) * (2 * ws - 1) + (c[:, None] - c[None, :] + ws - 1)
+
+
+def _swin_windows(x, ws):
+    """window_partition (modeling_swin.py:486-496): [B,H,W,C] -> [B*nW, ws*ws, C]."""
+    B, H, W, C = x.shape
+    x = x.view(B, H // ws, ws, W // ws, ws, C).permute(0, 1, 3, 2, 4, 5)
+    return x.reshape(-1, ws * ws, C)
+
+
+def _swin_unwindows(w, ws, B, H, W):
+    C = w.shape[-1]
+    x = w.view(B, H // ws, W // ws, ws, ws, C).permute(0, 1, 3, 2, 4, 5)
+    return x.reshape(B, H, W, C)
+
+
+def _swin_shift_mask(H, W, ws, shift):
+    """SwinLayer.get_attn_mask (modeling_swin.py:584-607): -100 between tokens of different
+    cyclic-shift regions of a window (regions [0, n-ws), [n-ws, n-shift), [n-shift, n) per axis)."""
+    img = torch.zeros(1, H, W, 1)
+    cnt = 0
+    for hs in (slice(0, -ws), slice(-ws, -shift), slice(-shift, None)):
+        for wsl in (slice(0, -ws), slice(-ws, -shift), slice(-shift, None)):
+            img[:, hs, wsl, :] = cnt
+            cnt += 1
+    mw = _swin_windows(img, ws).squeeze(-1)
+    m = mw[:, None, :] - mw[:, :, None]
+    return m.masked_fill(m != 0, -100.0)
+
+
+def swin_block(p, pre, x, H, W, num_heads, ws, shift, eps=1e-5, keep=None):
+    """SwinLayer.forward (modeling_swin.py:529-574): x [B, H*W, C] natural order.
+    keep [B] (optional): SwinDropPath's per-sample factor floor(U + keep_prob)/keep_prob on the
+    attention branch (the MLP branch has no drop path in this transformers version)."""
+    B, L, C = x.shape
+    if min(H, W) <= ws:  # set_shift_and_window_size
+        ws, shift = min(H, W), 0
+    hd = C // num_heads
+    h = F.layer_norm(x, (C,), p[pre + "layernorm_before.weight"], p[pre + "layernorm_before.bias"], eps)
+    h = h.view(B, H, W, C)
+    if shift:
+        h = torch.roll(h, (-shift, -shift), dims=(1, 2))
+    win = _swin_windows(h, ws)
+    nWB, N, _ = win.shape
+    a = pre + "attention."
+    q = F.linear(win, p[a + "q_proj.weight"], p[a + "q_proj.bias"]).view(nWB, N, num_heads, hd).transpose(1, 2)
+    k = F.linear(win, p[a + "k_proj.weight"], p[a + "k_proj.bias"]).view(nWB, N, num_heads, hd).transpose(1, 2)
+    v = F.linear(win, p[a + "v_proj.weight"], p[a + "v_proj.bias"]).view(nWB, N, num_heads, hd).transpose(1, 2)
+    s = torch.matmul(q, k.transpose(-1, -2)) * hd ** -0.5
+    table = p[a + "relative_position_bias.relative_position_bias_table"]
+    bias = table[_swin_rel_index(ws).reshape(-1)].view(N, N, -1).permute(2, 0, 1)
+    s = s + bias.unsqueeze(0)
+    if shift:
+        m = _swin_shift_mask(H, W, ws, shift)
+        nW = m.shape[0]
+        s = (s.view(B, nW, num_heads, N, N) + m[None, :, None]).view(nWB, num_heads, N, N)
+    o = torch.matmul(torch.softmax(s, dim=-1), v).transpose(1, 2).reshape(nWB, N, C)
+    o = F.linear(o, p[a + "o_proj.weight"], p[a + "o_proj.bias"])
+    o = _swin_unwindows(o, ws, B, H, W)
+    if shift:
+        o = torch.roll(o, (shift, shift), dims=(1, 2))
+    o = o.reshape(B, L, C)
+    if keep is not None:
+        o = o * keep.view(B, 1, 1)
+    x = x + o
+    h = F.layer_norm(x, (C,), p[pre + "layernorm_after.weight"], p[pre + "layernorm_after.bias"], eps)
+    h = F.linear(F.gelu(F.linear(h, p[pre + "mlp.fc1.weight"], p[pre + "mlp.fc1.bias"])),
+                 p[pre + "mlp.fc2.weight"], p[pre + "mlp.fc2.bias"])
+    return x + h
+
+
+def swin_merge(p, pre, x, H, W):
+    """SwinPatchMerging.forward (modeling_swin.py:309-326): 2x2 neighbours concatenated in the
+    order (row 0, col 0), (1, 0), (0, 1), (1, 1) -> LN(4C) -> Linear(4C -> 2C, no bias)."""
+    B, L, C = x.shape
+    x = x.view(B, H, W, C)
+    x = torch.cat([x[:, 0::2, 0::2], x[:, 1::2, 0::2], x[:, 0::2, 1::2], x[:, 1::2, 1::2]], dim=-1)
+    x = x.reshape(B, -1, 4 * C)
+    x = F.layer_norm(x, (4 * C,), p[pre + "norm.weight"], p[pre + "norm.bias"], 1e-5)
+    return F.linear(x, p[pre + "reduction.weight"])
+
+
+def swin_model(p, images, depths, heads, patch_size=4, window_size=7, eps=1e-5, keep=None):
+    """SwinModel.forward (modeling_swin.py:849-900) up to the final layernorm:
+    patch conv -> embeddings.norm -> stages (blocks alternate shift 0 / ws//2, patch merge
+    between stages) -> layernorm.  Returns [B, h*w, C_last].  keep: optional list of [B]
+    drop-path factors, one per block in order."""
+    x = F.conv2d(images, p["embeddings.patch_embeddings.projection.weight"],
+                 p["embeddings.patch_embeddings.projection.bias"], stride=patch_size)
+    B, C, H, W = x.shape
+    x = x.flatten(2).transpose(1, 2)
+    x = F.layer_norm(x, (C,), p["embeddings.norm.weight"], p["embeddings.norm.bias"], 1e-5)
+    bi = 0
+    for s, d in enumerate(depths):
+        for i in range(d):
+            pre = f"encoder.layers.{s}.blocks.{i}."
+            x = swin_block(p, pre, x, H, W, heads[s], window_size, 0 if i % 2 == 0 else window_size // 2, eps,
+                           None if keep is None else keep[bi])
+            bi += 1
+        if s < len(depths) - 1:
+            x = swin_merge(p, f"encoder.layers.{s}.downsample.", x, H, W)
+            H, W = H // 2, W // 2
+    C = x.shape[-1]
+    return F.layer_norm(x, (C,), p["layernorm.weight"], p["layernorm.bias"], eps)
+
+
+def swin_encoder(p, images, depths, heads, patch_size=4, window_size=7, keep=None):
+    """SwinEncoder.forward (src/models/encoders.py:165-182): features = proj(last_hidden_state)
+    (proj = Linear when hidden_size != feature_dim, else identity), pooled = features.mean(1).
+    p: the encoder's state dict ("model.*", "proj.*")."""
+    x = swin_model(_strip(p, "model."), images, depths, heads, patch_size, window_size, keep=keep)
+    if "proj.weight" in p:
+        x = F.linear(x, p["proj.weight"], p["proj.bias"])
+    return x, x.mean(dim=1)

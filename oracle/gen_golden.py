@@ -428,9 +428,50 @@ def case_qformer(R):
     return arrs
 
 
+def case_swin_encoder(R):
+    """The reference's SwinEncoder.forward (src/models/encoders.py:140-182) on a random-init
+    transformers SwinModel: 112x112 input -> stages at 28x28 (16 windows, shifted blocks),
+    14x14 (4 windows, shifted) and 7x7 (window clamped to the resolution, no shift); proj
+    Linear(128 -> 48) since hidden_size != feature_dim; features.mean pooling.  Eval mode
+    (SwinDropPath off).  The relative-position tables (zero at HF init) are randomised so
+    the bias path is exercised.  Loss = <features, gf> + <pooled, gp> with fixed random
+    gf, gp, so every parameter receives a gradient through both outputs."""
+    from transformers import SwinConfig, SwinModel
+    torch.manual_seed(4321)
+    scfg = SwinConfig(image_size=112, patch_size=4, embed_dim=32, depths=[2, 2, 2], num_heads=[1, 2, 4],
+                      window_size=7, drop_path_rate=0.1)
+    enc = R.enc.SwinEncoder.__new__(R.enc.SwinEncoder)
+    nn.Module.__init__(enc)
+    enc.model = SwinModel(scfg)
+    enc.feature_dim = 48
+    enc.proj = nn.Linear(enc.model.config.hidden_size, enc.feature_dim)  # encoders.py:153-158
+    with torch.no_grad():
+        for n, p in enc.named_parameters():
+            if n.endswith("relative_position_bias_table"):
+                p.normal_(0.0, 0.5)
+            elif n.endswith("norm.weight") or "layernorm" in n and n.endswith("weight"):
+                p.add_(0.1 * torch.randn_like(p))
+    enc.eval()
+    B = 2
+    images = torch.randn(B, 3, 112, 112)
+    out = enc(images)
+    feats, pooled = out["features"], out["pooled_features"]
+    gf = torch.randn_like(feats)
+    gp = torch.randn_like(pooled)
+    ((feats * gf).sum() + (pooled * gp).sum()).backward()
+    arrs = {"meta/dims": np.array([112, 4, 32, 7, 48, B], dtype=np.int64),
+            "meta/depths": np.array([2, 2, 2], dtype=np.int64), "meta/heads": np.array([1, 2, 4], dtype=np.int64),
+            "in/images": _np(images), "in/gf": _np(gf), "in/gp": _np(gp),
+            "out/features": _np(feats), "out/pooled": _np(pooled), "out/mask": _np(out["attention_mask"])}
+    for n, p in enc.named_parameters():
+        arrs["p0/" + n] = _np(p)
+        arrs["grad/" + n] = _np(p.grad)
+    return arrs
+
+
 CASES = {"vit_transformer_step": case_vit_transformer, "qformer_step": case_qformer, "clip_gpt2_step": case_clip_gpt2,
          "lstm_attention": case_lstm_attention, "resnet_lstm_step": case_resnet_lstm,
-         "legacy_decoder_step": case_legacy_decoder}
+         "legacy_decoder_step": case_legacy_decoder, "swin_encoder": case_swin_encoder}
 
 
 def main(names=None):

@@ -1,0 +1,27 @@
+#!/bin/bash
+# Quick GPU check of the tree: -m gpu suite, smoke, config-3 bench.  Each GPU step has its
+# own time limit; a crash-type exit ends the session.
+set -u
+OUT=gpurun_out/chk
+mkdir -p $OUT
+ok_rc() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "== $name: $*" | tee -a $OUT/status
+  timeout -k 10 $secs "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a $OUT/status
+  tail -3 $OUT/$name.log | cut -c1-300
+  ok_rc $rc || { echo "stopping after $name (rc=$rc)"; exit $rc; }
+}
+for step in "$@"; do
+  case $step in
+    tests) run tests 600 python -u -m pytest tests -m gpu -q -rf --timeout 240 --timeout-method thread ;;
+    smoke) run smoke 240 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench3) run bench_config3 480 python bench.py --steps 10 --warmup 3 ;;
+    bench2) run bench_config2 420 python bench.py --workload config2 --steps 8 --warmup 3 ;;
+    bench5) run bench_config5 480 python bench.py --workload config5 --steps 5 --warmup 2 ;;
+    prof3) run prof3 480 rocprofv3 --kernel-trace --stats -d $OUT/prof3 -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+  esac
+done
+exit 0

@@ -50,17 +50,14 @@ def test_update_config_assigns_strings_and_coerces():
 def test_every_cli_combination_builds_and_round_trips(enc, dec, att, tmp_path):
     from capk.models.attention import AttentionOnAttention, AdaptiveAttention, MultiHeadAttention, SoftAttention
     from capk.models.decoders import GPT2Decoder, LSTMDecoder, TransformerDecoder
-    from capk.models.encoders import CLIPEncoder, ResNetEncoder, ViTEncoder
+    from capk.models.encoders import CLIPEncoder, ResNetEncoder, SwinEncoder, ViTEncoder
     cfg_path = tmp_path / "cfg.json"
     argv = ["--encoder_type", enc, "--decoder_type", dec, "--attention_type", att, "--save_config", str(cfg_path),
             "--steps", "0"]
-    if enc == "swin":  # §8f-4: Swin is not built (SURVEY marks it after the hot path)
-        with pytest.raises(NotImplementedError):
-            main(argv)
-        return
     cfg, model, trainer = main(argv)
     assert trainer is None
-    assert isinstance(model.encoder, {"resnet": ResNetEncoder, "vit": ViTEncoder, "clip": CLIPEncoder}[enc])
+    assert isinstance(model.encoder, {"resnet": ResNetEncoder, "vit": ViTEncoder, "clip": CLIPEncoder,
+                                      "swin": SwinEncoder}[enc])
     assert isinstance(model.decoder, {"lstm": LSTMDecoder, "transformer": TransformerDecoder,
                                       "gpt2": GPT2Decoder}[dec])
     if dec == "lstm":  # only the LSTM decoder builds an attention plugin

@@ -275,3 +275,39 @@ def test_qformer_matches_reference(golden_dir):
         ref = z["grad/" + n]
         np.testing.assert_allclose(t.grad.numpy(), ref, rtol=1e-4, atol=1e-6 * max(1.0, float(np.abs(ref).max())),
                                    err_msg=n)
+
+
+def test_swin_encoder_matches_reference(golden_dir):
+    """oracle/encoders.py swin_encoder vs the reference SwinEncoder.forward
+    (src/models/encoders.py:140-182 on transformers SwinModel, oracle/gen_golden.py
+    case_swin_encoder): features, pooled and every parameter gradient.  The k_proj bias
+    gradients are exactly zero in exact arithmetic (softmax is invariant to a per-query
+    shift), so they are compared against an absolute floor."""
+    z = _load(golden_dir, "swin_encoder")
+    depths = [int(x) for x in z["meta/depths"]]
+    heads = [int(x) for x in z["meta/heads"]]
+    p = {k: v.requires_grad_(True) for k, v in _params(z, "p0").items()}
+    f, pooled = oenc.swin_encoder(p, torch.from_numpy(z["in/images"]), depths, heads)
+    np.testing.assert_allclose(f.detach().numpy(), z["out/features"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(pooled.detach().numpy(), z["out/pooled"], rtol=1e-5, atol=1e-6)
+    ((f * torch.from_numpy(z["in/gf"])).sum() + (pooled * torch.from_numpy(z["in/gp"])).sum()).backward()
+    for n, t in p.items():
+        ref = z["grad/" + n]
+        np.testing.assert_allclose(t.grad.numpy(), ref, rtol=1e-4, atol=1e-6 * max(1.0, float(np.abs(ref).max())),
+                                   err_msg=n)
+
+
+def test_swin_state_dict_names_match_reference(golden_dir):
+    """capk's SwinEncoder exposes the reference SwinEncoder's state-dict names (model.* of
+    transformers SwinModel + proj.*), so a reference checkpoint loads unchanged."""
+    from capk import config as C
+    from capk.models.encoders import SwinEncoder
+    z = _load(golden_dir, "swin_encoder")
+    img, P, E, ws, Fd, B = [int(x) for x in z["meta/dims"]]
+    arch = dict(image_size=img, patch_size=P, num_channels=3, embed_dim=E, depths=tuple(int(x) for x in z["meta/depths"]),
+                num_heads=tuple(int(x) for x in z["meta/heads"]), window_size=ws, mlp_ratio=4.0, qkv_bias=True,
+                layer_norm_eps=1e-5, drop_path_rate=0.1)
+    enc = SwinEncoder(C.EncoderConfig(encoder_type="swin", feature_dim=Fd), arch=arch)
+    want = {k[3:]: z[k].shape for k in z.files if k.startswith("p0/")}
+    got = {k: tuple(v.shape) for k, v in enc.state_dict().items()}
+    assert got == want
