@@ -48,7 +48,7 @@ SIGNATURES = {
     "capk_layernorm_fwd": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _c_p, _f, _c_p, _i64, _c_p, _c_p, _c_p]),
     "capk_layernorm_bwd_workspace": (_sz, [_i, _i]),
     "capk_layernorm_bwd": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p, _c_p, _c_p, _c_p, _i64, _c_p, _i64,
-                                _c_p, _c_p, _i, _f, _u32, _c_p, _i64, _c_p, _sz, _c_p]),
+                                _c_p, _c_p, _c_p, _i, _f, _u32, _c_p, _i64, _c_p, _sz, _c_p]),
     "capk_attention_fwd": (_i, [_i, _i, _i, _i, _i, _i, _f, _i, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _i64,
                                 _i64, _c_p, _c_p, _i64, _i64, _c_p, _f, _u32, _c_p]),
     "capk_attention_bwd": (_i, [_i, _i, _i, _i, _i, _i, _f, _i,            # dtype B H Nq Nk hd scale causal

@@ -134,6 +134,10 @@ class CapkViTModel(CapkModule):
         self.layers = nn.ModuleList([ViTLayer(arch) for _ in range(arch["num_hidden_layers"])])
         self.layernorm = nn.LayerNorm(arch["hidden_size"], eps=arch["layer_norm_eps"])
         self.pooler = _Pooler(arch["hidden_size"])
+        # backward links (not submodules): layer i's LN1 backward emits layer i-1's FC2 bias
+        # gradient (the column sums of its dx), the head's final-LN backward the last layer's
+        for prev, layer in zip(self.layers, self.layers[1:]):
+            object.__setattr__(layer, "_capk_prev", prev)
         self._init_weights()
 
     def _init_weights(self):
@@ -240,16 +244,26 @@ class _ViTLayerFn(torch.autograd.Function):
         hd = D // H
         at, fc1, fc2, act = L.attn, L.fc1, L.fc2, L.act
         ln1, ln2 = L.ln1, L.ln2
-        dfp = linear_bwd(dy, f, fc2.weight, fc2.bias, dt, act_bwd=act, aux=f_pre)
+        # FC2's bias gradient = colsum(dy): already produced by the LN backward that made dy
+        # (next layer's LN1 / the head's final LN) when that one was linked to this layer
+        fused_b2 = getattr(L, "_capk_fc2_bias_done", False)
+        L._capk_fc2_bias_done = False
+        dfp = linear_bwd(dy, f, fc2.weight, None if fused_b2 else fc2.bias, dt, act_bwd=act, aux=f_pre)
         dh2 = linear_bwd(dfp, h2, fc1.weight, fc1.bias, dt)
-        dx1 = ops.layernorm_bwd(dh2, x1, ln2.weight.detach(), mu2, rs2, G(ln2.weight), G(ln2.bias), dres=dy)
-        do = linear_bwd(dx1, o, at.o_proj.weight, at.o_proj.bias, dt)
+        # dx1 = the O projection's output gradient: its column sums (O bias grad) come out of the LN kernel
+        dx1 = ops.layernorm_bwd(dh2, x1, ln2.weight.detach(), mu2, rs2, G(ln2.weight), G(ln2.bias), dres=dy,
+                                dsum=G(at.o_proj.bias))
+        do = linear_bwd(dx1, o, at.o_proj.weight, None, dt)
         dqkv = torch.empty_like(qkv)
         ops.attention_bwd(heads(qkv, 0, B, N), heads(qkv, D, B, N), heads(qkv, 2 * D, B, N), heads(o, 0, B, N),
                           heads(do, 0, B, N), lse, heads(dqkv, 0, B, N), heads(dqkv, D, B, N),
                           heads(dqkv, 2 * D, B, N), B, H, N, N, hd, 1.0 / math.sqrt(hd))
         dh1 = linear_bwd(dqkv, h1, None, None, dt, fused=(at.qkv_w, at.qkv_b))
-        dx = ops.layernorm_bwd(dh1, x, ln1.weight.detach(), mu1, rs1, G(ln1.weight), G(ln1.bias), dres=dx1)
+        prev = getattr(L, "_capk_prev", None)
+        dx = ops.layernorm_bwd(dh1, x, ln1.weight.detach(), mu1, rs1, G(ln1.weight), G(ln1.bias), dres=dx1,
+                               dsum=G(prev.fc2.bias) if prev is not None else None)
+        if prev is not None:
+            prev._capk_fc2_bias_done = True
         notify_final(store_of(L), L.parameters())  # this layer's gradients are complete
         return dx, None, None, None, None
 
@@ -294,7 +308,11 @@ class _ViTHeadFn(torch.autograd.Function):
             dcls = dseq.view(B, N, D)[:, 0]
             ops.linear_dx(dpre, W(dense.weight, dt), out=dcls, beta=1.0)
         ln = m.layernorm
-        dx = ops.layernorm_bwd(dseq, x, ln.weight.detach(), mu, rs, G(ln.weight), G(ln.bias))
+        last = m.layers[-1] if len(m.layers) else None
+        dx = ops.layernorm_bwd(dseq, x, ln.weight.detach(), mu, rs, G(ln.weight), G(ln.bias),
+                               dsum=G(last.fc2.bias) if last is not None else None)
+        if last is not None:
+            last._capk_fc2_bias_done = True
         # the decoder and this head are done: everything but the embeddings and the layers is final
         notify_final(store_of(m), all_except=list(m.embeddings.parameters()) + list(m.layers.parameters()))
         return dx, None, None, None, None

@@ -292,8 +292,9 @@ def layernorm_fwd(x, w, b, eps, out=None):
 
 
 def layernorm_bwd(dy, x, w, mean, rstd, dw, db, *, dres=None, out=None, accumulate=False, drop=NO_DROP,
-                  out_drop=None):
-    """dx = LN'(dy) (+ dres); with drop != off also fills out_drop = LN'(dy) * mask."""
+                  out_drop=None, dsum=None):
+    """dx = LN'(dy) (+ dres); with drop != off also fills out_drop = LN'(dy) * mask;
+    dsum (fp32 [cols], optional) (+)= column sums of dx (a fused bias gradient)."""
     L = lib()
     rows, cols = x.shape
     if out is None:
@@ -302,7 +303,7 @@ def layernorm_bwd(dy, x, w, mean, rstd, dw, db, *, dres=None, out=None, accumula
     ws = _ws(wsb, x.device)
     check(L.capk_layernorm_bwd(dtype_code(x), rows, cols, _p(dy), dy.stride(0), _p(x), x.stride(0), _p(w),
                                _p(mean), _p(rstd), _p(out), out.stride(0), _p(dres),
-                               dres.stride(0) if dres is not None else 0, _p(dw), _p(db), int(accumulate),
+                               dres.stride(0) if dres is not None else 0, _p(dw), _p(db), _p(dsum), int(accumulate),
                                float(drop[0]), int(drop[1]) & 0xFFFFFFFF, _p(out_drop),
                                out_drop.stride(0) if out_drop is not None else 0, _p(ws), wsb, _stream()),
           "capk_layernorm_bwd")

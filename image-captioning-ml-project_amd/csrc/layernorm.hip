@@ -58,8 +58,25 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int cols, const T
   }
 }
 
-// dx = rstd * (g - mean(g) - xhat * mean(g*xhat)), g = dy*w ; partial dw/db per block.
-template <typename T, int MAXC>
+// Raw 8-element row segment kept in registers between its load and its use (the row loop
+// is software-pipelined: the next row's operands are in flight while this row reduces).
+template <typename T> struct Seg8;
+template <> struct Seg8<bf16> {
+  bf16x8 v;
+  __device__ __forceinline__ void load(const bf16* p) { v = *(const bf16x8*)p; }
+  __device__ __forceinline__ float operator[](int i) const { return (float)v[i]; }
+};
+template <> struct Seg8<float> {
+  f32x4 a, b;
+  __device__ __forceinline__ void load(const float* p) { a = *(const f32x4*)p; b = *(const f32x4*)(p + 4); }
+  __device__ __forceinline__ float operator[](int i) const { return i < 4 ? a[i] : b[i - 4]; }
+};
+
+// dx = rstd * (g - mean(g) - xhat * mean(g*xhat)), g = dy*w (+ dres); partial dw/db (and,
+// with SUM, the column sums of dx: the bias gradient of the Linear whose output gradient
+// dx is) per block.  One wave per row, rows grid-strided; row r+stride's x / dy / dres are
+// loaded before row r's reductions, so one memory round trip overlaps one row of work.
+template <typename T, int MAXC, bool SUM>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T* __restrict__ dy, int64_t lddy,
                                                      const T* __restrict__ x, int64_t ldx,
                                                      const float* __restrict__ w, const float* __restrict__ mean,
@@ -67,42 +84,63 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T
                                                      int64_t lddx, const T* __restrict__ dres, int64_t ldres,
                                                      float* __restrict__ part, Drop drop, T* __restrict__ dxd,
                                                      int64_t lddxd) {
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [4 waves][2][cols]
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [4 waves][NP][cols]
+  constexpr int NP = SUM ? 3 : 2;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nch = cols >> 3;
-  float dw[MAXC][8], db[MAXC][8];
+  float dw[MAXC][8], db[MAXC][8], ds[SUM ? MAXC : 1][8];
 #pragma unroll
   for (int c = 0; c < MAXC; ++c)
 #pragma unroll
     for (int i = 0; i < 8; ++i) dw[c][i] = db[c][i] = 0.f;
+#pragma unroll
+  for (int c = 0; c < (SUM ? MAXC : 1); ++c)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ds[c][i] = 0.f;
   float wv[MAXC][8];
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     const int ch = lane + c * 64;
     if (ch < nch) Vec8<float>::load(w + ch * 8, wv[c]);
   }
-  for (int row = blockIdx.x * 4 + wave; row < rows; row += gridDim.x * 4) {
+  const int stride = gridDim.x * 4;
+  Seg8<T> xs[MAXC], dys[MAXC], rss[MAXC];
+  auto fetch = [&](int row) {
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = lane + c * 64;
+      if (ch < nch) {
+        xs[c].load(x + (int64_t)row * ldx + ch * 8);
+        dys[c].load(dy + (int64_t)row * lddy + ch * 8);
+        if (dres) rss[c].load(dres + (int64_t)row * ldres + ch * 8);
+      }
+    }
+  };
+  int row = blockIdx.x * 4 + wave;
+  if (row < rows) fetch(row);
+  for (; row < rows; row += stride) {
     const float mu = mean[row], rs = rstd[row];
-    float xh[MAXC][8], g[MAXC][8];
+    float xh[MAXC][8], g[MAXC][8], r[MAXC][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
       const int ch = lane + c * 64;
       if (ch < nch) {
-        float xv[8], d[8];
-        Vec8<T>::load(x + (int64_t)row * ldx + ch * 8, xv);
-        Vec8<T>::load(dy + (int64_t)row * lddy + ch * 8, d);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          xh[c][i] = (xv[i] - mu) * rs;
-          g[c][i] = d[i] * wv[c][i];
+          const float d = dys[c][i];
+          xh[c][i] = (xs[c][i] - mu) * rs;
+          g[c][i] = d * wv[c][i];
+          r[c][i] = dres ? rss[c][i] : 0.f;
           s1 += g[c][i];
           s2 += g[c][i] * xh[c][i];
-          dw[c][i] += d[i] * xh[c][i];
-          db[c][i] += d[i];
+          dw[c][i] += d * xh[c][i];
+          db[c][i] += d;
         }
       }
     }
+    const int next = row + stride;
+    if (next < rows) fetch(next);  // registers of this row's operands are free again
     const float m1 = wave_sum(s1) / cols, m2 = wave_sum(s2) / cols;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
@@ -118,48 +156,51 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T
           for (int i = 0; i < 8; ++i) od[i] = o[i] * drop.mul(base + i);
           Vec8<T>::store(dxd + (int64_t)row * lddxd + ch * 8, od);
         }
-        if (dres) {
-          float r[8];
-          Vec8<T>::load(dres + (int64_t)row * ldres + ch * 8, r);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) o[i] += r[i];
+        for (int i = 0; i < 8; ++i) o[i] += r[c][i];
+        if constexpr (SUM) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) ds[c][i] += o[i];
         }
         Vec8<T>::store(dx + (int64_t)row * lddx + ch * 8, o);
       }
     }
   }
-  // block reduction of dw/db over the 4 waves
+  // block reduction of dw/db (/ds) over the 4 waves
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     const int ch = lane + c * 64;
     if (ch < nch) {
-      Vec8<float>::store(red + (wave * 2 + 0) * cols + ch * 8, dw[c]);
-      Vec8<float>::store(red + (wave * 2 + 1) * cols + ch * 8, db[c]);
+      Vec8<float>::store(red + (wave * NP + 0) * cols + ch * 8, dw[c]);
+      Vec8<float>::store(red + (wave * NP + 1) * cols + ch * 8, db[c]);
+      if constexpr (SUM) Vec8<float>::store(red + (wave * NP + 2) * cols + ch * 8, ds[c]);
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 2 * cols; i += 256) {
+  for (int i = threadIdx.x; i < NP * cols; i += 256) {
     const int which = i / cols, col = i % cols;
     float s = 0.f;
 #pragma unroll
-    for (int wv2 = 0; wv2 < 4; ++wv2) s += red[(wv2 * 2 + which) * cols + col];
-    part[(int64_t)blockIdx.x * 2 * cols + i] = s;
+    for (int wv2 = 0; wv2 < 4; ++wv2) s += red[(wv2 * NP + which) * cols + col];
+    part[(int64_t)blockIdx.x * NP * cols + i] = s;
   }
 }
 
 // sum the per-block partials [nblocks][2*cols] (sum_parts / finish_parts16, common.h)
-__global__ __launch_bounds__(1024) void ln_bwd_finish_kernel(int nblocks, int cols, const float* __restrict__ part,
-                                                             float* __restrict__ dw, float* __restrict__ db,
+__global__ __launch_bounds__(1024) void ln_bwd_finish_kernel(int nblocks, int cols, int np,
+                                                             const float* __restrict__ part, float* __restrict__ dw,
+                                                             float* __restrict__ db, float* __restrict__ dsum,
                                                              int accumulate) {
-  const float s = finish_parts16(part, 2 * cols, nblocks, 2 * cols);
+  const float s = finish_parts16(part, np * cols, nblocks, np * cols);
   const int i = blockIdx.x * 16 + threadIdx.x;
-  if (threadIdx.x < 16 && i < 2 * cols) {
-    float* dst = i < cols ? dw + i : db + (i - cols);
+  if (threadIdx.x < 16 && i < np * cols) {
+    float* dst = i < cols ? dw + i : i < 2 * cols ? db + (i - cols) : dsum + (i - 2 * cols);
     *dst = accumulate ? *dst + s : s;
   }
 }
 
-static int ln_bwd_blocks(int rows) { return std::max(1, std::min(1024, (rows + 15) / 16)); }
+// (the pipelined kernel holds ~200 VGPRs: 2 waves per SIMD, so 512 blocks are all resident)
+static int ln_bwd_blocks(int rows) { return std::max(1, std::min(512, (rows + 15) / 16)); }
 
 }  // namespace capk
 
@@ -182,30 +223,34 @@ extern "C" int capk_layernorm_fwd(int dtype, int rows, int cols, const void* x, 
 }
 
 extern "C" size_t capk_layernorm_bwd_workspace(int rows, int cols) {
-  return (size_t)ln_bwd_blocks(rows) * 2 * cols * sizeof(float);
+  return (size_t)ln_bwd_blocks(rows) * 3 * cols * sizeof(float);
 }
 
 extern "C" int capk_layernorm_bwd(int dtype, int rows, int cols, const void* dy, int64_t lddy, const void* x,
                                   int64_t ldx, const float* w, const float* mean, const float* rstd, void* dx,
                                   int64_t lddx, const void* dres, int64_t ldres, float* dw, float* db,
-                                  int accumulate, float drop_p, uint32_t drop_seed, void* dx_drop,
+                                  float* dsum, int accumulate, float drop_p, uint32_t drop_seed, void* dx_drop,
                                   int64_t lddx_drop, void* ws, size_t ws_bytes, void* stream) {
   CAPK_CHECK_ARG(rows > 0 && cols > 0 && cols % 8 == 0 && cols <= 2048, "capk_layernorm_bwd: cols=%d", cols);
   const int nb = ln_bwd_blocks(rows);
-  CAPK_CHECK_ARG(ws && ws_bytes >= (size_t)nb * 2 * cols * sizeof(float), "capk_layernorm_bwd: workspace too small");
+  const int np = dsum ? 3 : 2;
+  CAPK_CHECK_ARG(ws && ws_bytes >= (size_t)nb * np * cols * sizeof(float), "capk_layernorm_bwd: workspace too small");
   hipStream_t st = S(stream);
-  const size_t shm = (size_t)8 * cols * sizeof(float);
-#define L(T, MC)                                                                                              \
-  hipLaunchKernelGGL((ln_bwd_kernel<T, MC>), dim3(nb), dim3(256), shm, st, rows, cols, (const T*)dy, lddy,  \
-                     (const T*)x, ldx, w, mean, rstd, (T*)dx, lddx, (const T*)dres, ldres, (float*)ws,       \
+  const size_t shm = (size_t)4 * np * cols * sizeof(float);
+#define L(T, MC, SM)                                                                                              \
+  hipLaunchKernelGGL((ln_bwd_kernel<T, MC, SM>), dim3(nb), dim3(256), shm, st, rows, cols, (const T*)dy, lddy,  \
+                     (const T*)x, ldx, w, mean, rstd, (T*)dx, lddx, (const T*)dres, ldres, (float*)ws,           \
                      make_drop(drop_p, drop_seed), (T*)dx_drop, lddx_drop)
-  if (dtype == CAPK_BF16) { if (cols <= 1024) L(bf16, 2); else L(bf16, 4); }
-  else if (dtype == CAPK_F32) { if (cols <= 1024) L(float, 2); else L(float, 4); }
+#define LS(T, MC) \
+  if (dsum) L(T, MC, true); else L(T, MC, false);
+  if (dtype == CAPK_BF16) { if (cols <= 1024) { LS(bf16, 2) } else { LS(bf16, 4) } }
+  else if (dtype == CAPK_F32) { if (cols <= 1024) { LS(float, 2) } else { LS(float, 4) } }
   else { set_error("capk_layernorm_bwd: dtype"); return CAPK_EINVAL; }
+#undef LS
 #undef L
   CAPK_LAUNCH_CHECK("ln_bwd_kernel");
-  hipLaunchKernelGGL(ln_bwd_finish_kernel, dim3(cdiv(2 * cols, 16)), dim3(1024), 0, st, nb, cols, (const float*)ws, dw,
-                     db, accumulate);
+  hipLaunchKernelGGL(ln_bwd_finish_kernel, dim3(cdiv(np * cols, 16)), dim3(1024), 0, st, nb, cols, np,
+                     (const float*)ws, dw, db, dsum, accumulate);
   CAPK_LAUNCH_CHECK("ln_bwd_finish_kernel");
   return CAPK_OK;
 }

@@ -126,7 +126,9 @@ int capk_layernorm_fwd(int dtype, int rows, int cols, const void* x, int64_t ldx
                        const float* w, const float* b, float eps,
                        void* y, int64_t ldy, float* mean, float* rstd, void* stream);
 /* dx = LN'(dy) (+ dres if non-NULL); dw/db (fp32 [cols]) = sum over rows
- * (accumulate into existing dw/db when accumulate != 0).  If dx_drop != NULL it also
+ * (accumulate into existing dw/db when accumulate != 0); dsum (optional, fp32 [cols])
+ * (+)= the column sums of dx -- the bias gradient of the Linear whose output gradient dx
+ * is (the residual-stream producers of a pre-LN block), fused instead of a capk_colsum.  If dx_drop != NULL it also
  * receives LN'(dy) * dropout-mask (the gradient of a dropped residual branch, e.g.
  * nn.TransformerDecoderLayer dropout1..3).  ws: capk_layernorm_bwd_workspace. */
 size_t capk_layernorm_bwd_workspace(int rows, int cols);
@@ -134,7 +136,7 @@ int capk_layernorm_bwd(int dtype, int rows, int cols, const void* dy, int64_t ld
                        const void* x, int64_t ldx, const float* w,
                        const float* mean, const float* rstd,
                        void* dx, int64_t lddx, const void* dres, int64_t ldres,
-                       float* dw, float* db, int accumulate,
+                       float* dw, float* db, float* dsum, int accumulate,
                        float drop_p, uint32_t drop_seed, void* dx_drop, int64_t lddx_drop,
                        void* ws, size_t ws_bytes, void* stream);
 

@@ -99,7 +99,7 @@ def test_gemm_bf16_strided_rows_and_beta_output(ops):
 # ------------------------------------------------------------- LayerNorm ----
 @cuda
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("cols,eps", [(768, 1e-12), (1536, 1e-5), (32, 1e-5)])
+@pytest.mark.parametrize("cols,eps", [(768, 1e-12), (1536, 1e-5), (32, 1e-5), (2048, 1e-5)])
 def test_layernorm(ops, dtype, cols, eps):
     g = torch.Generator(device="cuda").manual_seed(4)
     rows = 1000
@@ -118,8 +118,14 @@ def test_layernorm(ops, dtype, cols, eps):
     yr.backward(dy.float())
     dw = torch.empty(cols, device="cuda")
     db = torch.empty(cols, device="cuda")
-    dx = ops.layernorm_bwd(dy, x, w, mu, rs, dw, db, dres=dres)
+    dsum = torch.empty(cols, device="cuda")
+    dx = ops.layernorm_bwd(dy, x, w, mu, rs, dw, db, dres=dres, dsum=dsum)
     assert _rel(dx, xr.grad + dres.float()) < tol
+    # fused bias gradient: column sums of dx, accumulated in fp32 before dx is rounded to the
+    # storage dtype -> compared with the fp32 reference's column sums
+    assert _rel(dsum, (xr.grad + dres.float()).sum(0)) < (1e-5 if dtype == torch.float32 else 5e-3)
+    dx2 = ops.layernorm_bwd(dy, x, w, mu, rs, dw, db, dres=dres)  # without dsum: same dx
+    assert torch.equal(dx2, dx)
     assert _rel(dw, wr.grad) < (1e-5 if dtype == torch.float32 else 5e-3)
     assert _rel(db, br.grad) < (1e-5 if dtype == torch.float32 else 5e-3)
 
