@@ -71,8 +71,10 @@ class CapkModule(nn.Module):
 
 
 def linear_bwd(dy, x, w_param, b_param, dtype, *, fused=None, need_dx=True, act_bwd=0, aux=None,
-               dw_accumulate=False, drop=(0.0, 0)):
-    """Backward of y = x W^T + b: dW, db into the grad buffer; returns dX (or None)."""
+               dw_accumulate=False, drop=(0.0, 0), dsum=None):
+    """Backward of y = x W^T + b: dW, db into the grad buffer; returns dX (or None).
+    dsum: with act_bwd, the column sums of the returned dX (the bias gradient of the Linear
+    below the activation) are written there, fused into the activation pass."""
     if fused is not None:
         wmat, gw = fused[0].w(dtype), fused[0].grad
         gb = fused[1].grad if fused[1] is not None else None
@@ -84,7 +86,7 @@ def linear_bwd(dy, x, w_param, b_param, dtype, *, fused=None, need_dx=True, act_
         ops.colsum(dy, gb, accumulate=dw_accumulate)
     if not need_dx:
         return None
-    return ops.linear_dx(dy, wmat, act_bwd=act_bwd, aux=aux, drop=drop)
+    return ops.linear_dx(dy, wmat, act_bwd=act_bwd, aux=aux, drop=drop, dsum=dsum)
 
 
 def heads(buf, col_off, B, N, row_stride_rows=None):

@@ -248,8 +248,10 @@ class _ViTLayerFn(torch.autograd.Function):
         # (next layer's LN1 / the head's final LN) when that one was linked to this layer
         fused_b2 = getattr(L, "_capk_fc2_bias_done", False)
         L._capk_fc2_bias_done = False
-        dfp = linear_bwd(dy, f, fc2.weight, None if fused_b2 else fc2.bias, dt, act_bwd=act, aux=f_pre)
-        dh2 = linear_bwd(dfp, h2, fc1.weight, fc1.bias, dt)
+        # FC1's bias gradient = colsum(dfp), fused into the GELU' pass that produces dfp
+        dfp = linear_bwd(dy, f, fc2.weight, None if fused_b2 else fc2.bias, dt, act_bwd=act, aux=f_pre,
+                         dsum=G(fc1.bias))
+        dh2 = linear_bwd(dfp, h2, fc1.weight, None, dt)
         # dx1 = the O projection's output gradient: its column sums (O bias grad) come out of the LN kernel
         dx1 = ops.layernorm_bwd(dh2, x1, ln2.weight.detach(), mu2, rs2, G(ln2.weight), G(ln2.bias), dres=dy,
                                 dsum=G(at.o_proj.bias))

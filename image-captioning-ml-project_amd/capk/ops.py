@@ -245,12 +245,17 @@ def linear(x, w, b=None, *, out=None, residual=None, act=0, preact=None, out_dty
     return out
 
 
-def linear_dx(dy, w, *, out=None, act_bwd=0, aux=None, beta=0.0, drop=NO_DROP):
-    """dX[M,K] = dY[M,N] @ W[N,K]  (optionally * act'(aux) * dropout-mask: fused activation backward)."""
+def linear_dx(dy, w, *, out=None, act_bwd=0, aux=None, beta=0.0, drop=NO_DROP, dsum=None):
+    """dX[M,K] = dY[M,N] @ W[N,K]  (optionally * act'(aux) * dropout-mask: fused activation backward).
+    dsum (fp32 [K], with act_bwd): also the column sums of the result (the bias gradient of the
+    Linear that produced aux), fused into the activation pass."""
     M, N = dy.shape
     K = w.shape[1]
     if out is None:
         out = torch.empty(M, K, dtype=dy.dtype, device=dy.device)
+    if dsum is not None and act_bwd and beta == 0.0 and drop[0] <= 0:
+        gemm(dy, True, w, False, M, K, N, out, lda=dy.stride(0), ldb=w.stride(0), ldc=out.stride(0))
+        return act_bwd_colsum(out, aux, act_bwd, dsum)
     gemm(dy, True, w, False, M, K, N, out, lda=dy.stride(0), ldb=w.stride(0), ldc=out.stride(0), beta=beta,
          act=(ACT_BWD | act_bwd) if act_bwd else 0, aux=aux, ldx=aux.stride(0) if aux is not None else 0,
          drop=drop)
@@ -276,6 +281,18 @@ def colsum(dy, out, accumulate=False):
     check(L.capk_colsum(dtype_code(dy), M, N, _p(dy), dy.stride(0), _p(out), int(accumulate), _p(ws), wsb,
                         _stream()), "capk_colsum")
     return out
+
+
+def act_bwd_colsum(c, aux, act, db, accumulate=False):
+    """c <- c * act'(aux) in place; db (+)= column sums of the result (capk_act_bwd_colsum)."""
+    _need_gpu(c, aux, db)
+    L = lib()
+    M, N = c.shape
+    wsb = L.capk_colsum_workspace(M, N)
+    ws = _ws(wsb, c.device)
+    check(L.capk_act_bwd_colsum(dtype_code(c), M, N, _p(c), c.stride(0), _p(aux), aux.stride(0), int(act), _p(db),
+                                int(accumulate), _p(ws), wsb, _stream()), "capk_act_bwd_colsum")
+    return c
 
 
 # -------------------------------------------------------------- LayerNorm ---

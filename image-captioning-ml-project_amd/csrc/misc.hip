@@ -249,6 +249,59 @@ __global__ __launch_bounds__(256) void colsum_kernel(int M, int N, const T* __re
   }
 }
 
+// Backward activation pass with the bias gradient fused: C (= dY.W of the next Linear)
+// <- C * act'(aux) (or * aux with CAPK_ACT_DERIV) in place, and the column sums of the
+// result (the producing Linear's bias gradient) as colsum_kernel's per-split partials --
+// one HBM pass instead of the activation pass + a colsum pass over the same matrix.
+template <typename T>
+__global__ __launch_bounds__(256) void act_bwd_colsum_kernel(int M, int N, T* __restrict__ C, int64_t ldc,
+                                                             const T* __restrict__ aux, int64_t ldx, int act,
+                                                             float* __restrict__ part) {
+  __shared__ float red[4][64 * 8 + 4];
+  const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int m0 = blockIdx.y * CS_ROWS_PER_SPLIT, m1 = min(M, m0 + CS_ROWS_PER_SPLIT);
+  const int a = act & 15;
+  const bool deriv = act & CAPK_ACT_DERIV;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c * 8 < N) {
+    int m = m0 + ph;
+    for (; m + 4 < m1; m += 8) {  // two rows (four loads) in flight
+      float v0[8], g0[8], v1[8], g1[8];
+      Vec8<T>::load(C + (int64_t)m * ldc + c * 8, v0);
+      Vec8<T>::load(aux + (int64_t)m * ldx + c * 8, g0);
+      Vec8<T>::load(C + (int64_t)(m + 4) * ldc + c * 8, v1);
+      Vec8<T>::load(aux + (int64_t)(m + 4) * ldx + c * 8, g1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        v0[i] *= deriv ? g0[i] : act_grad_fast(a, g0[i]);
+        v1[i] *= deriv ? g1[i] : act_grad_fast(a, g1[i]);
+        acc[i] += v0[i] + v1[i];
+      }
+      Vec8<T>::store(C + (int64_t)m * ldc + c * 8, v0);
+      Vec8<T>::store(C + (int64_t)(m + 4) * ldc + c * 8, v1);
+    }
+    for (; m < m1; m += 4) {
+      float v[8], g[8];
+      Vec8<T>::load(C + (int64_t)m * ldc + c * 8, v);
+      Vec8<T>::load(aux + (int64_t)m * ldx + c * 8, g);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        v[i] *= deriv ? g[i] : act_grad_fast(a, g[i]);
+        acc[i] += v[i];
+      }
+      Vec8<T>::store(C + (int64_t)m * ldc + c * 8, v);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[ph][lane * 8 + i] = acc[i];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 512; i += 256) {
+    const int col = blockIdx.x * 512 + i;
+    if (col < N) part[(int64_t)blockIdx.y * N + col] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+  }
+}
+
 __global__ __launch_bounds__(1024) void colsum_finish_kernel(int splits, int N, const float* __restrict__ part,
                                                              float* __restrict__ out, int accumulate) {
   const float s = finish_parts16(part, N, splits, N);
@@ -416,6 +469,26 @@ extern "C" int capk_colsum(int dtype, int M, int N, const void* dy, int64_t ldy,
   DT_DISPATCH(dtype, L, 0)
 #undef L
   CAPK_LAUNCH_CHECK("colsum_kernel");
+  hipLaunchKernelGGL(colsum_finish_kernel, dim3(cdiv(N, 16)), dim3(1024), 0, S(stream), splits, N, (const float*)ws, db,
+                     accumulate);
+  CAPK_LAUNCH_CHECK("colsum_finish_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_act_bwd_colsum(int dtype, int M, int N, void* C, int64_t ldc, const void* aux, int64_t ldx,
+                                   int act, float* db, int accumulate, void* ws, size_t ws_bytes, void* stream) {
+  CAPK_CHECK_ARG(M > 0 && N > 0 && N % 8 == 0 && ldc % 8 == 0 && ldx % 8 == 0 && C && aux && db,
+                 "capk_act_bwd_colsum: N, ldc, ldx must be multiples of 8");
+  CAPK_CHECK_ARG((act & 15) != 0, "capk_act_bwd_colsum: no activation");
+  const int splits = cdiv(M, CS_ROWS_PER_SPLIT);
+  CAPK_CHECK_ARG(ws && ws_bytes >= (size_t)splits * N * sizeof(float), "capk_act_bwd_colsum: workspace too small");
+  dim3 grid(cdiv(N, 512), splits);
+#define L(T, _)                                                                                                  \
+  hipLaunchKernelGGL(act_bwd_colsum_kernel<T>, grid, dim3(256), 0, S(stream), M, N, (T*)C, ldc, (const T*)aux, ldx, \
+                     act, (float*)ws)
+  DT_DISPATCH(dtype, L, 0)
+#undef L
+  CAPK_LAUNCH_CHECK("act_bwd_colsum_kernel");
   hipLaunchKernelGGL(colsum_finish_kernel, dim3(cdiv(N, 16)), dim3(1024), 0, S(stream), splits, N, (const float*)ws, db,
                      accumulate);
   CAPK_LAUNCH_CHECK("colsum_finish_kernel");

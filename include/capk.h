@@ -227,6 +227,12 @@ int capk_zero(void* ptr, size_t bytes, void* stream);
 size_t capk_colsum_workspace(int M, int N);
 int capk_colsum(int dtype, int M, int N, const void* dy, int64_t ldy, float* db, int accumulate,
                 void* ws, size_t ws_bytes, void* stream);
+/* C <- C * act'(aux) (CAPK_ACT_DERIV: C * aux) in place and db (+)= its column sums: the
+ * backward activation of an FFN product fused with the bias gradient of the Linear that
+ * produced the activation's input (ViTMLP fc1.bias, modeling_vit.py:249-254).
+ * ws: capk_colsum_workspace(M, N). */
+int capk_act_bwd_colsum(int dtype, int M, int N, void* C, int64_t ldc, const void* aux, int64_t ldx, int act,
+                        float* db, int accumulate, void* ws, size_t ws_bytes, void* stream);
 /* elementwise casts / copies */
 int capk_cast(int in_dtype, int out_dtype, int64_t n, const void* x, void* y, void* stream);
 int capk_copy_rows(int dtype, int rows, int cols, const void* x, int64_t ldx, void* y, int64_t ldy, void* stream);

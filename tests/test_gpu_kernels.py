@@ -395,3 +395,31 @@ def test_attention_dropout_fwd_bwd(ops):
         assert _rel(dq.float().view(B, Nq, H, hd).transpose(1, 2), qr.grad) < tolb
         assert _rel(dkv.float()[:, :D].reshape(B, Nk, H, hd).transpose(1, 2), kr.grad) < tolb
         assert _rel(dkv.float()[:, D:].reshape(B, Nk, H, hd).transpose(1, 2), vr.grad) < tolb
+
+
+@cuda
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("deriv", [False, True])
+def test_act_bwd_colsum(ops, dtype, deriv):
+    """capk_act_bwd_colsum: c <- c * GELU'(aux) (or * aux with CAPK_ACT_DERIV) in place, db = colsum
+    (the FC1 bias gradient fused into the FC2-dX activation pass), vs torch fp32."""
+    from capk._lib import ACT_DERIV, ACT_GELU_ERF
+    g = torch.Generator(device="cuda").manual_seed(9)
+    M, N = 1037, 3072  # M not a multiple of the 256-row split or of the 8-row unroll
+    c = torch.randn(M, N, device="cuda", generator=g).to(dtype)
+    aux = torch.randn(M, N, device="cuda", generator=g).to(dtype)
+    xr = aux.float().requires_grad_(True)
+    if deriv:
+        ref = c.float() * aux.float()
+    else:
+        F.gelu(xr).backward(c.float())
+        ref = xr.grad
+    db = torch.full((N,), 7.0, device="cuda")
+    out = ops.act_bwd_colsum(c, aux, ACT_GELU_ERF | (ACT_DERIV if deriv else 0), db)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert out.data_ptr() == c.data_ptr()
+    assert _rel(c, ref) < tol, _rel(c, ref)
+    assert _rel(db, ref.sum(0)) < (1e-5 if dtype == torch.float32 else 5e-3), _rel(db, ref.sum(0))
+    db2 = db.clone()
+    ops.act_bwd_colsum(c.clone(), aux, ACT_GELU_ERF | (ACT_DERIV if deriv else 0), db2, accumulate=True)
+    assert db2.shape == db.shape and bool(torch.isfinite(db2).all())
