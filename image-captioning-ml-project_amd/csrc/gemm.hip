@@ -339,10 +339,13 @@ static int choose_cfg(int M, int N, int K, int a_kmajor, int b_kmajor, int act) 
 // Split-K factor: fill one round of resident workgroups when the tile grid alone cannot
 // (any integer factor; every split keeps >= 4 K-tiles).
 static int choose_splits(int cfg, int M, int N, int K) {
-  static const int max_split = [] {  // A/B control (tools/gemm_bench.py): CAPK_GEMM_MAXSPLIT=1 disables split-K
+  static const int max_split_env = [] {  // A/B control (tools/gemm_bench.py): CAPK_GEMM_MAXSPLIT=1 disables split-K
     const char* v = getenv("CAPK_GEMM_MAXSPLIT");
-    return v ? std::max(1, atoi(v)) : 16;
+    return v ? std::max(1, atoi(v)) : 0;
   }();
+  // very long reductions (conv weight gradients: K = B*H*W up to 4e5) with a tiny M x N
+  // grid fill the chip only with more than 16 splits (each split still >= 4 K-tiles)
+  const int max_split = max_split_env ? max_split_env : (K >= 65536 ? 64 : 16);
   const int bk = (cfg == 3 || cfg == 4) ? 32 : 64;
   const int tiles = tiles_of(cfg, M, N), slots = slots_of(cfg);
   const int nk = cdiv(K, bk);
