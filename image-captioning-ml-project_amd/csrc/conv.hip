@@ -186,11 +186,12 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(int M, int C, int rows_p
 // MODE 0: mean = s/M.  MODE 1: var = s/M, rstd = 1/sqrt(var+eps), running stats.
 // MODE 2: dbeta = s0, dgamma = s1 -> out0/out1 (batch values for the apply pass) and
 //         (+)= into the parameter gradients.
-// Block = 64 columns x 16 split groups (1024 threads): each thread sums every 16th split
-// partial of its column (coalesced 256-B rows of `part`), then an LDS reduction over the
-// groups.  (One thread per column looping over up to 2048 splits took ~300 us per call on
-// the 64-channel stages: 92 ms of a 153-ms config-2 step.)
-constexpr int BNF_COLS = 64, BNF_GROUPS = 16;
+// Block = 16 columns x 64 split phases (1024 threads, finish_parts16 of common.h): each
+// thread sums every 64th split partial of its column with four loads in flight, then an
+// LDS reduction over the phases -- the partial matrix is read in about one memory round
+// trip.  (Round 2 before: 64 columns x 16 groups with one load in flight, ~25 us per call
+// x 3 calls per BatchNorm on config 2; one thread per column before that, ~300 us.)
+constexpr int BNF_COLS = 16;
 template <int MODE>
 __global__ __launch_bounds__(1024) void bn_finish_kernel(int M, int C, int splits, const float* __restrict__ part,
                                                          float eps, float momentum, float* __restrict__ out0,
@@ -199,27 +200,13 @@ __global__ __launch_bounds__(1024) void bn_finish_kernel(int M, int C, int split
                                                          float* __restrict__ g0, float* __restrict__ g1,
                                                          int accumulate) {
   constexpr int NACC = MODE == 2 ? 2 : 1;
-  __shared__ float red[NACC][BNF_GROUPS][BNF_COLS];
-  const int cl = threadIdx.x % BNF_COLS, grp = threadIdx.x / BNF_COLS;
-  const int c = blockIdx.x * BNF_COLS + cl;
-  float s0 = 0.f, s1 = 0.f;
-  if (c < C) {
-    for (int k = grp; k < splits; k += BNF_GROUPS) {
-      s0 += part[((int64_t)k * NACC) * C + c];
-      if (MODE == 2) s1 += part[((int64_t)k * NACC + 1) * C + c];
-    }
+  float s0 = finish_parts16(part, (int64_t)NACC * C, splits, C), s1 = 0.f;
+  if (MODE == 2) {
+    __syncthreads();  // finish_parts16's LDS image is reused
+    s1 = finish_parts16(part + C, (int64_t)NACC * C, splits, C);
   }
-  red[0][grp][cl] = s0;
-  if (MODE == 2) red[NACC - 1][grp][cl] = s1;
-  __syncthreads();
-  if (grp != 0 || c >= C) return;
-  s0 = 0.f;
-  s1 = 0.f;
-#pragma unroll
-  for (int g = 0; g < BNF_GROUPS; ++g) {
-    s0 += red[0][g][cl];
-    if (MODE == 2) s1 += red[NACC - 1][g][cl];
-  }
+  const int c = blockIdx.x * BNF_COLS + threadIdx.x;
+  if (threadIdx.x >= BNF_COLS || c >= C) return;
   if (MODE == 0) {
     out0[c] = s0 / (float)M;
   } else if (MODE == 1) {
