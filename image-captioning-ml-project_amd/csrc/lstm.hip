@@ -83,7 +83,11 @@ __global__ __launch_bounds__(256) void soft_attn_fwd_kernel(int S, int D, int Dv
                                                             const float* __restrict__ we, const float* __restrict__ be,
                                                             float inv_temp, const uint8_t* __restrict__ key_pad,
                                                             T* __restrict__ ctx, int64_t ldc, float* __restrict__ wout) {
+  // grid (B, column chunks of 256): every chunk block recomputes the step's S-vector
+  // (dctx . v[s], softmax Jacobian) -- S*Dv MACs -- and owns 256 columns of dq / dkp /
+  // dwe / dv; chunk 0 also writes dbe.  (One block per image left half the CUs idle.)
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int d0 = blockIdx.y * 256;
   __shared__ float sc[SA_MAXS];
   __shared__ float red[4];
   const T* q = qp + (int64_t)b * ldq;
@@ -140,7 +144,11 @@ __global__ __launch_bounds__(256) void soft_attn_bwd_kernel(int S, int D, int Dv
                                                             T* __restrict__ dqp, int64_t lddq,
                                                             float* __restrict__ dkp, float* __restrict__ dv,
                                                             float* __restrict__ dwe_part, float* __restrict__ dbe_part) {
+  // grid (B, column chunks of 256): every chunk block recomputes the step's S-vector
+  // (dctx . v[s], softmax Jacobian) -- S*Dv MACs -- and owns 256 columns of dq / dkp /
+  // dwe / dv; chunk 0 also writes dbe.  (One block per image left half the CUs idle.)
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int d0 = blockIdx.y * 256;
   __shared__ float ws[SA_MAXS], de[SA_MAXS];
   __shared__ float red[4];
   const T* g = dctx + (int64_t)b * lddc;
@@ -171,9 +179,10 @@ __global__ __launch_bounds__(256) void soft_attn_bwd_kernel(int S, int D, int Dv
   float* dkb = dkp + (int64_t)b * S * D;
   float dbe = 0.f;
   for (int s = tid; s < S; s += 256) dbe += de[s];
-  for (int d = tid; d < D; d += 256) {
+  for (int d = d0 + tid; d < D && d < d0 + 256; d += 256) {
     const float qd = to_f32(q[d]), wd = we[d];
     float dq = 0.f, dw = 0.f;
+#pragma unroll 7
     for (int s = 0; s < S; ++s) {
       const float pre = qd + to_f32(kb[(int64_t)s * kp_rs + d]);
       const float a = energy_act<ACT>(pre);
@@ -187,11 +196,15 @@ __global__ __launch_bounds__(256) void soft_attn_bwd_kernel(int S, int D, int Dv
   }
   if (dv) {
     float* dvb = dv + (int64_t)b * S * Dv;
-    for (int d = tid; d < Dv; d += 256) {
+    // columns [Dv * y / Y, Dv * (y + 1) / Y) of dv for chunk y of Y (Dv may differ from D)
+    const int Y = gridDim.y, e0 = (int)((int64_t)Dv * blockIdx.y / Y), e1 = (int)((int64_t)Dv * (blockIdx.y + 1) / Y);
+    for (int d = e0 + tid; d < e1; d += 256) {
       const float gd = to_f32(g[d]);
+#pragma unroll 7
       for (int s = 0; s < S; ++s) dvb[(int64_t)s * Dv + d] += ws[s] * gd;
     }
   }
+  if (blockIdx.y != 0) return;
   dbe = wave_sum(dbe);
   if (lane == 0) red[w] = dbe;
   __syncthreads();
@@ -257,7 +270,7 @@ extern "C" int capk_additive_attn_bwd(int dtype, int act, int B, int S, int D, i
   CAPK_CHECK_ARG(B > 0 && S > 0 && S <= SA_MAXS && D > 0 && Dv > 0, "capk_additive_attn_bwd: need 0 < S <= %d",
                  SA_MAXS);
   CAPK_CHECK_ARG(act == 0 || act == 1, "capk_additive_attn_bwd: act must be 0 (tanh) or 1 (relu)");
-#define K(T, A) hipLaunchKernelGGL((soft_attn_bwd_kernel<T, A>), dim3(B), dim3(256), 0, capk::S(stream), S, D, Dv, (const T*)qp, ldq, (const T*)kp, kp_bs, kp_rs, (const T*)v, v_bs, v_rs, we, inv_temp, w, (const T*)dctx, lddc, dw_in, (T*)dqp, lddq, dkp, dv, dwe_part, dbe_part)
+#define K(T, A) hipLaunchKernelGGL((soft_attn_bwd_kernel<T, A>), dim3(B, (D + 255) / 256), dim3(256), 0, capk::S(stream), S, D, Dv, (const T*)qp, ldq, (const T*)kp, kp_bs, kp_rs, (const T*)v, v_bs, v_rs, we, inv_temp, w, (const T*)dctx, lddc, dw_in, (T*)dqp, lddq, dkp, dv, dwe_part, dbe_part)
   if (act == 0) DT2(dtype, K, 0); else DT2(dtype, K, 1);
 #undef K
   CAPK_LAUNCH_CHECK("soft_attn_bwd_kernel");
