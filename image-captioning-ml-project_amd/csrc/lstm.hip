@@ -83,11 +83,7 @@ __global__ __launch_bounds__(256) void soft_attn_fwd_kernel(int S, int D, int Dv
                                                             const float* __restrict__ we, const float* __restrict__ be,
                                                             float inv_temp, const uint8_t* __restrict__ key_pad,
                                                             T* __restrict__ ctx, int64_t ldc, float* __restrict__ wout) {
-  // grid (B, column chunks of 256): every chunk block recomputes the step's S-vector
-  // (dctx . v[s], softmax Jacobian) -- S*Dv MACs -- and owns 256 columns of dq / dkp /
-  // dwe / dv; chunk 0 also writes dbe.  (One block per image left half the CUs idle.)
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int d0 = blockIdx.y * 256;
   __shared__ float sc[SA_MAXS];
   __shared__ float red[4];
   const T* q = qp + (int64_t)b * ldq;
