@@ -77,18 +77,20 @@ template <int ACT>
 __device__ __forceinline__ float energy_act_grad(float pre, float a) { return ACT == 0 ? 1.f - a * a : (pre > 0.f ? 1.f : 0.f); }
 
 template <typename T, int ACT>
-__global__ __launch_bounds__(256) void soft_attn_fwd_kernel(int S, int D, int Dv, const T* __restrict__ qp, int64_t ldq,
+__global__ __launch_bounds__(1024) void soft_attn_fwd_kernel(int S, int D, int Dv, const T* __restrict__ qp, int64_t ldq,
                                                             const T* __restrict__ kp, int64_t kp_bs, int64_t kp_rs,
                                                             const T* __restrict__ v, int64_t v_bs, int64_t v_rs,
                                                             const float* __restrict__ we, const float* __restrict__ be,
                                                             float inv_temp, const uint8_t* __restrict__ key_pad,
                                                             T* __restrict__ ctx, int64_t ldc, float* __restrict__ wout) {
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // 1024 threads (16 waves) per image: the per-key energies are 16 wave-dot-products in
+  // flight and the context columns one per thread (4 waves left the latency exposed)
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
   __shared__ float sc[SA_MAXS];
-  __shared__ float red[4];
+  __shared__ float red[1];
   const T* q = qp + (int64_t)b * ldq;
   const T* kb = kp + (int64_t)b * kp_bs;
-  for (int s = w; s < S; s += 4) {
+  for (int s = w; s < S; s += nw) {
     const T* k = kb + (int64_t)s * kp_rs;
     float acc = 0.f;
     for (int d = lane; d < D; d += 64) acc += we[d] * energy_act<ACT>(to_f32(q[d]) + to_f32(k[d]));
@@ -115,13 +117,13 @@ __global__ __launch_bounds__(256) void soft_attn_fwd_kernel(int S, int D, int Dv
   }
   __syncthreads();
   const float inv = red[0];
-  for (int s = tid; s < S; s += 256) {
+  for (int s = tid; s < S; s += blockDim.x) {
     sc[s] *= inv;
     wout[(int64_t)b * S + s] = sc[s];
   }
   __syncthreads();
   const T* vb = v + (int64_t)b * v_bs;
-  for (int d = tid; d < Dv; d += 256) {
+  for (int d = tid; d < Dv; d += blockDim.x) {
     float acc = 0.f;
     for (int s = 0; s < S; ++s) acc += sc[s] * to_f32(vb[(int64_t)s * v_rs + d]);
     ctx[(int64_t)b * ldc + d] = from_f32<T>(acc);
@@ -251,7 +253,7 @@ extern "C" int capk_additive_attn_fwd(int dtype, int act, int B, int S, int D, i
   CAPK_CHECK_ARG(B > 0 && S > 0 && S <= SA_MAXS && D > 0 && Dv > 0, "capk_additive_attn_fwd: need 0 < S <= %d",
                  SA_MAXS);
   CAPK_CHECK_ARG(act == 0 || act == 1, "capk_additive_attn_fwd: act must be 0 (tanh) or 1 (relu)");
-#define K(T, A) hipLaunchKernelGGL((soft_attn_fwd_kernel<T, A>), dim3(B), dim3(256), 0, capk::S(stream), S, D, Dv, (const T*)qp, ldq, (const T*)kp, kp_bs, kp_rs, (const T*)v, v_bs, v_rs, we, be, inv_temp, key_pad, (T*)ctx, ldc, w_out)
+#define K(T, A) hipLaunchKernelGGL((soft_attn_fwd_kernel<T, A>), dim3(B), dim3(1024), 0, capk::S(stream), S, D, Dv, (const T*)qp, ldq, (const T*)kp, kp_bs, kp_rs, (const T*)v, v_bs, v_rs, we, be, inv_temp, key_pad, (T*)ctx, ldc, w_out)
   if (act == 0) DT2(dtype, K, 0); else DT2(dtype, K, 1);
 #undef K
   CAPK_LAUNCH_CHECK("soft_attn_fwd_kernel");
