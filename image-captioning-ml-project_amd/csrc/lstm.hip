@@ -133,7 +133,7 @@ __global__ __launch_bounds__(1024) void soft_attn_fwd_kernel(int S, int D, int D
 // Gradients of one step; the key/value/energy gradients ACCUMULATE (fp32) over the
 // decode steps: dkp [B,S,D], dv [B,S,D], dwe_part [B,D], dbe_part [B].
 template <typename T, int ACT>
-__global__ __launch_bounds__(256) void soft_attn_bwd_kernel(int S, int D, int Dv, const T* __restrict__ qp, int64_t ldq,
+__global__ __launch_bounds__(1024) void soft_attn_bwd_kernel(int S, int D, int Dv, const T* __restrict__ qp, int64_t ldq,
                                                             const T* __restrict__ kp, int64_t kp_bs, int64_t kp_rs,
                                                             const T* __restrict__ v, int64_t v_bs, int64_t v_rs,
                                                             const float* __restrict__ we, float inv_temp,
@@ -142,19 +142,20 @@ __global__ __launch_bounds__(256) void soft_attn_bwd_kernel(int S, int D, int Dv
                                                             T* __restrict__ dqp, int64_t lddq,
                                                             float* __restrict__ dkp, float* __restrict__ dv,
                                                             float* __restrict__ dwe_part, float* __restrict__ dbe_part) {
-  // grid (B, column chunks of 256): every chunk block recomputes the step's S-vector
-  // (dctx . v[s], softmax Jacobian) -- S*Dv MACs -- and owns 256 columns of dq / dkp /
-  // dwe / dv; chunk 0 also writes dbe.  (One block per image left half the CUs idle.)
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int d0 = blockIdx.y * 256;
+  // grid (B, column chunks of blockDim): every chunk block recomputes the step's S-vector
+  // (dctx . v[s], softmax Jacobian) -- S*Dv MACs -- and owns blockDim columns of dq / dkp /
+  // dwe / dv; chunk 0 also writes dbe.  (One 4-wave block per image left the latency and
+  // half the CUs idle.)
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
+  const int CH = blockDim.x, d0 = blockIdx.y * CH;
   __shared__ float ws[SA_MAXS], de[SA_MAXS];
-  __shared__ float red[4];
+  __shared__ float red[16];
   const T* g = dctx + (int64_t)b * lddc;
   const T* vb = v + (int64_t)b * v_bs;
-  for (int s = tid; s < S; s += 256) ws[s] = wsave[(int64_t)b * S + s];
+  for (int s = tid; s < S; s += CH) ws[s] = wsave[(int64_t)b * S + s];
   __syncthreads();
   // dw[s] = dctx . v[s]
-  for (int s = w; s < S; s += 4) {
+  for (int s = w; s < S; s += nw) {
     const T* vr = vb + (int64_t)s * v_rs;
     float acc = 0.f;
     for (int d = lane; d < Dv; d += 64) acc += to_f32(g[d]) * to_f32(vr[d]);
@@ -170,14 +171,14 @@ __global__ __launch_bounds__(256) void soft_attn_bwd_kernel(int S, int D, int Dv
   }
   __syncthreads();
   const float dot = red[0];
-  for (int s = tid; s < S; s += 256) de[s] = ws[s] * (de[s] - dot) * inv_temp;
+  for (int s = tid; s < S; s += CH) de[s] = ws[s] * (de[s] - dot) * inv_temp;
   __syncthreads();
   const T* q = qp + (int64_t)b * ldq;
   const T* kb = kp + (int64_t)b * kp_bs;
   float* dkb = dkp + (int64_t)b * S * D;
   float dbe = 0.f;
-  for (int s = tid; s < S; s += 256) dbe += de[s];
-  for (int d = d0 + tid; d < D && d < d0 + 256; d += 256) {
+  for (int s = tid; s < S; s += CH) dbe += de[s];
+  for (int d = d0 + tid; d < D && d < d0 + CH; d += CH) {
     const float qd = to_f32(q[d]), wd = we[d];
     float dq = 0.f, dw = 0.f;
 #pragma unroll 7
@@ -196,7 +197,7 @@ __global__ __launch_bounds__(256) void soft_attn_bwd_kernel(int S, int D, int Dv
     float* dvb = dv + (int64_t)b * S * Dv;
     // columns [Dv * y / Y, Dv * (y + 1) / Y) of dv for chunk y of Y (Dv may differ from D)
     const int Y = gridDim.y, e0 = (int)((int64_t)Dv * blockIdx.y / Y), e1 = (int)((int64_t)Dv * (blockIdx.y + 1) / Y);
-    for (int d = e0 + tid; d < e1; d += 256) {
+    for (int d = e0 + tid; d < e1; d += CH) {
       const float gd = to_f32(g[d]);
 #pragma unroll 7
       for (int s = 0; s < S; ++s) dvb[(int64_t)s * Dv + d] += ws[s] * gd;
@@ -206,7 +207,11 @@ __global__ __launch_bounds__(256) void soft_attn_bwd_kernel(int S, int D, int Dv
   dbe = wave_sum(dbe);
   if (lane == 0) red[w] = dbe;
   __syncthreads();
-  if (tid == 0) dbe_part[b] += red[0] + red[1] + red[2] + red[3];
+  if (tid == 0) {
+    float t = 0.f;
+    for (int i = 0; i < nw; ++i) t += red[i];
+    dbe_part[b] += t;
+  }
 }
 
 static int grid_n(int64_t n) {
@@ -268,7 +273,7 @@ extern "C" int capk_additive_attn_bwd(int dtype, int act, int B, int S, int D, i
   CAPK_CHECK_ARG(B > 0 && S > 0 && S <= SA_MAXS && D > 0 && Dv > 0, "capk_additive_attn_bwd: need 0 < S <= %d",
                  SA_MAXS);
   CAPK_CHECK_ARG(act == 0 || act == 1, "capk_additive_attn_bwd: act must be 0 (tanh) or 1 (relu)");
-#define K(T, A) hipLaunchKernelGGL((soft_attn_bwd_kernel<T, A>), dim3(B, (D + 255) / 256), dim3(256), 0, capk::S(stream), S, D, Dv, (const T*)qp, ldq, (const T*)kp, kp_bs, kp_rs, (const T*)v, v_bs, v_rs, we, inv_temp, w, (const T*)dctx, lddc, dw_in, (T*)dqp, lddq, dkp, dv, dwe_part, dbe_part)
+#define K(T, A) hipLaunchKernelGGL((soft_attn_bwd_kernel<T, A>), dim3(B, (D + 1023) / 1024), dim3(1024), 0, capk::S(stream), S, D, Dv, (const T*)qp, ldq, (const T*)kp, kp_bs, kp_rs, (const T*)v, v_bs, v_rs, we, inv_temp, w, (const T*)dctx, lddc, dw_in, (T*)dqp, lddq, dkp, dv, dwe_part, dbe_part)
   if (act == 0) DT2(dtype, K, 0); else DT2(dtype, K, 1);
 #undef K
   CAPK_LAUNCH_CHECK("soft_attn_bwd_kernel");
