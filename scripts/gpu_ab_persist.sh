@@ -1,4 +1,6 @@
 #!/bin/bash
+# NOTE: the persistent gemm8p variant this A/B measured is not in the build;
+# CAPK_GEMM_PERSIST is read only by that variant.
 # A/B of the persistent 256x256 GEMM (CAPK_GEMM_PERSIST=0: one work item per WG) after the
 # GEMM parity tests.  Any failure (including a test failure) ends the run.
 set -u
