@@ -21,7 +21,7 @@ for step in "$@"; do
     bench3) run bench_config3 480 python bench.py --steps 10 --warmup 3 ;;
     bench2) run bench_config2 420 python bench.py --workload config2 --steps 8 --warmup 3 ;;
     bench5) run bench_config5 480 python bench.py --workload config5 --steps 5 --warmup 2 ;;
-    prof3) run prof3 480 rocprofv3 --kernel-trace --stats -d $OUT/prof3 -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    prof3) run prof3 480 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof3 -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --beam-batch 0 ;;
   esac
 done
 exit 0
