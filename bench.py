@@ -8,7 +8,8 @@ One step = forward + shifted CE + backward + (DP: gradient all-reduce over RCCL)
 CaptioningTrainer._train_epoch body (src/train/trainer.py:218-289).
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
-N>1:    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+N>1:    python bench.py --gpus N  (starts N ranks through torch.distributed.run as a child process),
+        or the driver's  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 Rank 0 prints ONE JSON line.
 """
 import argparse
@@ -56,7 +57,7 @@ def beam_bench(model, batch, reps, device, rank):
 
 
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "round2", "gemm_traffic.json")
-KERNEL_SOURCES = ["gemm.hip", "gemm8p.hip", "gemm_common.h", "common.h", "blaslt.cpp"]
+KERNEL_SOURCES = ["gemm.hip", "gemm8p.hip", "gemm_common.h", "common.h"]
 
 
 def kernel_source_hash():
@@ -157,6 +158,81 @@ def dist_init(backend=None):
     return world, rank, local
 
 
+def launch_ranks(n):
+    """`python bench.py --gpus N` without a torchrun environment: start N rank processes with
+    torch.distributed.run as a CHILD process (this process has made no HIP call yet and never
+    execs) and return its exit code.  Each rank re-enters main() with RANK / WORLD_SIZE set."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def check_world(gpus, world):
+    """The rank count must be what --gpus asked for (the JSON line reports the real one)."""
+    if world != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but the process group has {world} ranks")
+
+
+def dp_selftest(args, world, rank):
+    """--dp-selftest (CPU, gloo): the N>1 plumbing of this script without a GPU -- the
+    self-launch above, dist_init, the backward-overlapped GradBucketer over a tiny captioner's
+    flat gradient buffers (gradients notified final in reverse order, as the backward does),
+    timed_steps' barrier + MAX-over-ranks timing and the whole-job throughput formula.  Prints
+    the same line shape with n_gpus = the process group's size."""
+    import numpy as np
+    from capk import config as C
+    from capk.models import captioning_model as cm
+    from capk.models import encoders as E
+    from capk.params import attach, notify_final
+    from capk.train.dp import GradBucketer
+    torch.manual_seed(0)
+    D = 64
+    cfg = C.Config()
+    cfg.model.encoder = C.EncoderConfig(encoder_type="vit", feature_dim=D)
+    cfg.model.decoder = C.DecoderConfig(decoder_type="transformer", hidden_dim=D, num_layers=1, num_heads=2)
+    cfg.model.vocab_size, cfg.model.pad_token_id = 100, 99
+    arch = dict(hidden_size=D, num_hidden_layers=1, num_attention_heads=2, intermediate_size=2 * D,
+                image_size=32, patch_size=16, num_channels=3, layer_norm_eps=1e-12)
+    orig = E.VIT_ARCHS["google/vit-base-patch16-224"]
+    E.VIT_ARCHS["google/vit-base-patch16-224"] = arch
+    try:
+        m = cm.ImageCaptioningModel(cfg)
+    finally:
+        E.VIT_ARCHS["google/vit-base-patch16-224"] = orig
+    store = attach(m, "cpu")
+    bucketer = GradBucketer(store, bucket_elems=4096, exchange=args.grad_exchange)
+    named = list(m.named_parameters())
+    order = [p for _, p in reversed(named) if id(p) in store.optional]
+    order += [p for _, p in reversed(named) if id(p) not in store.optional]
+    g = torch.Generator().manual_seed(1 + rank)
+
+    def step():
+        for p in order:
+            with torch.no_grad():
+                p._capk_grad.copy_(torch.randn(p.shape, generator=g))
+            notify_final(store, [p])
+        bucketer.finish()
+
+    elapsed = timed_steps(step, args.steps, args.warmup, world, sync=lambda: None, device="cpu")
+    if rank == 0:
+        B = args.batch
+        print(json.dumps({"metric": "dp-selftest (gloo, CPU): gradient exchange only", "value": round(throughput(
+            B, world, args.steps, elapsed), 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic gradients",
+            "config": {"workload": "dp-selftest", "global_batch": B * world, "per_gpu_batch": B,
+                       "parallelism": f"dp{world}", "grad_exchange": args.grad_exchange},
+            "process_group": {"backend": dist.get_backend() if world > 1 else None, "world_size": world},
+            "grad_params": int(sum(int(np.prod(p.shape)) for p in order))}), flush=True)
+
+
 def timed_steps(step, steps, warmup, world, sync, device="cuda"):
     """W untimed steps, then exactly K timed steps bracketed by barrier + device sync on
     both sides; returns the MAX elapsed seconds over ranks (the driver's contract)."""
@@ -179,6 +255,13 @@ def timed_steps(step, steps, warmup, world, sync, device="cuda"):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     return elapsed
+
+
+def process_group(world):
+    """The rank count the timing came from: the RCCL (nccl) process group's size at N>1."""
+    if world > 1:
+        return {"backend": dist.get_backend(), "world_size": dist.get_world_size()}
+    return {"backend": None, "world_size": 1}
 
 
 def throughput(per_rank_batch, world, steps, elapsed):
@@ -292,6 +375,7 @@ def run_config5(args, world, rank, device):
                      "gemm_share_of_step": round(gem["total_ms"] / (elapsed * 1e3), 3)},
         "model_flops": {"per_image": fpi, "tflops": round(fpi * value / world / 1e12, 1)},
         "final_loss": round(float(loss), 5), "reward_sample": round(rs, 4), "reward_baseline": round(rb, 4),
+        "process_group": process_group(world),
     }
     if beam is not None:
         bdt, bgem, blen = beam
@@ -391,6 +475,7 @@ def run_config2(args, world, rank, device):
                      "traffic_source": "not collected for config 2", "launches": bf["launches"],
                      "gemm_share_of_step": round(gem["total_ms"] / (elapsed * 1e3), 3)},
         "final_loss": round(float(last[0]), 4),
+        "process_group": process_group(world),
     }
     if world == 1 and not args.no_cpu_baseline:
         from oracle.step import time_cpu_config2
@@ -423,9 +508,21 @@ def main():
                          "config5 (CLIP+GPT-2 SCST, fp8)")
     ap.add_argument("--precision", choices=["fp8", "bf16"], default="fp8", help="config5 forward precision")
     ap.add_argument("--cpu-batch-scst", type=int, default=4)
+    ap.add_argument("--dp-selftest", action="store_true",
+                    help="CPU/gloo check of the multi-rank plumbing (no GPU; see dp_selftest)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))  # before any GPU call: one child process per rank
+    if args.dp_selftest:
+        world, rank, _ = dist_init("gloo")
+        check_world(args.gpus, world)
+        dp_selftest(args, world, rank)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     world, rank, local = dist_init("nccl")
+    check_world(args.gpus, world)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     if args.workload in ("config2", "config5"):
@@ -510,7 +607,8 @@ def main():
                        "vocab": 50257, "parallelism": f"dp{world}",
                        "grad_exchange": args.grad_exchange if world > 1 else None},
             "roofline": {"bound": "mfma", "kernel": "bf16 GEMM family: every capk_gemm launch in the timed steps "
-                                                    "(hand-written gemm_bf16_kernel + hipBLASLt plain products)",
+                                                    "(hand-written gemm8p / gemm_bf16 kernels, split-K reduce and "
+                                                    "activation passes included)",
                          "by_route": {k: {"launches": v["launches"], "ms": round(v["total_ms"], 2),
                                           "tflops": round(v["tflops"], 1)} for k, v in gem["by_route"].items()},
                          "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
@@ -523,6 +621,7 @@ def main():
                             "tflops": round(FLOP_PER_IMAGE * value / world / 1e12, 1),
                             "frac_of_peak": round(FLOP_PER_IMAGE * value / world / 1e12 / PEAK_BF16_TFLOPS, 4)},
             "final_loss": round(final_loss, 4),
+            "process_group": process_group(world),
         }
         if beam is not None:
             bdt, bgem, blen = beam

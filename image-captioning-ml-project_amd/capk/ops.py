@@ -63,7 +63,7 @@ class KernelTimer:
     def summary(self):
         torch.cuda.synchronize()
         tot_ms, tot_flops, tot_bytes, n = 0.0, 0.0, 0.0, 0
-        route = {0: [0, 0.0, 0.0], 1: [0, 0.0, 0.0], 2: [0, 0.0, 0.0]}  # per path: launches, ms, flops
+        route = {0: [0, 0.0, 0.0], 2: [0, 0.0, 0.0]}  # per path (0: bf16 kernels, 2: fp8): launches, ms, flops
         for s, e, fl, _, by, rt in self.records:
             ms = s.elapsed_time(e)
             tot_ms += ms
@@ -74,7 +74,7 @@ class KernelTimer:
             route[rt][1] += ms
             route[rt][2] += fl
         by_route = {name: {"launches": r[0], "total_ms": r[1], "tflops": (r[2] / (r[1] * 1e-3) / 1e12) if r[1] else 0.0}
-                    for name, r in (("gemm_bf16_kernel", route[0]), ("hipblaslt", route[1]), ("gemm_f8", route[2]))}
+                    for name, r in (("gemm_bf16_kernel", route[0]), ("gemm_f8", route[2]))}
         return {"launches": n, "total_ms": tot_ms, "flops": tot_flops, "by_route": by_route,
                 "avg_ms": tot_ms / max(n, 1), "avg_flops": tot_flops / max(n, 1), "avg_bytes": tot_bytes / max(n, 1)}
 
@@ -107,7 +107,7 @@ def gemm(A, a_kmajor, B, b_kmajor, M, N, K, C, *, lda, ldb, ldc, alpha=1.0, beta
         # algorithmic bytes: A and B read once, C written once (+ read when beta != 0)
         ein, eout = A.element_size(), C.element_size()
         nbytes = ein * (M * K + N * K) + eout * M * N * (2 if beta else 1)
-        GEMM_TIMER.records.append((ev0, ev1, 2.0 * M * N * K, it, nbytes, L.capk_gemm_last_route()))
+        GEMM_TIMER.records.append((ev0, ev1, 2.0 * M * N * K, it, nbytes, 0))
     return C
 
 

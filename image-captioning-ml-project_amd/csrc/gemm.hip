@@ -123,7 +123,7 @@ __global__ __launch_bounds__(BMX / 32 * 64) void gemm_bf16_kernel(
   }
 }
 
-// Activation pass after a library GEMM (the hipBLASLt route of an activation product):
+// Activation pass after the 256x256 kernel's plain product (the split activation route):
 // forward: C holds pre = acc + bias; writes act(pre) to C and pre or act'(pre)
 // (CAPK_ACT_DERIV) to `pre`.  Backward: C holds dY.W; multiplies by act'(aux) or by aux
 // itself (CAPK_ACT_DERIV).  One HBM pass, 8-wide segments, grid-stride.
@@ -358,25 +358,15 @@ static int choose_splits(int cfg, int M, int N, int K) {
   return std::max(1, s);
 }
 
-// blaslt.cpp
-bool lt_enabled();
-bool lt_gemm(int out_f32, int M, int N, int K, const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ldb,
-             int b_kmajor, void* C, int64_t ldc, float alpha, float beta, const float* bias, const void* residual,
-             int64_t ldr, void* ws, size_t ws_bytes, hipStream_t st);
-size_t lt_workspace_bytes();
 
 }  // namespace capk
 
 using namespace capk;
 
-static thread_local int g_last_route = 0;
 static thread_local int g_last_cfg = 0;
-static int g_force_lib = -1;  // -1: CAPK_GEMM_BLASLT env decides; 0 / 1: forced off / on
-extern "C" int capk_gemm_last_route(void) { return g_last_route; }
 extern "C" int capk_gemm_last_config(void) { return g_last_cfg; }
-extern "C" int capk_gemm_force_config(int cfg, int library) {
+extern "C" int capk_gemm_force_config(int cfg) {
   capk::g_forced_cfg = cfg;
-  g_force_lib = library;
   return CAPK_OK;
 }
 
@@ -386,8 +376,7 @@ extern "C" size_t capk_gemm_workspace(int in_dtype, int out_dtype, int M, int N,
   // upper bound over the configurations (the launch picks one of them)
   int s = 1;
   for (int c = 1; c <= 5; ++c) s = std::max(s, choose_splits(c, M, N, K));
-  const size_t slabs = s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
-  return lt_enabled() ? std::max(slabs, lt_workspace_bytes()) : slabs;
+  return s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
 }
 
 extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const void* A, int64_t lda,
@@ -423,35 +412,6 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
   CAPK_CHECK_ARG(((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % 8 == 0 && ldb % 8 == 0,
                  "capk_gemm(bf16): A/B must be 16-B aligned with lda, ldb %% 8 == 0");
   CAPK_CHECK_ARG(((uintptr_t)C % 16 == 0) && (ldc * esz) % 16 == 0, "capk_gemm(bf16): C alignment");
-  // plain products with a K-major A (forward Linear without activation, dX) -> hipBLASLt
-  // (K >= 32768, the LM-head dX, measured no faster there)
-  const bool lib_on = g_force_lib >= 0 ? g_force_lib == 1 : lt_enabled();
-  if (lib_on && act == 0 && !(drop_p > 0.f) && a_kmajor && K < 32768 &&
-      lt_gemm(out_dtype == CAPK_F32, M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, alpha, beta, bias, residual,
-              ldr, ws, ws_bytes, st)) {
-    g_last_route = 1;
-    return CAPK_OK;
-  }
-  // activation products (bias + act with its side output, or x act'): library GEMM for the
-  // product, then one elementwise pass -- measured faster than the fused epilogue on the
-  // FFN shapes because the library main loop is faster than gemm_bf16_kernel's
-  // (a plain forward act that keeps pre writes the product straight into preact: one stream less)
-  const int from_pre = !(act & CAPK_ACT_BWD) && !(act & CAPK_ACT_DERIV) && preact != nullptr;
-  if (lib_on && (act & 15) && !(drop_p > 0.f) && a_kmajor && K < 32768 && !residual && beta == 0.f &&
-      out_dtype == CAPK_BF16 &&
-      lt_gemm(0, M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, from_pre ? preact : C, from_pre ? ldx : ldc, alpha, 0.f,
-              (act & CAPK_ACT_BWD) ? nullptr : bias, nullptr, 0, ws, ws_bytes, st)) {
-    const int64_t segs = (int64_t)M * (N / 8);
-    // dense rows: one launch-wide pass, each lane a pair of segments (flat paths in act_pass_kernel)
-    const bool dense = ldc == N && ldx == N && (from_pre || (act & CAPK_ACT_BWD));
-    const int grid_a = (int)std::min<int64_t>(dense ? cdiv(segs, 512) : cdiv(segs, 256), dense ? (1 << 20) : 8192);
-    hipLaunchKernelGGL(act_pass_kernel<bf16>, dim3(grid_a), dim3(256), 0, st, M, N, (bf16*)C, ldc, (bf16*)preact,
-                       (const bf16*)aux, ldx, act, from_pre);
-    CAPK_LAUNCH_CHECK("act_pass_kernel");
-    g_last_route = 1;
-    return CAPK_OK;
-  }
-  g_last_route = 0;
   const int cfg = choose_cfg(M, N, K, a_kmajor, b_kmajor, act);
   g_last_cfg = cfg;
   int splits = choose_splits(cfg, M, N, K);

@@ -72,17 +72,12 @@ int capk_dropout_mask(int64_t n, uint64_t offset, float p, uint32_t seed, uint8_
  * Workspace (split-K partial slabs, fp32) — query with capk_gemm_workspace();
  * pass ws=NULL/ws_bytes=0 to disable split-K. */
 size_t capk_gemm_workspace(int in_dtype, int out_dtype, int M, int N, int K);
-/* Which path ran the calling thread's last capk_gemm: 0 = hand-written kernels (gemm.hip),
- * 1 = hipBLASLt (plain bf16 products with a K-major A; opt-in with CAPK_GEMM_BLASLT=1: an A/B reference, off by default).  For
- * per-path timing in bench.py. */
-int capk_gemm_last_route(void);
 /* Tile configuration of the calling thread's last hand-written capk_gemm (gemm.hip
  * choose_cfg: 1-4 = 128-row tiles, 5 = the 256x256 phased kernel). */
 int capk_gemm_last_config(void);
 /* Test / benchmark control: force the tile configuration (cfg 1..5; 0 = automatic choice;
- * -1 = CAPK_GEMM_CFG environment value) and the library route (library 0 = off, 1 = on,
- * -1 = CAPK_GEMM_BLASLT environment value) for every later capk_gemm call. */
-int capk_gemm_force_config(int cfg, int library);
+ * -1 = CAPK_GEMM_CFG environment value) for every later capk_gemm call. */
+int capk_gemm_force_config(int cfg);
 int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K,
               const void* A, int64_t lda, int a_kmajor,
               const void* B, int64_t ldb, int b_kmajor,

@@ -215,3 +215,23 @@ def test_bench_dp_path_gloo(tmp_path, golden_dir):
     assert r0["elapsed"] == r1["elapsed"] >= 0.1  # MAX over ranks: rank 1's 2 x 50 ms sleeps
     assert abs(r0["value"] - 2 * 2 * 2 / r0["elapsed"]) < 1e-9
     assert r0["err"] < 1e-2 * max(1.0, r0["gmax"]), r0  # bf16 exchange of the averaged gradient
+
+
+def test_bench_gpus2_self_launch():
+    """`python bench.py --gpus 2` with no torchrun environment starts 2 ranks itself (a child
+    torch.distributed.run, before any GPU call) and the printed line reports 2 ranks -- here
+    in the CPU/gloo self-test mode, which runs the same launch, dist_init, GradBucketer and
+    MAX-over-ranks timing as the GPU workloads."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dp-selftest", "--steps",
+                        "2", "--warmup", "1", "--batch", "4"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 prints ONE line
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["process_group"] == {"backend": "gloo", "world_size": 2}, rec
+    assert rec["config"]["global_batch"] == 8 and rec["steps"] == 2
+    assert abs(rec["value"] - 8 * 2 / (rec["ms_per_step"] * 2 / 1e3)) < 0.01 * rec["value"]

@@ -18,9 +18,9 @@ cuda = pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
 def ops():
     from capk import _lib, ops as _ops
     lib = _lib.load()
-    lib.capk_gemm_force_config(5, 0)  # the 256x256 kernel, library route off
+    lib.capk_gemm_force_config(5)  # the 256x256 kernel
     yield _ops
-    lib.capk_gemm_force_config(-1, -1)
+    lib.capk_gemm_force_config(-1)
 
 
 def _rel(a, b):
