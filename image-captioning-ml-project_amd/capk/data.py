@@ -12,6 +12,8 @@ and the transforms of src/main.py:139-153, with the pixel work on the GPU.
   descriptors; ``DeviceTransform`` uploads it once (non-blocking) and runs
   ``capk_resize_normalize`` (csrc/image.hip): crop + Pillow-exact antialiased bilinear
   resize + flip + ToTensor + Normalize in one kernel, bit-identical to PIL + torchvision.
+  Eval batches stack every image's reference set into ``[B, N, L]`` (pad rows past the
+  image's own ``num_references``).
 * ``build_coco_dataloaders(config, tokenizer, ...)`` — the reference's factory
   (dataset.py:390-472; curriculum sampling is out of scope) returning loaders whose batches
   are already on the device: ``{"image": [B,3,S,S], "caption_tokens", "attention_mask",
@@ -116,6 +118,7 @@ class COCOCaptionDataset(Dataset):
         self.is_training = is_training
         self.seed = seed
         self.epoch = 0
+        self.pad_token_id = int(getattr(tokenizer, "pad_token_id", None) or 0)
         with open(self.annotation_path, "r") as f:
             self.annotations = json.load(f)
         self._process_annotations()
@@ -140,12 +143,22 @@ class COCOCaptionDataset(Dataset):
                              return_tensors="pt")
         return enc.input_ids.squeeze(0), enc.attention_mask.squeeze(0)
 
+    def set_epoch(self, epoch):
+        """Epoch mixed into the crop / flip draws of a plain integer index (EpochSampler
+        passes (index, epoch) pairs instead, which also reach persistent workers)."""
+        self.epoch = int(epoch)
+
     def __getitem__(self, idx):
+        epoch = self.epoch
+        if isinstance(idx, tuple):  # (index, epoch) from EpochSampler
+            idx, epoch = idx
         ex = self.examples[idx]
         img = decode_rgb(os.path.join(self.image_dir, ex["filename"]))
         h, w = img.shape[:2]
         if self.is_training:
-            gen = torch.Generator().manual_seed((self.seed * 1_000_003 + self.epoch) * 10_000_019 + idx)
+            # torchvision draws fresh crop / flip parameters on every access; here they are a
+            # function of (seed, epoch, index): new every epoch, reproducible per run
+            gen = torch.Generator().manual_seed((self.seed * 1_000_003 + epoch) * 10_000_019 + idx)
             desc = train_desc(h, w, self.image_size, gen)
             ids, mask = self._tok(ex["caption"])
             return {"image_u8": img, "desc": desc, "caption_tokens": ids, "attention_mask": mask,
@@ -159,7 +172,37 @@ class COCOCaptionDataset(Dataset):
             ids = torch.zeros((1, self.max_length), dtype=torch.long)
             mask = torch.zeros((1, self.max_length), dtype=torch.long)
         return {"image_u8": img, "desc": desc, "caption_tokens": ids, "attention_mask": mask,
-                "captions": ex["captions"], "image_id": ex["image_id"]}
+                "captions": ex["captions"], "image_id": ex["image_id"], "pad_token_id": self.pad_token_id}
+
+
+class EpochSampler(torch.utils.data.Sampler):
+    """shuffle=True of the reference's train loader (dataset.py:436-444): a fresh permutation
+    per pass, each index tagged with the pass number, so the dataset's crop / flip draws
+    change every epoch even inside persistent workers (which never see set_epoch)."""
+
+    def __init__(self, n, seed=0):
+        self.n, self.seed, self.epoch = int(n), int(seed), -1
+
+    def set_epoch(self, epoch):
+        self.epoch = int(epoch) - 1  # the next __iter__ runs epoch `epoch`
+
+    def __len__(self):
+        return self.n
+
+    def __iter__(self):
+        self.epoch += 1
+        g = torch.Generator().manual_seed(self.seed * 1_000_003 + self.epoch)
+        ep = self.epoch
+        return iter([(i, ep) for i in torch.randperm(self.n, generator=g).tolist()])
+
+
+def _stack_padded(rows, fill):
+    """[N_i, L] tensors -> [B, max N_i, L]; missing rows filled with `fill`."""
+    n = max(r.shape[0] for r in rows)
+    out = torch.full((len(rows), n, rows[0].shape[1]), fill, dtype=rows[0].dtype)
+    for b, r in enumerate(rows):
+        out[b, :r.shape[0]] = r
+    return out
 
 
 def collate(items):
@@ -180,10 +223,14 @@ def collate(items):
             raise ValueError(f"capk data: downscale {ch}x{cw} -> {rh}x{rw} exceeds {MAX_DOWNSCALE}x")
         descs[k] = _ImgDesc(off, h, w, cy, cx, ch, cw, rh, rw, oy, ox, flip)
     out = {"images_packed": buf, "image_desc": torch.frombuffer(bytearray(descs), dtype=torch.uint8).clone()}
-    out["caption_tokens"] = torch.stack([it["caption_tokens"] for it in items]) if items[0]["caption_tokens"].dim() == 1 \
-        else [it["caption_tokens"] for it in items]
-    out["attention_mask"] = torch.stack([it["attention_mask"] for it in items]) if items[0]["attention_mask"].dim() == 1 \
-        else [it["attention_mask"] for it in items]
+    if items[0]["caption_tokens"].dim() == 1:
+        out["caption_tokens"] = torch.stack([it["caption_tokens"] for it in items])
+        out["attention_mask"] = torch.stack([it["attention_mask"] for it in items])
+    else:  # eval: every image's reference set, padded to the batch's largest with pad rows
+        pad = items[0].get("pad_token_id", 0)
+        out["caption_tokens"] = _stack_padded([it["caption_tokens"] for it in items], pad)
+        out["attention_mask"] = _stack_padded([it["attention_mask"] for it in items], 0)
+        out["num_references"] = torch.tensor([it["caption_tokens"].shape[0] for it in items], dtype=torch.long)
     for key in ("caption", "captions", "image_id"):
         if key in items[0]:
             out[key] = [it[key] for it in items]
@@ -247,7 +294,8 @@ def build_coco_dataloaders(config, tokenizer, device=None, use_curriculum=None):
                                 config.image_size, ml, is_training=False, seed=config.seed)
     kw = dict(num_workers=config.num_workers, collate_fn=collate, pin_memory=torch.cuda.is_available(),
               persistent_workers=config.num_workers > 0)
-    train = DataLoader(train_ds, batch_size=config.training.batch_size, shuffle=True, **kw)
+    train = DataLoader(train_ds, batch_size=config.training.batch_size,
+                       sampler=EpochSampler(len(train_ds), config.seed), **kw)
     val = DataLoader(val_ds, batch_size=config.inference.num_candidates, shuffle=False, **kw)
     tf = DeviceTransform(device, config.image_size)
     return DeviceLoader(train, tf), DeviceLoader(val, tf), None

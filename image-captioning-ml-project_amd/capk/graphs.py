@@ -60,18 +60,31 @@ def clear():
     _RUNNERS.clear()
 
 
+def _host_state(runner):
+    """The runner's host-side buffer roles that a chunk's Python body changes (the KV cache /
+    spare ping-pong of a reordering beam step)."""
+    return (getattr(runner, "cache", None), getattr(runner, "spare", None))
+
+
 def _replay(runner, key, body):
     """Capture `body` (launches on the current stream) as the graph `key` of `runner` on
-    first use, then replay it."""
-    g = runner.graphs.get(key)
-    if g is None:
+    first use, then replay it.  A replay runs none of the body's Python, so the host-side
+    roles the body leaves behind (which buffer is the live KV cache after the chunk's
+    reorders) are recorded at capture and restored after every replay: a chunk captured
+    later -- e.g. by a longer search after a short one -- then sees the buffers the replayed
+    chunks before it really left live."""
+    ent = runner.graphs.get(key)
+    if ent is None:
         if runner.pool is None:
             runner.pool = torch.cuda.graph_pool_handle()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, pool=runner.pool):
             body()
-        runner.graphs[key] = g
+        ent = runner.graphs[key] = (g, _host_state(runner))
+    g, after = ent
     g.replay()
+    if after[0] is not None:
+        runner.cache, runner.spare = after
 
 
 # ------------------------------------------------------------------ beam search ----

@@ -12,8 +12,10 @@ Checkpoint compatibility (trainer.py:569-620): ``state_dict()`` is torch.optim.A
 layout — ``{"state": {i: {"step", "exp_avg", "exp_avg_sq"}}, "param_groups": [...]}``
 with parameter indices numbered the way the reference's optimizer numbers them
 (``named_parameters()`` order, requires_grad only, decay group first) — and the
-schedulers' ``state_dict()`` is LambdaLR's / StepLR's, so a checkpoint written by the
-reference trainer loads here and vice versa.
+schedulers' ``state_dict()`` is LambdaLR's / StepLR's, so the optimizer / scheduler entries
+of a checkpoint written by the reference trainer load here and vice versa (the file itself
+through ``capk.train.trainer.load_checkpoint_file``, which maps the reference's pickled
+``src.config`` classes onto capk.config under ``weights_only=True``).
 """
 import math
 

@@ -13,8 +13,8 @@ Same loop structure and state as the reference trainer, with the compute on libc
 * ``save_checkpoint`` / ``load_checkpoint`` — trainer.py:569-620, the reference's layout
   ``{epoch, model_state_dict, optimizer_state_dict, scheduler_state_dict, config,
   best_val_score}`` with torch-AdamW / LambdaLR state dicts, written by rank 0 only
-  under DP.  ``config`` is stored as a plain dict (the reference pickles the dataclass,
-  which ``torch.load(weights_only=True)`` refuses).
+  under DP.  ``config`` is stored as a plain dict; reference checkpoints (which pickle the
+  dataclass) load through ``load_checkpoint_file``'s weights-only class mapping.
 """
 import logging
 from pathlib import Path
@@ -30,6 +30,22 @@ from .optim import CapkAdamW, build_scheduler
 from .scst import scst_step, strip_special
 
 log = logging.getLogger("capk.trainer")
+
+
+_REF_CONFIG_CLASSES = ("EncoderType", "DecoderType", "AttentionType", "EncoderConfig", "DecoderConfig",
+                       "AttentionConfig", "TrainingConfig", "InferenceConfig", "ModelConfig", "Config")
+
+
+def load_checkpoint_file(path, map_location="cpu"):
+    """torch.load(weights_only=True) of a checkpoint written by this trainer or by the
+    reference trainer (trainer.py:578-585, which pickles its ``src.config.Config`` dataclass
+    and Enums).  Nothing from the file is executed: only those ten class names are
+    allowlisted, each mapped to capk.config's class of the same name and fields, so the
+    reference's config comes back as a capk Config."""
+    from .. import config as C
+    safe = [(getattr(C, n), f"src.config.{n}") for n in _REF_CONFIG_CLASSES]
+    with torch.serialization.safe_globals(safe):
+        return torch.load(path, map_location=map_location, weights_only=True)
 
 
 def _rank():
@@ -144,8 +160,10 @@ class CaptioningTrainer:
             ids, _ = self.model.generate(images=images, max_length=self.config.inference.max_length)
             cands += [strip_special(r, dec.eos_token_id, dec.pad_token_id, dec.bos_token_id) for r in ids.tolist()]
             all_caps = caps if caps.dim() == 3 else caps[:, None, :]
-            refs += [[strip_special(c, dec.eos_token_id, dec.pad_token_id, dec.bos_token_id) for c in img]
-                     for img in all_caps.tolist()]
+            nref = batch.get("num_references")
+            nref = nref.tolist() if nref is not None else [all_caps.shape[1]] * all_caps.shape[0]
+            refs += [[strip_special(c, dec.eos_token_id, dec.pad_token_id, dec.bos_token_id) for c in img[:n]]
+                     for img, n in zip(all_caps.tolist(), nref)]
         self.model.train()
         val_loss = float(torch.stack(losses).mean()) if losses else 0.0
         cider = float(cider_d(cands, refs).mean()) if cands else 0.0
@@ -158,7 +176,8 @@ class CaptioningTrainer:
                 "optimizer_state_dict": self.optimizer.state_dict(),
                 "scheduler_state_dict": self.scheduler.state_dict(),
                 "config": _serialize(self.config),
-                "best_val_score": self.best_val_score}
+                "best_val_score": self.best_val_score,
+                "rl_updates": self.rl_updates}
 
     def save_checkpoint(self, epoch, is_best=False, path=None):
         """trainer.py:569-598; rank 0 writes (every rank holds identical weights under DP)."""
@@ -173,8 +192,9 @@ class CaptioningTrainer:
         return path
 
     def load_checkpoint(self, path):
-        """trainer.py:600-620 (loaded with weights_only=True: tensors and plain containers only)."""
-        ck = torch.load(path, map_location="cpu", weights_only=True)
+        """trainer.py:600-620 -- a checkpoint of this trainer or of the reference trainer
+        (load_checkpoint_file: weights_only=True, src.config classes mapped)."""
+        ck = load_checkpoint_file(path)
         self.load_state(ck)
         return ck
 
@@ -186,6 +206,8 @@ class CaptioningTrainer:
             self.scheduler.load_state_dict(ck["scheduler_state_dict"])
         self.best_val_score = ck.get("best_val_score", 0.0)
         self.global_step = int(self.scheduler.last_epoch)
+        # SCST sampler seeds continue where the run stopped (reference checkpoints: none ran)
+        self.rl_updates = int(ck.get("rl_updates", 0))
 
     # --------------------------------------------------------------- epochs ----
     def train(self):

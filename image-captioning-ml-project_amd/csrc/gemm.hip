@@ -304,7 +304,8 @@ static int cfg_override() {
 //   3: 128x128, BK 32, 4-deep ring (64 KiB, 2 WGs/CU)
 //   4: 128x128, BK 32, 3-deep ring (48 KiB, 3 WGs/CU)
 //   5: 256x256, BK 64, 8 waves, phased half-tile ring (128 KiB, 1 WG/CU)
-static bool big_tile(int cfg) { return cfg == 5; }
+//   6: the same tile as a persistent kernel with a register-direct epilogue (gemm8q.hip)
+static bool big_tile(int cfg) { return cfg == 5 || cfg == 6; }
 static int slots_of(int cfg) { return (cfg == 2 || big_tile(cfg)) ? 256 : cfg == 4 ? 768 : 512; }  // resident WGs
 static int tiles_of(int cfg, int M, int N) {
   return cdiv(M, (cfg == 2 || big_tile(cfg)) ? 256 : 128) * cdiv(N, big_tile(cfg) ? 256 : BN);
@@ -319,16 +320,16 @@ static int choose_cfg(int M, int N, int K, int a_kmajor, int b_kmajor, int act) 
   if ((a_kmajor || b_kmajor) && K % 64) return o == 3 ? 3 : 4;
   if ((o == 2 || big_tile(o)) && M < 256) o = 1;
   if ((o == 3 || o == 4) && (a_kmajor || b_kmajor) && K % 32) o = 1;
-  if (o >= 1 && o <= 5) return o;
+  if (o >= 1 && o <= 6) return o;
   // the 256x256 phased kernel (gemm8p.hip) whenever its grid (x split-K for the weight
   // gradients) fills most of the chip: measured faster than the 128-row tiles on every
   // config-3 shape of that size (tools/gemm_bench.py, profiles/round2/)
   if (M >= 256 && N >= 256) {
     const int t5 = tiles_of(5, M, N);
     if (!a_kmajor && !b_kmajor) {
-      if (t5 * choose_splits(5, M, N, K) >= 128) return 5;
+      if (t5 * choose_splits(5, M, N, K) >= 128) return 6;
     } else if (t5 >= 160) {
-      return 5;
+      return 6;
     }
   }
   // (decode-step rows, M < 2048: the 2-WG/CU BK-64 ring measured faster with an activation too)
@@ -375,7 +376,7 @@ extern "C" size_t capk_gemm_workspace(int in_dtype, int out_dtype, int M, int N,
   if (in_dtype != CAPK_BF16) return 0;
   // upper bound over the configurations (the launch picks one of them)
   int s = 1;
-  for (int c = 1; c <= 5; ++c) s = std::max(s, choose_splits(c, M, N, K));
+  for (int c = 1; c <= 6; ++c) s = std::max(s, choose_splits(c, M, N, K));
   return s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
 }
 
@@ -412,10 +413,25 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
   CAPK_CHECK_ARG(((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % 8 == 0 && ldb % 8 == 0,
                  "capk_gemm(bf16): A/B must be 16-B aligned with lda, ldb %% 8 == 0");
   CAPK_CHECK_ARG(((uintptr_t)C % 16 == 0) && (ldc * esz) % 16 == 0, "capk_gemm(bf16): C alignment");
-  const int cfg = choose_cfg(M, N, K, a_kmajor, b_kmajor, act);
-  g_last_cfg = cfg;
+  int cfg = choose_cfg(M, N, K, a_kmajor, b_kmajor, act);
   int splits = choose_splits(cfg, M, N, K);
   if (!ws || ws_bytes < (size_t)splits * M * N * sizeof(float)) splits = 1;
+  if (splits > 1) {  // effective count: every split owns >= 1 K-tile (the reduce sums exactly these)
+    const int bk = (cfg == 3 || cfg == 4) ? 32 : 64, nk = cdiv(K, bk), per = cdiv(nk, splits);
+    splits = cdiv(nk, per);
+  }
+  // gemm8q: at most one side operand and >= 2 K-tiles per item (else the 8p kernel); its
+  // items all run kt_per K-tiles, so a split count that pads the last split is taken only
+  // for MN-major operands (whose K rows past K read as zero; a K-major row would run on
+  // into the next row)
+  if (cfg == 6) {
+    const int nk64 = cdiv(K, 64), per = cdiv(nk64, splits);
+    const bool padded = nk64 % per != 0;
+    if (!gemm8q_supports(e, out_dtype == CAPK_F32) || per < 2 || (padded && (a_kmajor || b_kmajor)) ||
+        ((act & 15) && !(act & CAPK_ACT_BWD) && splits == 1 && !(a_kmajor && b_kmajor)))
+      cfg = 5;
+  }
+  g_last_cfg = cfg;
   const int tiles = tiles_of(cfg, M, N);
   const int grid = tiles * splits;
   float* slab = splits > 1 ? (float*)ws : nullptr;
@@ -436,7 +452,11 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
   else if (a_kmajor) LAUNCH(true, false, OT);           \
   else if (b_kmajor) LAUNCH(false, true, OT);           \
   else LAUNCH(false, false, OT);
-  if (cfg == 5) {
+  if (cfg == 6) {
+    const int rc = launch_gemm8q(a_kmajor, b_kmajor, out_dtype == CAPK_F32, A, lda, B, ldb, M, N, K, splits, e, slab,
+                                 st);
+    if (rc != CAPK_OK) return rc;
+  } else if (cfg == 5) {
     // Activation products on the 256x256 kernel: plain product (+ bias) into the kept
     // pre-activation / C, then one elementwise pass (act_pass_kernel) -- measured faster than
     // the fused activation epilogue, which runs while the CU's MFMAs idle (1 WG per CU), at

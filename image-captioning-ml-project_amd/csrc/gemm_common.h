@@ -265,6 +265,68 @@ __device__ __forceinline__ void wait_vm() {
   else static_assert(VM == 0, "unsupported vmcnt");
 }
 
+// ---- pieces shared by the 256x256 kernels (gemm8p.hip, gemm8q.hip) ----
+template <int VM>
+__device__ __forceinline__ void wait_vmc() {
+  static_assert(VM >= 0 && VM <= 16 && VM % 2 == 0, "unsupported vmcnt");
+  if constexpr (VM == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (VM == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (VM == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (VM == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (VM == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (VM == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else if constexpr (VM == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (VM == 14) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+}
+__device__ __forceinline__ void raw_barrier() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Per-lane byte offset of LDS-DMA piece `ins` (0..15) of a 128-row half-tile whose first
+// row (K-major) / column (MN-major) is row0; k0 = 0.  K-major image [128 rows][64 k]
+// (chunk c of row r at c ^ swz_k<64>(r)); MN-major image [64 k][128 cols] (chunk c of
+// k-row r at c ^ swz_t(r)).
+template <bool KMAJ, int ESZ = 2>
+__device__ __forceinline__ uint32_t piece_voff(int ins, int lane, int row0, int rows, int64_t ld) {
+  if constexpr (KMAJ) {
+    const int r = ins * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ swz_k<64>(r);
+    return (uint32_t)((int64_t)(row0 + r) * ld * ESZ + lc * 16);
+  } else {
+    const int kr = ins * 4 + (lane >> 4);
+    const int lc = (lane & 15) ^ swz_t(kr);
+    int gc = row0 + lc * 8;
+    gc = gc + 8 <= rows ? gc : rows - 8;
+    return (uint32_t)(((int64_t)kr * ld + gc) * 2);
+  }
+}
+
+// One 16x16x32 operand fragment from a half-tile image.  K-major: ds_read_b128 (as
+// read_frag).  MN-major: two ds_read_b64_tr_b16 issued as inline asm -- hipcc treats the
+// transpose-read builtin as aliasing every LDS-DMA in flight and drains vmcnt(0) before it,
+// which would serialise the load pipeline; the caller waits lgkmcnt itself (every phase
+// boundary has `s_waitcnt lgkmcnt(0)` before the first MFMA that consumes a fragment).
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8 frag(const char* half, int rbase, int s, int lane) {
+  if constexpr (KMAJ) {
+    return read_frag<true, 128, 64>(half, rbase, s, lane);
+  } else {
+    const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+    const int lc = (rbase >> 3) + (p >> 1);
+    const int kr0 = s * 32 + g * 8 + q;  // kr0 + 4 has the same swizzle: +1024 bytes
+    const uint32_t a = (uint32_t)(uintptr_t)LDS_PTR(char, half + kr0 * 256 + ((lc ^ swz_t(kr0)) << 4) + (p & 1) * 8);
+    bf16x4 x0, x1;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(x0) : "v"(a));
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:1024" : "=v"(x1) : "v"(a));
+    bf16x8 r;
+    r[0] = x0[0]; r[1] = x0[1]; r[2] = x0[2]; r[3] = x0[3];
+    r[4] = x1[0]; r[5] = x1[1]; r[6] = x1[2]; r[7] = x1[3];
+    return r;
+  }
+}
+
 // gemm8p.hip: launch the 256x256 phased kernel (grid = tiles * splits)
 int launch_gemm8p(bool a_kmajor, bool b_kmajor, bool out_f32, int grid, const void* A, int64_t lda, const void* B,
                   int64_t ldb, int M, int N, int K, int splits, const Epi& e, float* slab, hipStream_t st);
@@ -272,5 +334,9 @@ int launch_gemm8p(bool a_kmajor, bool b_kmajor, bool out_f32, int grid, const vo
 int launch_gemm8p_f8(bool out_f32, int grid, const void* A, int64_t lda, const uint8_t* scA, const void* B,
                      int64_t ldb, const uint8_t* scB, int M, int N, int K, int splits, const Epi& e, float* slab,
                      hipStream_t st);
+// gemm8q.hip: the persistent 256x256 kernel (grid = min(tiles * splits, 256))
+bool gemm8q_supports(const Epi& e, bool out_f32);
+int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int64_t lda, const void* B, int64_t ldb,
+                  int M, int N, int K, int splits, const Epi& e, float* slab, hipStream_t st);
 
 }  // namespace capk

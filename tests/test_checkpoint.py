@@ -122,3 +122,26 @@ def test_mismatched_state_dict_is_rejected():
     copt = CapkAdamW(attach(other, "cpu"))
     with pytest.raises(ValueError):
         copt.load_state_dict(opt.state_dict())
+
+
+def test_reference_checkpoint_file_loads_weights_only(golden_dir):
+    """A checkpoint in the reference trainer's layout, with the reference's own pickled
+    src.config.Config (oracle/gen_ref_checkpoint.py), loads under weights_only=True: the ten
+    src.config classes come back as capk.config's, nothing else is allowlisted."""
+    import os
+    import pickle
+
+    from capk import config as C
+    from capk.train.trainer import load_checkpoint_file
+    path = os.path.join(golden_dir, "ref_checkpoint.pth")
+    ck = load_checkpoint_file(path)
+    cfg = ck["config"]
+    assert isinstance(cfg, C.Config) and isinstance(cfg.model.encoder, C.EncoderConfig)
+    assert cfg.model.encoder.encoder_type is C.EncoderType.CLIP
+    assert cfg.model.decoder.decoder_type is C.DecoderType.LSTM
+    assert cfg.model.attention.attention_type is C.AttentionType.AOA
+    assert cfg.training.batch_size == 48 and ck["epoch"] == 2 and ck["best_val_score"] == 0.625
+    assert set(ck["model_state_dict"]) == {"weight", "bias"}
+    assert ck["optimizer_state_dict"]["state"][0]["step"] == 1
+    with pytest.raises(pickle.UnpicklingError):  # the plain weights-only load refuses the file
+        torch.load(path, weights_only=True)

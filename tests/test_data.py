@@ -100,3 +100,41 @@ def test_collate_packs_images(tmp_path):
         assert np.array_equal(buf[d.offset:d.offset + img.nbytes].reshape(img.shape), img)
     assert b["caption_tokens"].shape == (3, 8)
     assert ctypes.sizeof(D._ImgDesc) == 56
+
+
+def test_eval_collate_pads_reference_sets(tmp_path):
+    """Eval items carry 2, 3 and 4 references: the batch stacks them to [3, 4, L] with pad
+    rows (the tokenizer's pad id, mask 0) and records each image's own count."""
+    root = _coco(tmp_path)
+    ev = D.COCOCaptionDataset(root, "ann.json", "imgs", StubTokenizer(), image_size=32, max_length=6,
+                              is_training=False)
+    items = [ev[k] for k in range(3)]
+    b = D.collate(items)
+    assert b["caption_tokens"].shape == (3, 4, 6) and b["attention_mask"].shape == (3, 4, 6)
+    assert b["num_references"].tolist() == [2, 3, 4]
+    for k, it in enumerate(items):
+        n = it["caption_tokens"].shape[0]
+        assert torch.equal(b["caption_tokens"][k, :n], it["caption_tokens"])
+        assert bool((b["caption_tokens"][k, n:] == StubTokenizer.pad_id).all())
+        assert int(b["attention_mask"][k, n:].sum()) == 0
+
+
+def test_epoch_sampler_changes_augmentation_per_epoch(tmp_path):
+    """EpochSampler: a fresh permutation per pass, each index tagged with its epoch, so the
+    crop / flip draws differ between epochs and repeat for the same (epoch, index) -- also
+    inside persistent DataLoader workers, which never see set_epoch."""
+    root = _coco(tmp_path)
+    tr = D.COCOCaptionDataset(root, "ann.json", "imgs", StubTokenizer(), image_size=32, max_length=8)
+    s = D.EpochSampler(len(tr), seed=3)
+    e0, e1 = list(s), list(s)
+    assert sorted(i for i, _ in e0) == list(range(len(tr))) and {e for _, e in e0} == {0} and {e for _, e in e1} == {1}
+    assert [i for i, _ in e0] != [i for i, _ in e1]
+    descs = lambda ep: [tr[(i, ep)]["desc"] for i in range(len(tr))]
+    assert descs(0) != descs(1) and descs(1) == descs(1)
+    s.set_epoch(5)
+    assert {e for _, e in s} == {5}
+    loader = torch.utils.data.DataLoader(tr, batch_size=len(tr), sampler=D.EpochSampler(len(tr), 3),
+                                         collate_fn=lambda it: [x["desc"] for x in it], num_workers=1,
+                                         persistent_workers=True)
+    a, b = next(iter(loader)), next(iter(loader))
+    assert sorted(a) != sorted(b)  # second pass = epoch 1: different crops

@@ -113,3 +113,54 @@ def test_coco_loader_end_to_end(tmp_path):
         assert torch.equal(got[k], _pil_ref(arrays[ds.examples[idx]["image_id"]], ds[idx]["desc"], 224))
     vb = next(iter(val))
     assert vb["image"].shape == (2, 3, 224, 224) and len(vb["captions"]) == 2
+
+
+@cuda
+def test_validate_over_coco_loaders(tmp_path):
+    """CaptioningTrainer.validate over build_coco_dataloaders' eval loader: images with 1, 2
+    and 3 reference captions in one batch (padded reference sets), CE on caption 0 and
+    CIDEr-D of the greedy captions -- the path `--mode eval` and train() run."""
+    import json
+    import os
+    from PIL import Image
+    from capk import config as C
+    from capk import data as D
+    from capk.models import captioning_model as cm
+    from capk.models import encoders as E
+    from capk.train.trainer import CaptioningTrainer
+    from test_data import StubTokenizer
+    os.makedirs(tmp_path / "v")
+    rng = np.random.default_rng(5)
+    images, anns = [], []
+    for k, (h, w) in enumerate(((240, 300), (256, 256), (230, 260))):
+        Image.fromarray(rng.integers(0, 256, (h, w, 3), dtype=np.uint8)).save(tmp_path / "v" / f"{k}.png")
+        images.append({"id": k, "file_name": f"{k}.png"})
+        anns += [{"image_id": k, "caption": f"a caption of image {k} number {c}"} for c in range(k + 1)]
+    with open(tmp_path / "a.json", "w") as f:
+        json.dump({"images": images, "annotations": anns}, f)
+    cfg = C.Config()
+    cfg.data_root, cfg.train_json, cfg.val_json = str(tmp_path), "a.json", "a.json"
+    cfg.train_image_dir = cfg.val_image_dir = "v"
+    cfg.num_workers = 0
+    cfg.inference.num_candidates = 3  # one eval batch holds all three images
+    cfg.inference.max_length = 8
+    cfg.model.encoder = C.EncoderConfig(encoder_type="vit", feature_dim=64)
+    cfg.model.decoder = C.DecoderConfig(decoder_type="transformer", hidden_dim=64, num_layers=1, num_heads=2,
+                                        max_length=12)
+    cfg.model.vocab_size, cfg.model.pad_token_id, cfg.model.bos_token_id, cfg.model.eos_token_id = 1001, 0, 0, 0
+    cfg.output_dir = cfg.checkpoint_dir = str(tmp_path / "out")
+    arch = dict(hidden_size=64, num_hidden_layers=1, num_attention_heads=2, intermediate_size=128, image_size=224,
+                patch_size=16, num_channels=3, layer_norm_eps=1e-12)
+    orig = E.VIT_ARCHS["google/vit-base-patch16-224"]
+    E.VIT_ARCHS["google/vit-base-patch16-224"] = arch
+    try:
+        torch.manual_seed(0)
+        model = cm.ImageCaptioningModel(cfg)
+    finally:
+        E.VIT_ARCHS["google/vit-base-patch16-224"] = orig
+    _, val, _ = D.build_coco_dataloaders(cfg, StubTokenizer(), device="cuda")
+    vb = next(iter(val))
+    assert vb["caption_tokens"].shape[:2] == (3, 3) and vb["num_references"].tolist() == [1, 2, 3]
+    tr = CaptioningTrainer(cfg, model, None, val, StubTokenizer(), device="cuda", precision="fp32", total_steps=10)
+    loss, metrics = tr.validate()
+    assert np.isfinite(loss) and loss > 0 and np.isfinite(metrics["CIDEr"]) and metrics["CIDEr"] >= 0

@@ -14,11 +14,14 @@ pytestmark = pytest.mark.gpu
 cuda = pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
 
 
-@pytest.fixture(scope="module")
-def ops():
+@pytest.fixture(scope="module", params=[5, 6], ids=["gemm8p", "gemm8q"])
+def ops(request):
+    """Every test runs on both 256x256 kernels: the phased one-tile-per-WG kernel (5) and the
+    persistent register-epilogue kernel (6; epilogues it does not take fall back to 5)."""
     from capk import _lib, ops as _ops
     lib = _lib.load()
-    lib.capk_gemm_force_config(5)  # the 256x256 kernel
+    lib.capk_gemm_force_config(request.param)
+    _ops.FORCED_CFG = request.param
     yield _ops
     lib.capk_gemm_force_config(-1)
 
@@ -44,7 +47,8 @@ def test_layouts_and_tails(ops, ak, bk, M, N, K, out):
     b, B = _operand(N, K, bk, g, 1.0 / math.sqrt(K))
     C = torch.empty(M, N, device="cuda", dtype=out)
     ops.gemm(A, ak, B, bk, M, N, K, C, lda=A.stride(0), ldb=B.stride(0), ldc=C.stride(0))
-    assert _lib.load().capk_gemm_last_config() == 5
+    # (gemm8q falls back to gemm8p for K <= 64 and for a split-K padding a K-major operand)
+    assert _lib.load().capk_gemm_last_config() in (ops.FORCED_CFG, 5)
     ref = a.float() @ b.float().t()
     assert _rel(C, ref) < (1e-2 if out == torch.bfloat16 else 3e-3), (ak, bk, M, N, K)
 
@@ -88,3 +92,69 @@ def test_fused_epilogues(ops):
     a = pre.float().requires_grad_(True)
     F.gelu(a).backward(dy.float() @ w.float())
     assert _rel(dxa, a.grad) < 1e-2
+
+
+@cuda
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("K", [128, 192, 1000])
+def test_many_items_per_workgroup(ops, ak, bk, K):
+    """289 tiles (> 256 workgroups): the persistent kernel runs several items per WG with the
+    next item's first K-tiles loaded under the previous item's last ones and its epilogue
+    stores in flight; K = 128 is the shortest item (2 K-tiles), 1000 a K tail (MN-major)."""
+    if (ak or bk) and K % 64:
+        pytest.skip("K-major operands need K % 64 == 0 on the 256x256 kernels")
+    g = torch.Generator(device="cuda").manual_seed(K + 2 * ak + bk)
+    M, N = 17 * 256 - 40, 17 * 256 - 8
+    a, A = _operand(M, K, ak, g)
+    b, B = _operand(N, K, bk, g, 1.0 / math.sqrt(K))
+    bias = torch.randn(N, device="cuda", generator=g)
+    C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    ops.gemm(A, ak, B, bk, M, N, K, C, lda=A.stride(0), ldb=B.stride(0), ldc=C.stride(0), bias=bias)
+    ref = a.float() @ b.float().t() + bias
+    assert _rel(C, ref) < 1e-2
+    # the rows / columns of every tile landed where they belong (not only on average)
+    err = (C.float() - ref).abs().amax(dim=1)
+    assert float(err.max()) < 0.05 * float(ref.abs().max()), int(err.argmax())
+
+
+@cuda
+def test_epilogue_variants_exact_layout(ops):
+    """The register-direct epilogue's lane -> (row, column) map, checked element by element
+    with exact small-integer operands (asymmetric, so a transposed or permuted store shows):
+    plain, bias + residual, beta * C, dropout (mask from capk_dropout_mask), GELU with the
+    act' side output (CAPK_ACT_DERIV) and the backward multiply by aux."""
+    from capk._lib import ACT_BWD, ACT_DERIV, ACT_GELU_ERF
+    g = torch.Generator(device="cuda").manual_seed(11)
+    M, N, K = 3 * 256 + 72, 2 * 256 + 128, 128
+    a = torch.randint(-2, 3, (M, K), device="cuda", generator=g).bfloat16()
+    w = torch.randint(-2, 3, (N, K), device="cuda", generator=g).bfloat16()
+    ref = a.float() @ w.float().t()  # exact in fp32 and in bf16 (|x| <= 512)
+    C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    ops.gemm(a, True, w, True, M, N, K, C, lda=K, ldb=K, ldc=N)
+    assert torch.equal(C.float(), ref)
+    bias = torch.randint(-3, 4, (N,), device="cuda", generator=g).float()
+    res = torch.randint(-8, 9, (M, N), device="cuda", generator=g).bfloat16()
+    ops.gemm(a, True, w, True, M, N, K, C, lda=K, ldb=K, ldc=N, bias=bias, residual=res, ldr=N)
+    assert torch.equal(C.float(), ref + bias + res.float())
+    C0 = torch.randint(-8, 9, (M, N), device="cuda", generator=g).bfloat16()
+    C.copy_(C0)
+    ops.gemm(a, True, w, True, M, N, K, C, lda=K, ldb=K, ldc=N, beta=1.0)
+    assert torch.equal(C.float(), ref + C0.float())
+    # dropout: keep mask of index m * N + n, scale 2 (p = 0.5)
+    from capk import _lib
+    mask = torch.empty(M * N, device="cuda", dtype=torch.uint8)
+    L = _lib.load()
+    _lib.check(L.capk_dropout_mask(M * N, 0, 0.5, 1234, mask.data_ptr(), ops._stream()), "capk_dropout_mask")
+    ops.gemm(a, True, w, True, M, N, K, C, lda=K, ldb=K, ldc=N, drop=(0.5, 1234))
+    assert torch.equal(C.float(), ref * 2.0 * mask.view(M, N).float())
+    # forward GELU with act'(pre) kept; backward multiply by aux
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    y = ops.linear(x, w, bias, act=ACT_GELU_ERF | ACT_DERIV, preact=pre)
+    z = (x.float() @ w.float().t() + bias).requires_grad_(True)
+    F.gelu(z).sum().backward()
+    assert _rel(y, F.gelu(z.detach())) < 1e-2 and _rel(pre, z.grad) < 1e-2
+    dy = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    wt = torch.randn(N, N, device="cuda", generator=g).bfloat16() / 16
+    dx = ops.linear_dx(dy, wt, act_bwd=ACT_GELU_ERF | ACT_DERIV, aux=pre)
+    assert _rel(dx, (dy.float() @ wt.float()) * pre.float()) < 1e-2

@@ -113,3 +113,32 @@ def test_early_stopping_search_graphs_equal_eager():
     assert ref[0][0].shape[1] < 20, "the forced-EOS search should stop early"
     for r, g in zip(ref, got):
         _same(r, g)
+
+
+@cuda
+def test_short_search_then_full_search_graphs_equal_eager():
+    """A search that stops early captures only its first chunk(s); the next, full-length
+    search replays those and captures the rest.  The KV cache / spare roles the replayed
+    chunks leave behind must be the ones the later capture builds on (graphs._replay
+    restores them), else the later chunks read the stale cache buffer."""
+    dec = _decoder("transformer", seed=5)
+    bias = dec.output_layer.bias._capk_pad_master
+    orig = float(bias[50256])
+    # (encoder output, EOS logit boost): short, short, full, full
+    inputs = [(_enc(2, 11), 12.0), (_enc(2, 12), 12.0), (_enc(2, 13), 0.0), (_enc(2, 14), 0.0)]
+
+    def fn(x):
+        enc, boost = x
+        with torch.no_grad():
+            bias[50256] = orig + boost
+            ids, info = dec.generate(enc, 20, num_beams=5)
+        return [ids.clone(), info["sequences_scores"].clone(), info["beam_indices"].clone()]
+
+    try:
+        ref, got = _eager_then_graphed(fn, inputs)
+    finally:
+        with torch.no_grad():
+            bias[50256] = orig
+    assert ref[1][0].shape[1] < 20 and ref[2][0].shape[1] == 20, [r[0].shape for r in ref]
+    for r, g in zip(ref, got):
+        _same(r, g)
