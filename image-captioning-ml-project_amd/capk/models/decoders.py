@@ -10,9 +10,10 @@ from abc import ABC, abstractmethod
 import torch
 import torch.nn as nn
 
+from .. import ops
 from ..config import AttentionConfig, DecoderConfig, DecoderType
 from .gpt2 import GPT2DecoderCore
-from .lstm import LSTMDecoderCore, lstm_greedy
+from .lstm import LSTMDecoderCore, LSTMStepRunner, lstm_greedy
 from .transformer import TransformerDecoderCore
 
 
@@ -105,6 +106,10 @@ class LSTMDecoder(LSTMDecoderCore, CaptionDecoder):
                  embedding_dim: int = None):
         LSTMDecoderCore.__init__(self, config, attention_config, vocab_size, pad_token_id, embedding_dim)
         self.max_length = config.max_length
+        # the reference LSTMDecoder keeps no bos/eos ids, so its SCST sampler
+        # (trainer.py:404-407, 435) cannot run it; build_decoder sets the model's ids here
+        self.bos_token_id = 1
+        self.eos_token_id = None
 
     def forward(self, encoder_features, captions=None, caption_lengths=None, **kwargs):
         if captions is None:  # decoders.py:145-148 (D11: `config` restated as the decoder's own max_length)
@@ -116,9 +121,26 @@ class LSTMDecoder(LSTMDecoderCore, CaptionDecoder):
         return {"logits": logits, "attention_weights": weights}
 
     @torch.no_grad()
-    def generate(self, encoder_features, max_length, start_token_id=1, **kwargs):
-        return lstm_greedy(self, encoder_features["features"], encoder_features["pooled_features"], max_length,
-                           start_token_id)
+    def generate(self, encoder_features, max_length, start_token_id=1, num_beams=1, length_penalty=1.0,
+                 early_stopping=False, **kwargs):
+        """num_beams == 1: the reference's greedy loop (decoders.py:236-314: ids[:, t] = current
+        token from start_token_id, no EOS stop).  num_beams > 1 (the reference swallows it in
+        **kwargs): HF beam-search semantics (capk.beam) over the LSTM step with
+        prompt start_token_id and the model's eos id; returns (sequences, {"sequences_scores",
+        "beam_indices"})."""
+        feats, pooled = encoder_features["features"], encoder_features["pooled_features"]
+        if num_beams < 2:
+            return lstm_greedy(self, feats, pooled, max_length, start_token_id)
+        if self.eos_token_id is None:
+            raise ValueError("capk LSTMDecoder.generate(num_beams > 1) needs eos_token_id (set by build_decoder)")
+        from ..beam import beam_search
+        B = pooled.shape[0]
+        runner = LSTMStepRunner(self, feats, pooled, num_beams, max_length)
+        prompt = torch.full((B,), start_token_id, dtype=torch.long, device=pooled.device)
+        out = beam_search(runner.step, B, num_beams, max_length, prompt, self.eos_token_id,
+                          pad_token_id=self.pad_token_id, length_penalty=length_penalty,
+                          early_stopping=early_stopping, vocab_size=self.vocab_size)
+        return out["sequences"], {"sequences_scores": out["sequences_scores"], "beam_indices": out["beam_indices"]}
 
 
 class GPT2Decoder(GPT2DecoderCore, CaptionDecoder):
@@ -145,8 +167,7 @@ class GPT2Decoder(GPT2DecoderCore, CaptionDecoder):
         one-token bos prompt with the image prefix as cache (D7) -> HF beam search
         semantics on the KV-cached decoder.  Returns (sequences, info)."""
         if num_beams < 2:
-            raise NotImplementedError("capk GPT2Decoder.generate: greedy (num_beams=1) is not on the hot path; "
-                                      "the reference always beam-searches (decoders.py:623)")
+            return _gpt2_greedy(self, encoder_features["pooled_features"], max_length), {}
         from .. import graphs
         from ..beam import beam_search
         from .gpt2 import GPT2KVRunner
@@ -166,6 +187,35 @@ class GPT2Decoder(GPT2DecoderCore, CaptionDecoder):
         return out["sequences"], {"sequences_scores": out["sequences_scores"], "beam_indices": out["beam_indices"]}
 
 
+def _gpt2_greedy(self, pooled, max_length):
+    """HF generate(num_beams=1, do_sample=False) from the one-token bos prompt
+    (GenerationMixin._sample with greedy selection, transformers/generation/utils.py):
+    next = argmax(last logits); rows that already emitted eos get pad_token_id
+    (next * unfinished + pad * (1 - unfinished)); stop when every row has finished or the
+    sequence reached max_length (prompt included).  KV-cached decode, argmax on the device."""
+    from .gpt2 import GPT2KVRunner
+    B, dev = pooled.shape[0], pooled.device
+    runner = GPT2KVRunner(self, pooled, 1, max_length)
+    ids = torch.empty(B, max_length, dtype=torch.long, device=dev)
+    ids[:, 0] = self.bos_token_id
+    unfinished = torch.ones(B, dtype=torch.bool, device=dev)
+    pad = self.pad_token_id if self.pad_token_id is not None else self.eos_token_id
+    cur = ids[:, 0].contiguous()
+    T = 1
+    for t in range(1, max_length):
+        logits = runner.step(t, cur, None)
+        nxt = torch.empty(B, dtype=torch.long, device=dev)
+        ops.argmax_rows(logits, self.vocab_size, nxt)
+        nxt = torch.where(unfinished, nxt, torch.full_like(nxt, pad))
+        ids[:, t] = nxt
+        cur = nxt
+        T = t + 1
+        unfinished &= nxt != self.eos_token_id
+        if not bool(unfinished.any()):
+            break
+    return ids[:, :T]
+
+
 def build_decoder(config: DecoderConfig, attention_config: AttentionConfig, vocab_size: int, pad_token_id: int,
                   bos_token_id: int, eos_token_id: int) -> CaptionDecoder:
     """decoders.py:659-692 (with D2: string types accepted; D3: attention hidden_dim filled)."""
@@ -176,5 +226,7 @@ def build_decoder(config: DecoderConfig, attention_config: AttentionConfig, voca
     if dt == DecoderType.GPT2:
         return GPT2Decoder(config, vocab_size, pad_token_id, bos_token_id, eos_token_id)
     if dt == DecoderType.LSTM:
-        return LSTMDecoder(config, attention_config, vocab_size, pad_token_id)
+        d = LSTMDecoder(config, attention_config, vocab_size, pad_token_id)
+        d.bos_token_id, d.eos_token_id = bos_token_id, eos_token_id
+        return d
     raise ValueError(f"Unsupported decoder type: {config.decoder_type}")

@@ -14,7 +14,8 @@ import torch.nn as nn
 
 from ..config import EncoderConfig, EncoderType
 from .clip import CLIP_ARCHS, CapkCLIPVisionModel
-from .common import CapkModule
+from .. import ops
+from .common import CapkModule, G, W
 from .resnet import RESNET_ARCHS, CapkResNetModel, _ResNetHeadFn
 from .swin import SWIN_ARCHS, CapkSwinModel, SwinHeadFn
 from .vit import VIT_ARCHS, CapkViTModel
@@ -26,6 +27,64 @@ class ImageEncoder(nn.Module, ABC):
     @abstractmethod
     def forward(self, images):
         ...
+
+
+class _TokenProjFn(torch.autograd.Function):
+    """``self.proj`` of the ViT / CLIP encoders when hidden_size != feature_dim
+    (encoders.py:108-112, 199-203): features = proj(last_hidden_state[:, 1:]),
+    pooled = proj(pooler_output).  The projection runs over every sequence row (the CLS
+    row's output is never read: 1 of N rows) so the result keeps the strided-view
+    geometry the decoders consume; its backward scatters the patch-row gradient into a
+    zero CLS row with one row gather, then dW / db / dX as for any Linear."""
+
+    @staticmethod
+    def forward(ctx, seq, pooled, anchor, enc, B, N):
+        ctx.set_materialize_grads(False)
+        dt = enc.cdtype
+        proj = enc.proj
+        wt = W(proj.weight, dt)
+        out = ops.linear(seq, wt, proj.bias.detach())
+        pout = ops.linear(pooled.contiguous(), wt, proj.bias.detach())
+        ctx.enc, ctx.B, ctx.N = enc, B, N
+        ctx.saved = (seq, pooled)
+        F = out.shape[1]
+        return out.view(B, N, F)[:, 1:], pout
+
+    @staticmethod
+    def backward(ctx, dfeat, dpooled):
+        enc, B, N = ctx.enc, ctx.B, ctx.N
+        seq, pooled = ctx.saved
+        ctx.saved = None
+        dt = enc.cdtype
+        proj = enc.proj
+        wt = W(proj.weight, dt)
+        gw, gb = G(proj.weight), G(proj.bias)
+        F = proj.weight.shape[0]
+        dseq = dpi = None
+        acc = False
+        if dfeat is not None:
+            dfull = ops.zero_(torch.empty(B * N, F, dtype=seq.dtype, device=seq.device))
+            idx = torch.arange(N - 1, dtype=torch.int32, device=seq.device)
+            ops.gather_rows(dfeat, idx, dfull, B, N - 1, F, dfeat.stride(1), dfeat.stride(0), F, N * F, y_off=F)
+            ops.linear_dw(dfull, seq, gw)
+            ops.colsum(dfull, gb)
+            dseq = ops.linear_dx(dfull, wt)
+            acc = True
+        if dpooled is not None:
+            dpooled = dpooled.contiguous()
+            ops.linear_dw(dpooled, pooled.contiguous(), gw, accumulate=acc)
+            ops.colsum(dpooled, gb, accumulate=acc)
+            dpi = ops.linear_dx(dpooled, wt)
+        return dseq, dpi, None, None, None, None
+
+
+def _token_proj(enc, seq, pooled, B):
+    """(features, pooled) of a ViT-style encoder: strided view of the sequence without CLS
+    (no copy) when proj is the identity, else _TokenProjFn."""
+    N = seq.shape[0] // B
+    if isinstance(enc.proj, nn.Linear):
+        return _TokenProjFn.apply(seq, pooled, enc.proj.weight, enc, B, N)
+    return seq.view(B, N, seq.shape[1])[:, 1:], pooled
 
 
 class ViTEncoder(ImageEncoder):
@@ -40,9 +99,8 @@ class ViTEncoder(ImageEncoder):
             arch = VIT_ARCHS[name]
         self.model = CapkViTModel(arch)
         self.feature_dim = config.feature_dim
-        if arch["hidden_size"] != self.feature_dim:
-            raise NotImplementedError("capk ViTEncoder: hidden_size != feature_dim projection not on the hot path")
-        self.proj = nn.Identity()  # encoders.py:109-113 (hidden == feature_dim)
+        hidden = arch["hidden_size"]  # encoders.py:108-112
+        self.proj = nn.Linear(hidden, self.feature_dim) if hidden != self.feature_dim else nn.Identity()
         if config.freeze:
             for p in self.model.parameters():
                 p.requires_grad = False
@@ -51,8 +109,7 @@ class ViTEncoder(ImageEncoder):
         B = images.shape[0]
         seq, pooled = self.model(images)
         N = seq.shape[0] // B
-        D = seq.shape[1]
-        features = seq.view(B, N, D)[:, 1:]  # encoders.py:122 (drop CLS) — strided view, no copy
+        features, pooled = _token_proj(self, seq, pooled, B)  # encoders.py:122-127 (drop CLS, proj)
         # encoders.py:130-131 returns a float all-ones mask; restated as a bool "valid" mask (D4)
         mask = torch.ones(B, N - 1, dtype=torch.bool, device=images.device)
         return {"features": features, "pooled_features": pooled, "attention_mask": mask}
@@ -71,9 +128,8 @@ class CLIPEncoder(ImageEncoder):
             arch = CLIP_ARCHS[name]
         self.model = CapkCLIPVisionModel(arch)
         self.feature_dim = config.feature_dim
-        if arch["hidden_size"] != self.feature_dim:
-            raise NotImplementedError("capk CLIPEncoder: hidden_size != feature_dim projection not on the hot path")
-        self.proj = nn.Identity()  # encoders.py:199-203
+        hidden = arch["hidden_size"]  # encoders.py:199-203
+        self.proj = nn.Linear(hidden, self.feature_dim) if hidden != self.feature_dim else nn.Identity()
         if config.freeze:
             for p in self.model.parameters():
                 p.requires_grad = False
@@ -82,8 +138,7 @@ class CLIPEncoder(ImageEncoder):
         B = images.shape[0]
         seq, pooled = self.model(images)
         N = seq.shape[0] // B
-        D = seq.shape[1]
-        features = seq.view(B, N, D)[:, 1:]  # encoders.py:213 — strided view of the unnormalised sequence
+        features, pooled = _token_proj(self, seq, pooled, B)  # encoders.py:213-221 (unnormalised sequence)
         mask = torch.ones(B, N - 1, dtype=torch.bool, device=images.device)  # D4 restatement
         return {"features": features, "pooled_features": pooled, "attention_mask": mask}
 
@@ -103,18 +158,17 @@ class ResNetEncoder(ImageEncoder, CapkModule):
             arch = RESNET_ARCHS[name]
         self.model = CapkResNetModel(arch)
         self.feature_dim = config.feature_dim
-        hidden = arch["hidden_sizes"][-1]
-        if hidden == self.feature_dim:
-            raise NotImplementedError("capk ResNetEncoder: identity projection (hidden == feature_dim) not wired")
-        self.proj = nn.Linear(hidden, self.feature_dim)  # encoders.py:50-54
+        hidden = arch["hidden_sizes"][-1]  # encoders.py:50-54
+        self.proj = nn.Linear(hidden, self.feature_dim) if hidden != self.feature_dim else nn.Identity()
         if config.freeze:
             for p in self.model.parameters():
                 p.requires_grad = False
 
     def forward(self, images):
         x, (B, H, W) = self.model(images)
-        feats, pooled = _ResNetHeadFn.apply(x, self.proj.weight, self, B, H, W)
-        features = feats.view(B, H * W, self.feature_dim)
+        anchor = self.proj.weight if isinstance(self.proj, nn.Linear) else x
+        feats, pooled = _ResNetHeadFn.apply(x, anchor, self, B, H, W)
+        features = feats.view(B, H * W, feats.shape[1])
         mask = torch.ones(B, H * W, dtype=torch.bool, device=images.device)  # D4 restatement
         return {"features": features, "pooled_features": pooled, "attention_mask": mask}
 

@@ -278,3 +278,98 @@ def lstm_greedy(m, features, pooled, max_length, start_token_id):
         logits = ops.linear(ctx[b], wout, _pad_bias(ol))
         ops.argmax_rows(logits, V, cur)
     return ids, {"attention_weights": H.w.permute(1, 0, 2)}
+
+
+class _LSTMBank:
+    """One copy of the per-row decode state: h and c of every layer ([L, R, D]; c fp32) and
+    the previous attention context [R, D]."""
+
+    def __init__(self, L, R, D, dt, dev):
+        self.h = torch.empty(L, R, D, dtype=dt, device=dev)
+        self.c = torch.empty(L, R, D, dtype=torch.float32, device=dev)
+        self.ctx = torch.empty(R, D, dtype=dt, device=dev)
+        self.device = dev
+
+
+class LSTMStepRunner:
+    """Incremental decode of the LSTM decoder for beam search and SCST sampling: the
+    generate() loop body of decoders.py:266-303 (embed the current token, concat the
+    previous context, one nn.LSTM step over all layers, attention with memory = h[-1] /
+    c[-1], logits = output_layer(context)) over R = B * num_beams rows.  The image
+    features, h0/c0 and the hoisted key/value projections are replicated per beam once;
+    a beam reorder gathers the (h, c, context) rows of every layer into the spare bank
+    (three launches) — the LSTM counterpart of the KV-cache reorder of the Transformer /
+    GPT-2 runners (HF Cache.reorder_cache).  ``step(cur_len, ids, reorder)`` follows the
+    capk.beam step protocol and returns [R, Vp] logits (V valid columns)."""
+
+    def __init__(self, m, features, pooled, num_beams, max_length):
+        dt = m.cdtype
+        if features.dtype != dt or pooled.dtype != dt:
+            raise TypeError(f"capk LSTMDecoder: feature dtype {features.dtype}/{pooled.dtype} != compute dtype {dt}")
+        dev = pooled.device
+        B, S, D = features.shape
+        L = m.num_layers
+        self.m, self.dt, self.k, self.B, self.D, self.L = m, dt, num_beams, B, D, L
+        R = self.R = B * num_beams
+        self.max_length = max_length
+        self.rep_idx = torch.arange(R, dtype=torch.int32, device=dev) // num_beams
+        pooled = pooled.contiguous()
+        h0 = ops.linear(pooled, W(m.init_h.weight, dt), m.init_h.bias.detach())  # [B, L*D]
+        c0 = ops.linear(pooled, W(m.init_c.weight, dt), m.init_c.bias.detach(), out_dtype=torch.float32)
+        self._banks = (_LSTMBank(L, R, D, dt, dev), _LSTMBank(L, R, D, dt, dev))
+        self.reset()
+        b0 = self.cache
+        # layer l of h0/c0 = columns [l*D, (l+1)*D) (decoders.py:122-135), replicated per beam
+        ops.gather_rows(h0, self.rep_idx, b0.h, L, R, D, L * D, D, D, R * D)
+        ops.gather_rows(c0, self.rep_idx, b0.c, L, R, D, L * D, D, D, R * D)
+        ops.zero_(b0.ctx)  # prev_context = zeros (decoders.py:263-264)
+        if num_beams > 1:
+            fr = torch.empty(R, S, D, dtype=dt, device=dev)
+            ops.gather_rows(features, self.rep_idx, fr, 1, R, S * D, features.stride(0), 0, S * D, 0)
+        else:
+            fr = features
+        self.H = m.attention.hoist(fr, fr, None, max_length)
+        self.gates = torch.empty(R, 4 * D, dtype=dt, device=dev)
+        self.act = torch.empty(R, 4 * D, dtype=dt, device=dev)
+        self.logits = torch.empty(R, m.vocab_pad, dtype=dt, device=dev)
+        ol = m.output_layer
+        self.wout = ol.weight._capk_pad_bf16 if dt == torch.bfloat16 else ol.weight._capk_pad_master
+        self.bout = _pad_bias(ol)
+
+    def reset(self):
+        self.cache, self.spare = self._banks
+
+    def _reorder(self, idx):
+        s, d = self.cache, self.spare
+        L, R, D = self.L, self.R, self.D
+        ops.gather_rows(s.h, idx, d.h, L, R, D, D, R * D, D, R * D)
+        ops.gather_rows(s.c, idx, d.c, L, R, D, D, R * D, D, R * D)
+        ops.gather_rows(s.ctx, idx, d.ctx, 1, R, D, D, 0, D, 0)
+        self.cache, self.spare = d, s
+
+    def step(self, cur_len, ids, reorder_idx):
+        m, dt, R, D, L = self.m, self.dt, self.R, self.D, self.L
+        E = m.embedding_dim
+        lstm = m.lstm
+        if reorder_idx is not None:
+            self._reorder(reorder_idx)
+        src, dst = self.cache, self.spare
+        t = cur_len - 1
+        emb = ops.embedding_fwd(ids.view(R, 1), m.embedding.weight.detach(), None, 0, dt)
+        w_ih0 = W(lstm.weight_ih_l0, dt)
+        gates = self.gates
+        for layer in range(L):
+            if layer == 0:
+                ops.linear(emb, w_ih0[:, :E], lstm.bias_ih_l0.detach(), out=gates)
+                ops.gemm(src.ctx, True, w_ih0[:, E:], True, R, 4 * D, D, gates, lda=D, ldb=E + D, ldc=4 * D,
+                         beta=1.0)
+            else:
+                ops.linear(dst.h[layer - 1], W(lstm.w("weight_ih", layer), dt), lstm.w("bias_ih", layer).detach(),
+                           out=gates)
+            ops.gemm(src.h[layer], True, W(lstm.w("weight_hh", layer), dt), True, R, 4 * D, D, gates, lda=D, ldb=D,
+                     ldc=4 * D, beta=1.0, bias=lstm.w("bias_hh", layer).detach())
+            ops.lstm_cell_fwd(gates, src.c[layer], dst.c[layer], dst.h[layer], self.act)
+        m.attention.step_fwd(self.H, t, dst.h[L - 1], dst.h[L - 1], dst.c[L - 1], dst.ctx)
+        ops.linear(dst.ctx, self.wout, self.bout, out=self.logits)
+        self.cache, self.spare = dst, src
+        return self.logits

@@ -347,19 +347,24 @@ class _ResNetHeadFn(torch.autograd.Function):
     """ResNetEncoder.forward (src/models/encoders.py:60-91) with the SURVEY §0.1 D6
     restatement: features = proj(last_hidden_state.flatten(2).transpose(1, 2)),
     pooled = proj(AdaptiveAvgPool2d(1)(last_hidden_state).flatten(1)).  The channels-last
-    rows ARE the flattened/transposed map, so `features` is one GEMM on them."""
+    rows ARE the flattened/transposed map, so `features` is one GEMM on them.  proj is
+    nn.Identity when hidden_sizes[-1] == feature_dim (encoders.py:50-54): features are then
+    the map rows themselves and pooled the average-pooled map."""
 
     @staticmethod
     def forward(ctx, x, anchor, enc, B, H, W):
         ctx.set_materialize_grads(False)
         dt = enc.cdtype
-        proj = enc.proj
+        proj = enc.proj if isinstance(enc.proj, nn.Linear) else None
         C = x.shape[1]
         pooled_raw = ops.avgpool_fwd(x, B, H, W, C, 1, 1)
+        ctx.enc, ctx.geo = enc, (B, H, W, C)
+        if proj is None:
+            ctx.saved = None
+            return x.view_as(x), pooled_raw
         wt = proj.weight._capk_bf16 if dt == torch.bfloat16 else proj.weight.detach()
         feats = ops.linear(x, wt, proj.bias.detach())
         pooled = ops.linear(pooled_raw, wt, proj.bias.detach())
-        ctx.enc, ctx.geo = enc, (B, H, W, C)
         ctx.saved = (x, pooled_raw)
         return feats, pooled
 
@@ -368,9 +373,15 @@ class _ResNetHeadFn(torch.autograd.Function):
         enc = ctx.enc
         dt = enc.cdtype
         B, H, W, C = ctx.geo
+        proj = enc.proj if isinstance(enc.proj, nn.Linear) else None
+        if proj is None:
+            dx = dfeat.contiguous() if dfeat is not None else None
+            if dpooled is not None:
+                dx = ops.avgpool_bwd(dpooled.contiguous(), B, H, W, C, 1, 1,
+                                     dx=dx.clone() if dx is not None else None, beta=1.0 if dx is not None else 0.0)
+            return dx, None, None, None, None, None
         x, pooled_raw = ctx.saved
         ctx.saved = None
-        proj = enc.proj
         wt = proj.weight._capk_bf16 if dt == torch.bfloat16 else proj.weight.detach()
         gw, gb = proj.weight._capk_grad, proj.bias._capk_grad
         dx = None

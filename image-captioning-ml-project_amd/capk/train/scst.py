@@ -14,8 +14,15 @@ _calculate_rewards (src/train/trainer.py:319-484) with the SURVEY fixes:
         forward + backward over the sampled sequence produces the same log-probabilities
         and gradients.  Sampling and scoring both use generate()'s attention semantics
         (no key-padding mask inside a generated prefix).
-* baseline — model.generate (greedy for the Transformer decoder, beam-4 for GPT-2), reusing
-        the encoder features of the step instead of re-encoding the images.
+* baseline — model.generate (greedy for the Transformer decoder, beam-4 for GPT-2, the
+        reference's greedy loop from start token 1 for the LSTM decoder), reusing the encoder
+        features of the step instead of re-encoding the images.
+* LSTM decoder — the reference sampler reads ``decoder.bos_token_id`` / ``eos_token_id``,
+        which its LSTMDecoder does not define (``--use_rl --decoder_type lstm`` raises there);
+        here build_decoder gives the LSTM decoder the model's ids and the sampler runs the
+        incremental LSTM step (capk.models.lstm.LSTMStepRunner): the reference's full
+        re-decode of the prefix computes the same last-position logits (no dropout in the
+        sampler, the hidden state of a prefix does not depend on later tokens).
 """
 import numpy as np
 import torch
@@ -99,8 +106,15 @@ def sample_captions(decoder, encoder_features, max_length, seed, check_every=EOS
     (seed, step, row), so steps sampled past the stop are simply cut off and the result
     equals a per-step check, without a host sync per token."""
     from .. import graphs
-    from ..models.decoders import GPT2Decoder, TransformerDecoder
-    if isinstance(decoder, TransformerDecoder):
+    from ..models.decoders import GPT2Decoder, LSTMDecoder, TransformerDecoder
+    use_graphs = graphs.active()
+    if isinstance(decoder, LSTMDecoder):
+        from ..models.lstm import LSTMStepRunner
+        feats, pooled = encoder_features["features"], encoder_features["pooled_features"]
+        make = lambda: LSTMStepRunner(decoder, feats, pooled, 1, max_length)  # noqa: E731
+        src = pooled
+        use_graphs = False  # the runner's hoisted key/value buffers are built per call (eager loop)
+    elif isinstance(decoder, TransformerDecoder):
         from ..models.transformer import KVDecodeRunner, _mem_geometry
         feats = encoder_features["features"]
         make = lambda: KVDecodeRunner(decoder, feats, 1, max_length)  # noqa: E731
@@ -113,8 +127,8 @@ def sample_captions(decoder, encoder_features, max_length, seed, check_every=EOS
         key = ("gpt2", pooled.shape[0], pooled.dtype, 1, max_length)
         src = pooled
     else:
-        raise NotImplementedError(f"capk SCST sampler: {type(decoder).__name__} (Transformer / GPT-2 decoders)")
-    if graphs.active():  # cached runner, chunks of steps replayed as HIP graphs (capk/graphs.py)
+        raise TypeError(f"capk SCST sampler: unknown decoder {type(decoder).__name__}")
+    if use_graphs:  # cached runner, chunks of steps replayed as HIP graphs (capk/graphs.py)
         runner = graphs.runner_for(decoder, ("sample",) + key, make)
         runner.load(src)
         if runner.warm:
@@ -166,12 +180,13 @@ def scst_step(model, images, references, optimizer, lr, seed, max_length=20, bas
     refs = [[list(x) for x in rs] for rs in references]
     r_s, r_b = cider_d(samp, refs), cider_d(base, refs)
     adv = torch.tensor(r_s - r_b, dtype=torch.float32, device=ids.device)
-    if hasattr(dec, "forward_logits"):
-        from ..models.decoders import GPT2Decoder
-        if isinstance(dec, GPT2Decoder):
-            logits = dec.forward_logits(enc["pooled_features"], ids, use_pad_mask=False)
-        else:
-            logits, _ = dec.forward_logits(enc["features"], ids, use_pad_mask=False)
+    from ..models.decoders import GPT2Decoder, LSTMDecoder
+    if isinstance(dec, GPT2Decoder):
+        logits = dec.forward_logits(enc["pooled_features"], ids, use_pad_mask=False)
+    elif isinstance(dec, LSTMDecoder):
+        logits, _ = dec.forward_logits(enc["features"], enc["pooled_features"], ids)
+    else:
+        logits, _ = dec.forward_logits(enc["features"], ids, use_pad_mask=False)
     loss = policy_gradient_loss(logits, ids, adv, eos)
     loss.backward()
     if bucketer is not None:  # DP: rewards are rank-local, gradients are averaged

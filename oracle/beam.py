@@ -102,3 +102,22 @@ def beam_search(logits_fn, batch_size, num_beams, max_length, bos, eos, pad=None
     return {"sequences": sequences[:, 0, :out_len], "sequences_scores": beam_scores[:, 0],
             "beam_indices": best_bi[:, :max_gen], "steps": cur_len - prompt_len,
             "all_sequences": sequences, "all_scores": beam_scores, "is_sent_finished": is_sent_finished}
+
+
+def greedy_search(logits_fn, batch_size, max_length, eos, pad=None, prompt=None, bos=None):
+    """HF ``generate(num_beams=1, do_sample=False)`` (transformers 5.15 GenerationMixin._sample
+    with greedy selection, transformers/generation/utils.py): next = argmax(last logits);
+    with an eos id, finished rows emit ``pad`` (``next * unfinished + pad * (1 - unfinished)``);
+    a row finishes on eos; the loop stops when every row finished or the length reached
+    max_length (prompt of length 1 included).  Returns sequences [B, <= max_length]."""
+    fill = pad if pad is not None else eos
+    seqs = (prompt.view(batch_size, 1) if prompt is not None else torch.full((batch_size, 1), bos)).long()
+    unfinished = torch.ones(batch_size, dtype=torch.long)
+    while seqs.shape[1] < max_length:
+        nxt = logits_fn(seqs).float().argmax(-1)
+        nxt = nxt * unfinished + fill * (1 - unfinished)
+        seqs = torch.cat([seqs, nxt[:, None]], 1)
+        unfinished = unfinished & (nxt != eos).long()
+        if unfinished.max() == 0:
+            break
+    return seqs

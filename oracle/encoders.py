@@ -72,12 +72,18 @@ def vit_model(p, images, num_layers, num_heads, patch_size, eps=1e-12):
     return seq, pooled
 
 
-def vit_encoder(p, images, num_layers, num_heads, patch_size, eps=1e-12):
+def _proj(x, proj):
+    """encoders.py:108-112 / 199-203: nn.Linear(hidden, feature_dim) when the sizes differ
+    (proj = (weight, bias)), nn.Identity otherwise (proj = None)."""
+    return x if proj is None else F.linear(x, proj[0], proj[1])
+
+
+def vit_encoder(p, images, num_layers, num_heads, patch_size, eps=1e-12, proj=None):
     """ViTEncoder.forward (src/models/encoders.py:118-137): features drop CLS
-    (122), proj = Identity when hidden == feature_dim (109-113), all-ones mask
+    (122), proj applied to features and pooled (123, 127), all-ones mask
     (130-131; restated as None = no key padding)."""
     seq, pooled = vit_model(p, images, num_layers, num_heads, patch_size, eps)
-    return {"features": seq[:, 1:], "pooled_features": pooled, "attention_mask": None}
+    return {"features": _proj(seq[:, 1:], proj), "pooled_features": _proj(pooled, proj), "attention_mask": None}
 
 
 def clip_vision(p, images, num_layers, num_heads, patch_size, eps=1e-5):
@@ -107,11 +113,11 @@ def clip_vision(p, images, num_layers, num_heads, patch_size, eps=1e-5):
     return x, pooled
 
 
-def clip_encoder(p, images, num_layers, num_heads, patch_size, eps=1e-5):
+def clip_encoder(p, images, num_layers, num_heads, patch_size, eps=1e-5, proj=None):
     """CLIPEncoder.forward (src/models/encoders.py:209-230): features =
-    last_hidden_state[:, 1:] (no post-LN), pooled = pooler_output, proj = Identity."""
+    proj(last_hidden_state[:, 1:]) (no post-LN), pooled = proj(pooler_output)."""
     seq, pooled = clip_vision(p, images, num_layers, num_heads, patch_size, eps)
-    return {"features": seq[:, 1:], "pooled_features": pooled, "attention_mask": None}
+    return {"features": _proj(seq[:, 1:], proj), "pooled_features": _proj(pooled, proj), "attention_mask": None}
 
 
 # ------------------------------------------------------------------ ResNet (A3) --
@@ -151,11 +157,13 @@ def resnet_model(p, images, hidden_sizes, depths, training=True, state=None, dow
 
 def resnet_encoder(p, images, hidden_sizes, depths, training=True, state=None):
     """ResNetEncoder.forward (src/models/encoders.py:60-91) with the SURVEY §0.1 D6
-    restatement: features = proj(map.flatten(2).transpose(1,2)), pooled = proj(pool.flatten(1))."""
+    restatement: features = proj(map.flatten(2).transpose(1,2)), pooled = proj(pool.flatten(1));
+    proj = Identity when hidden_sizes[-1] == feature_dim (no "proj.*" entries, encoders.py:50-54)."""
     last, pool = resnet_model(_strip(p, "model."), images, hidden_sizes, depths, training,
                               None if state is None else _strip(state, "model."))
-    feats = F.linear(last.flatten(2).transpose(1, 2), p["proj.weight"], p["proj.bias"])
-    pooled = F.linear(pool.flatten(1), p["proj.weight"], p["proj.bias"])
+    pr = (p["proj.weight"], p["proj.bias"]) if "proj.weight" in p else None
+    feats = _proj(last.flatten(2).transpose(1, 2), pr)
+    pooled = _proj(pool.flatten(1), pr)
     return {"features": feats, "pooled_features": pooled}
 
 

@@ -9,6 +9,9 @@ stores the GPT-2 weights, the generate() arguments and its outputs
 (sequences, sequences_scores, beam_indices).
 
 Run in the build container:  python oracle/gen_beam_golden.py
+``python oracle/gen_beam_golden.py greedy`` writes tests/golden/greedy_gpt2.npz instead:
+HF generate(num_beams=1) (greedy, the GPT2Decoder.generate(num_beams=1) path) on the same
+kind of tiny models, pinning oracle/beam.py greedy_search.
 """
 import os
 
@@ -18,6 +21,12 @@ from transformers import GPT2Config, GPT2LMHeadModel
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "tests", "golden", "beam_gpt2.npz")
+GREEDY_OUT = os.path.join(ROOT, "tests", "golden", "greedy_gpt2.npz")
+# (name, batch, max_length, bos, eos, pad): pad != eos exercises the finished-row fill
+GREEDY_CASES = [
+    ("greedy_ref_like", 4, 12, 60, 60, 60),
+    ("greedy_eos_pad", 4, 14, 0, 7, 5),
+]
 
 # (name, batch, num_beams, max_length, bos, eos, length_penalty, early_stopping)
 CASES = [
@@ -63,5 +72,26 @@ def main():
     print("wrote", OUT, os.path.getsize(OUT))
 
 
+def main_greedy():
+    out = {}
+    for i, (name, B, L, bos, eos, pad) in enumerate(GREEDY_CASES):
+        cfg, m = tiny_gpt2(200 + i)
+        ids = torch.tensor([bos, 3, 11, 29][:B], dtype=torch.long)[:, None]
+        with torch.no_grad():
+            g = m.generate(input_ids=ids, attention_mask=torch.ones_like(ids), max_length=L, num_beams=1,
+                           pad_token_id=pad, bos_token_id=bos, eos_token_id=eos, do_sample=False)
+        out[f"{name}/args"] = np.array([B, L, bos, eos, pad], dtype=np.int64)
+        out[f"{name}/input_ids"] = ids.numpy()
+        out[f"{name}/sequences"] = g.numpy()
+        for kname, v in m.state_dict().items():
+            if kname.endswith("attn.bias") or kname.endswith("masked_bias"):
+                continue
+            out[f"{name}/w/{kname}"] = v.float().numpy()
+        print(name, g.tolist())
+    np.savez_compressed(GREEDY_OUT, **out)
+    print("wrote", GREEDY_OUT, os.path.getsize(GREEDY_OUT))
+
+
 if __name__ == "__main__":
-    main()
+    import sys
+    main_greedy() if sys.argv[1:] == ["greedy"] else main()

@@ -16,6 +16,8 @@ run() {  # name seconds cmd...
 }
 for step in "$@"; do
   case $step in
+    sweep) CFG=6 run sweep 200 python tools/gemm_sweep_check.py ;;
+    gemmtests) run gemmtests 400 python -u -m pytest tests/test_gpu_gemm.py tests/test_gpu_kernels.py -q -rf --timeout 120 --timeout-method thread ;;
     tests) run tests 600 python -u -m pytest tests -m gpu -q -rf --timeout 240 --timeout-method thread ;;
     smoke) run smoke 240 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench3) run bench_config3 480 python bench.py --steps 10 --warmup 3 ;;

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-from oracle.beam import beam_search
+from oracle.beam import beam_search, greedy_search
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "beam_gpt2.npz")
 CASES = ["ref_like_k5", "eos_k4_lp08", "eos_k5_es"]
@@ -45,3 +45,23 @@ def test_oracle_beam_matches_hf_generate(name):
     assert torch.equal(out["sequences"], torch.from_numpy(z[f"{name}/sequences"]))
     assert torch.equal(out["beam_indices"], torch.from_numpy(z[f"{name}/beam_indices"]))
     np.testing.assert_allclose(out["sequences_scores"].numpy(), z[f"{name}/sequences_scores"], rtol=1e-5, atol=1e-6)
+
+
+GREEDY = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "greedy_gpt2.npz")
+
+
+@pytest.mark.parametrize("name", ["greedy_ref_like", "greedy_eos_pad"])
+def test_oracle_greedy_matches_hf_generate(name):
+    """oracle greedy_search vs HF generate(num_beams=1) (GPT2Decoder.generate(num_beams=1),
+    decoders.py:645-654), tests/golden/greedy_gpt2.npz: bit-exact sequences."""
+    z = np.load(GREEDY)
+    B, L, bos, eos, pad = (int(v) for v in z[f"{name}/args"])
+    m = _gpt2(z, name)
+    prompt = torch.from_numpy(z[f"{name}/input_ids"])
+
+    def logits_fn(seqs):
+        with torch.no_grad():
+            return m(input_ids=seqs).logits[:, -1, :]
+
+    out = greedy_search(logits_fn, B, L, eos=eos, pad=pad, prompt=prompt)
+    assert torch.equal(out, torch.from_numpy(z[f"{name}/sequences"]))
