@@ -324,10 +324,13 @@ def run_config5(args, world, rank, device):
     model.train()
     upd = [0]
     last = [None]
+    phases = {}
+    timing = [False]
 
     def step():
         last[0] = scst_step(model, images, refs, opt, lr=cfg.training.learning_rate, seed=0x5C57 + upd[0],
-                            max_length=20, baseline_kwargs={"num_beams": 4}, bucketer=bucketer)
+                            max_length=20, baseline_kwargs={"num_beams": 4}, bucketer=bucketer,
+                            phase_times=phases if timing[0] else None)
         upd[0] += 1
 
     for _ in range(args.warmup):
@@ -335,6 +338,12 @@ def run_config5(args, world, rank, device):
     ops.GEMM_TIMER.start()
     elapsed = timed_steps(step, args.steps, 0, world, torch.cuda.synchronize, device)
     ops.GEMM_TIMER.stop()
+    # per-phase breakdown from separate (untimed) updates: HIP events between the phases
+    timing[0] = True
+    for _ in range(2):
+        step()
+    timing[0] = False
+    phase_ms = {k: round(v / 2, 3) for k, v in phases.items()}
     gem = ops.GEMM_TIMER.summary()
     beam = None
     if args.beam_batch > 0:
@@ -374,6 +383,9 @@ def run_config5(args, world, rank, device):
                                    "tflops": round(bf["tflops"], 1), "frac_of_bf16_peak": round(bf["tflops"] / PEAK_BF16_TFLOPS, 4)},
                      "gemm_share_of_step": round(gem["total_ms"] / (elapsed * 1e3), 3)},
         "model_flops": {"per_image": fpi, "tflops": round(fpi * value / world / 1e12, 1)},
+        "phases_ms": dict(phase_ms, note="GPU ms per update between HIP events on the compute stream (2 extra "
+                                         "untimed updates); cider_host = host CIDEr-D scoring, overlapped with "
+                                         "the teacher-forced forward"),
         "final_loss": round(float(loss), 5), "reward_sample": round(rs, 4), "reward_baseline": round(rb, 4),
         "process_group": process_group(world),
     }

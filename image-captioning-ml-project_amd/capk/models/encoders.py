@@ -15,7 +15,7 @@ import torch.nn as nn
 from ..config import EncoderConfig, EncoderType
 from .clip import CLIP_ARCHS, CapkCLIPVisionModel
 from .. import ops
-from .common import CapkModule, G, W
+from .common import CapkModule, G, W, compute_dtype
 from .resnet import RESNET_ARCHS, CapkResNetModel, _ResNetHeadFn
 from .swin import SWIN_ARCHS, CapkSwinModel, SwinHeadFn
 from .vit import VIT_ARCHS, CapkViTModel
@@ -40,7 +40,7 @@ class _TokenProjFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, seq, pooled, anchor, enc, B, N):
         ctx.set_materialize_grads(False)
-        dt = enc.cdtype
+        dt = compute_dtype(enc)
         proj = enc.proj
         wt = W(proj.weight, dt)
         out = ops.linear(seq, wt, proj.bias.detach())
@@ -55,7 +55,7 @@ class _TokenProjFn(torch.autograd.Function):
         enc, B, N = ctx.enc, ctx.B, ctx.N
         seq, pooled = ctx.saved
         ctx.saved = None
-        dt = enc.cdtype
+        dt = compute_dtype(enc)
         proj = enc.proj
         wt = W(proj.weight, dt)
         gw, gb = G(proj.weight), G(proj.bias)

@@ -160,26 +160,64 @@ def sample_captions(decoder, encoder_features, max_length, seed, check_every=EOS
     return ids[:, :T], logp[:steps].t()
 
 
-def scst_step(model, images, references, optimizer, lr, seed, max_length=20, baseline_kwargs=None, bucketer=None):
+class _Phases:
+    """Per-phase GPU time of an SCST update (HIP events on the compute stream) plus the host
+    time of the CIDEr-D scoring; ``times`` (dict) accumulates milliseconds per phase."""
+
+    def __init__(self, times):
+        self.times = times
+        self.marks = []
+
+    def mark(self, name):
+        if self.times is None:
+            return
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        self.marks.append((name, ev))
+
+    def close(self, host_ms):
+        if self.times is None:
+            return
+        self.marks[-1][1].synchronize()
+        for (_, e0), (name, e1) in zip(self.marks, self.marks[1:]):
+            self.times[name] = self.times.get(name, 0.0) + e0.elapsed_time(e1)
+        self.times["cider_host"] = self.times.get("cider_host", 0.0) + host_ms
+
+
+def scst_step(model, images, references, optimizer, lr, seed, max_length=20, baseline_kwargs=None, bucketer=None,
+              phase_times=None):
     """One SCST update (trainer.py:338-381): encoder forward, sampled captions, baseline
     captions (model.generate), per-sample CIDEr-D rewards, loss = masked mean of
     -logp * (r_sample - r_baseline), backward, AdamW step.  references: per image a list
     of token-id lists.  `seed` keys the sampler's uniforms: pass a fresh value per update
     (the trainer derives it from its step counter) or every update reuses the same draws.
     `lr` = None uses the optimizer's scheduled rate.  Returns (loss, mean sample reward,
-    mean baseline reward)."""
+    mean baseline reward).
+
+    The rewards are needed only by the loss: the sampled / baseline ids are copied to pinned
+    host memory right after the searches, the teacher-forced forward is queued behind the
+    copy, and the host scores CIDEr-D while the GPU runs that forward.  ``phase_times``
+    (dict, optional) accumulates the GPU milliseconds of each phase (encoder, sample,
+    baseline, forward, loss_backward, optimizer) and the host scoring time."""
+    import time
     dec = model.decoder
+    ph = _Phases(phase_times)
+    ph.mark("start")
     enc = model.encoder(images)
+    ph.mark("encoder")
     enc_nograd = {k: (v.detach() if torch.is_tensor(v) else v) for k, v in enc.items()}
     ids, _ = sample_captions(dec, enc_nograd, max_length, seed)
+    ph.mark("sample")
     with torch.no_grad():
         base_ids, _ = dec.generate(enc_nograd, max_length, **(baseline_kwargs or {}))
+    ph.mark("baseline")
     eos, pad, bos = dec.eos_token_id, dec.pad_token_id, dec.bos_token_id
-    samp = [strip_special(r, eos, pad, bos) for r in ids.cpu().tolist()]
-    base = [strip_special(r, eos, pad, bos) for r in base_ids.cpu().tolist()]
-    refs = [[list(x) for x in rs] for rs in references]
-    r_s, r_b = cider_d(samp, refs), cider_d(base, refs)
-    adv = torch.tensor(r_s - r_b, dtype=torch.float32, device=ids.device)
+    ids_h = torch.empty(ids.shape, dtype=ids.dtype, pin_memory=True)
+    base_h = torch.empty(base_ids.shape, dtype=base_ids.dtype, pin_memory=True)
+    ids_h.copy_(ids, non_blocking=True)
+    base_h.copy_(base_ids, non_blocking=True)
+    copied = torch.cuda.Event()
+    copied.record()
     from ..models.decoders import GPT2Decoder, LSTMDecoder
     if isinstance(dec, GPT2Decoder):
         logits = dec.forward_logits(enc["pooled_features"], ids, use_pad_mask=False)
@@ -187,9 +225,22 @@ def scst_step(model, images, references, optimizer, lr, seed, max_length=20, bas
         logits, _ = dec.forward_logits(enc["features"], enc["pooled_features"], ids)
     else:
         logits, _ = dec.forward_logits(enc["features"], ids, use_pad_mask=False)
+    ph.mark("forward")
+    copied.synchronize()  # the ids only; the forward keeps running
+    t0 = time.perf_counter()
+    samp = [strip_special(r, eos, pad, bos) for r in ids_h.tolist()]
+    base = [strip_special(r, eos, pad, bos) for r in base_h.tolist()]
+    refs = [[list(x) for x in rs] for rs in references]
+    r_s, r_b = cider_d(samp, refs), cider_d(base, refs)
+    adv_h = torch.from_numpy((r_s - r_b).astype(np.float32)).pin_memory()
+    host_ms = (time.perf_counter() - t0) * 1e3
+    adv = adv_h.to(ids.device, non_blocking=True)
     loss = policy_gradient_loss(logits, ids, adv, eos)
     loss.backward()
     if bucketer is not None:  # DP: rewards are rank-local, gradients are averaged
         bucketer.finish()
+    ph.mark("loss_backward")
     optimizer.step(lr=lr)
+    ph.mark("optimizer")
+    ph.close(host_ms)
     return loss.detach(), float(np.mean(r_s)), float(np.mean(r_b))

@@ -324,12 +324,18 @@ static int choose_cfg(int M, int N, int K, int a_kmajor, int b_kmajor, int act) 
   // the 256x256 phased kernel (gemm8p.hip) whenever its grid (x split-K for the weight
   // gradients) fills most of the chip: measured faster than the 128-row tiles on every
   // config-3 shape of that size (tools/gemm_bench.py, profiles/round2/)
+  // (the persistent gemm8q variant, cfg 6, measured slower in the full config-3 step:
+  // 50 vs 40 ms of GEMM per step, profiles/round3 -- CAPK_GEMM_8Q=1 selects it for A/B)
+  static const int big = [] {
+    const char* v = getenv("CAPK_GEMM_8Q");
+    return v && v[0] == '1' ? 6 : 5;
+  }();
   if (M >= 256 && N >= 256) {
     const int t5 = tiles_of(5, M, N);
     if (!a_kmajor && !b_kmajor) {
-      if (t5 * choose_splits(5, M, N, K) >= 128) return 6;
+      if (t5 * choose_splits(5, M, N, K) >= 128) return big;
     } else if (t5 >= 160) {
-      return 6;
+      return big;
     }
   }
   // (decode-step rows, M < 2048: the 2-WG/CU BK-64 ring measured faster with an activation too)

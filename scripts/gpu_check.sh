@@ -18,6 +18,9 @@ for step in "$@"; do
   case $step in
     sweep) CFG=6 run sweep 200 python tools/gemm_sweep_check.py ;;
     gemmtests) run gemmtests 400 python -u -m pytest tests/test_gpu_gemm.py tests/test_gpu_kernels.py -q -rf --timeout 120 --timeout-method thread ;;
+    gemm5) GEMM_GRAPH=1 GEMM_ONLY=${SHAPES:-vit_qkv_fwd,vit_o_fwd,vit_fc1_fwd_plain,vit_fc1_fwd_gelu_deriv,vit_fc2_fwd,vit_qkv_dx,vit_fc1_dx,vit_fc2_dx_gelu_deriv,vit_o_dw,vit_fc1_dw,vit_qkv_dw,lm_head_fwd,lm_head_dw,bf16_4k,bf16_8k} run gemm5 300 python tools/gemm_bench.py ;;
+    gemm6) CAPK_GEMM_8Q=1 GEMM_GRAPH=1 GEMM_ONLY=${SHAPES:-vit_qkv_fwd,vit_o_fwd,vit_fc1_fwd_plain,vit_fc1_fwd_gelu_deriv,vit_fc2_fwd,vit_qkv_dx,vit_fc1_dx,vit_fc2_dx_gelu_deriv,vit_o_dw,vit_fc1_dw,vit_qkv_dw,lm_head_fwd,lm_head_dw,bf16_4k,bf16_8k} run gemm6 300 python tools/gemm_bench.py ;;
+    plugins) run plugins 400 python -u -m pytest tests/test_gpu_plugins.py tests/test_gpu_checkpoint.py -q -rf --timeout 240 --timeout-method thread ;;
     tests) run tests 600 python -u -m pytest tests -m gpu -q -rf --timeout 240 --timeout-method thread ;;
     smoke) run smoke 240 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench3) run bench_config3 480 python bench.py --steps 10 --warmup 3 ;;

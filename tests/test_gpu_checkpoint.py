@@ -74,7 +74,7 @@ def test_trainer_save_load_resumes_bit_identically(tmp_path):
     assert t1.scheduler.get_last_lr() == t2.scheduler.get_last_lr()
     ck = torch.load(path, weights_only=True)
     assert set(ck) == {"epoch", "model_state_dict", "optimizer_state_dict", "scheduler_state_dict", "config",
-                       "best_val_score"}
+                       "best_val_score", "rl_updates"}
 
 
 @cuda

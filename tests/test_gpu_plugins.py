@@ -292,6 +292,8 @@ def test_lstm_scst_sampling_and_update_vs_oracle():
         if pr[n].grad is None:
             continue
         gref = pr[n].grad
+        if n == "embedding.weight":  # nn.Embedding(padding_idx=pad): the pad row gets no gradient
+            gref[pad] = 0
         torch.testing.assert_close(prm._capk_grad.cpu(), gref, rtol=2e-3, atol=2e-3 * float(gref.abs().max()) + 1e-8,
                                    msg=lambda m: f"{n}: {m}")
         checked += 1
@@ -302,13 +304,14 @@ def test_lstm_scst_sampling_and_update_vs_oracle():
 @cuda
 def test_cli_main_train_steps_and_checkpoint(tmp_path):
     """capk.main (src/main.py:17-102) --mode train on the config-3 model (ViT-B/16 +
-    Transformer decoder, bf16) for 2 synthetic steps at batch 8, then save / load a
-    checkpoint through the trainer (trainer.py:569-620 layout)."""
+    Transformer decoder, bf16) for 2 synthetic batches at batch 8 -- 2 CE steps, then (the
+    reference default use_rl=True) 2 SCST updates over the same batches -- then save / load
+    a checkpoint through the trainer (trainer.py:569-620 layout)."""
     from capk.main import main
     cfg, model, trainer = main(["--mode", "train", "--encoder_type", "vit", "--decoder_type", "transformer",
                                 "--attention_type", "multi_head", "--batch_size", "8", "--steps", "2",
                                 "--output_dir", str(tmp_path), "--seed", "3"])
-    assert trainer is not None and trainer.global_step == 2
+    assert trainer is not None and trainer.global_step == 4 and trainer.rl_updates == 2
     path = trainer.save_checkpoint(0, path=os.path.join(str(tmp_path), "ck.pth"))
     before = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
     trainer.train_step(*_batch(cfg))  # move the weights, then restore them from the file
@@ -316,7 +319,7 @@ def test_cli_main_train_steps_and_checkpoint(tmp_path):
     after = model.state_dict()
     for k, v in before.items():
         assert torch.equal(after[k].cpu(), v), k
-    assert trainer.global_step == 2
+    assert trainer.global_step == 4 and trainer.rl_updates == 2
 
 
 def _batch(cfg):

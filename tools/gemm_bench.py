@@ -28,6 +28,7 @@ SHAPES = [  # name, M, N, K, kind
     ("f8_clip_fc2", 12800, 768, 3072, "f8"), ("f8_gpt2_fc1", 5120, 3072, 768, "f8"),
     ("f8_lm_head", 5120, 50304, 768, "f8"), ("f8_lm_head_beam5", 1280, 50304, 768, "f8"),
     ("f8_big", 16384, 16384, 8192, "f8"), ("bf16_big", 16384, 16384, 8192, "fwd"),
+    ("bf16_4k", 4096, 4096, 4096, "fwd"), ("bf16_8k", 8192, 8192, 8192, "fwd"),
     ("f8_quant_x", 12800, 3072, 768, "quant"),
     # decode steps (GPT-2 Conv1D weights N-major: "c1d"): rows = beams in flight
     ("dec256_cattn", 256, 2304, 768, "c1d"), ("dec256_cproj", 256, 768, 768, "c1d"),
