@@ -71,12 +71,16 @@ def test_token_encoder_projection_fp32(family):
     assert _rel(out["features"], ref["features"]) < 1e-4
     assert _rel(out["pooled_features"], ref["pooled_features"]) < 1e-4
     checked = 0
+    gmax = max(float(p[n].grad.abs().max()) for n, _ in enc.named_parameters() if p[n].grad is not None)
     for n, prm in enc.named_parameters():
         gref = p[n].grad
         if gref is None:
             continue
-        torch.testing.assert_close(prm._capk_grad.cpu(), gref, rtol=1e-3, atol=1e-3 * float(gref.abs().max()) + 1e-7,
-                                   msg=lambda m: f"{n}: {m}")
+        # fp32 kernels vs fp32 autograd: 1e-3 relative per parameter, or within 1e-5 of the
+        # largest gradient of the model (parameters whose gradient is ~0, e.g. an LN bias
+        # before a mean-free path)
+        err = float((prm._capk_grad.cpu() - gref).norm())
+        assert err <= 1e-3 * float(gref.norm()) or float((prm._capk_grad.cpu() - gref).abs().max()) <= 1e-5 * gmax, n
         checked += 1
     assert checked >= 2 + 8 * Le
 
