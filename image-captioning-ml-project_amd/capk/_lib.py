@@ -69,6 +69,9 @@ SIGNATURES = {
     "capk_colsum_workspace": (_sz, [_i, _i]),
     "capk_colsum": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i, _c_p, _sz, _c_p]),
     "capk_act_bwd_colsum": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _i, _c_p, _i, _c_p, _sz, _c_p]),
+    "capk_gemm_dx_act_colsum_workspace": (_sz, [_i, _i, _i]),
+    "capk_gemm_dx_act_colsum": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p, _i64, _i, _c_p, _i64, _c_p, _i, _c_p,
+                                     _sz, _c_p]),
     "capk_cast": (_i, [_i, _i, _i64, _c_p, _c_p, _c_p]),
     "capk_copy_rows": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p]),
     "capk_act_bwd": (_i, [_i, _i64, _i, _c_p, _c_p, _c_p, _c_p]),

@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from .._lib import ACT_GELU_ERF, ACT_TANH
+from .._lib import ACT_DERIV, ACT_GELU_ERF, ACT_TANH
 from ..params import Fused, notify_final, store_of
 from .common import G, CapkModule, W, heads, linear_bwd, mark
 
@@ -224,9 +224,10 @@ class _ViTLayerFn(torch.autograd.Function):
         h2, mu2, rs2 = ops.layernorm_fwd(x1, ln2.weight.detach(), ln2.bias.detach(), L.eps)
         I = fc1.weight.shape[0]
         f_pre = torch.empty(x.shape[0], I, dtype=x.dtype, device=x.device)
-        # f_pre keeps the pre-activation: on the library route the FC1 product is written
-        # straight into it and one pass writes GELU(pre) (CAPK_ACT_DERIV would add a stream)
-        f = ops.linear(h2, W(fc1.weight, dt), fc1.bias.detach(), act=act, preact=f_pre)
+        # f_pre keeps act'(pre) (CAPK_ACT_DERIV): the FC1 epilogue writes GELU(pre) and its
+        # derivative together, and the backward's dX epilogue multiplies by it and takes
+        # FC1's bias gradient from the same registers (capk_gemm_dx_act_colsum)
+        f = ops.linear(h2, W(fc1.weight, dt), fc1.bias.detach(), act=act | ACT_DERIV, preact=f_pre)
         y = ops.linear(f, W(fc2.weight, dt), fc2.bias.detach(), residual=x1)
         ctx.L, ctx.B, ctx.N = L, B, N
         ctx.saved = (x, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, f_pre, f)
@@ -249,7 +250,7 @@ class _ViTLayerFn(torch.autograd.Function):
         fused_b2 = getattr(L, "_capk_fc2_bias_done", False)
         L._capk_fc2_bias_done = False
         # FC1's bias gradient = colsum(dfp), fused into the GELU' pass that produces dfp
-        dfp = linear_bwd(dy, f, fc2.weight, None if fused_b2 else fc2.bias, dt, act_bwd=act, aux=f_pre,
+        dfp = linear_bwd(dy, f, fc2.weight, None if fused_b2 else fc2.bias, dt, act_bwd=act | ACT_DERIV, aux=f_pre,
                          dsum=G(fc1.bias))
         dh2 = linear_bwd(dfp, h2, fc1.weight, None, dt)
         # dx1 = the O projection's output gradient: its column sums (O bias grad) come out of the LN kernel

@@ -254,6 +254,16 @@ def linear_dx(dy, w, *, out=None, act_bwd=0, aux=None, beta=0.0, drop=NO_DROP, d
     if out is None:
         out = torch.empty(M, K, dtype=dy.dtype, device=dy.device)
     if dsum is not None and act_bwd and beta == 0.0 and drop[0] <= 0:
+        if dy.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and out.dtype == torch.bfloat16:
+            # one call: the product x act'(aux) with the column sums (capk_gemm_dx_act_colsum)
+            _need_gpu(dy, w, out, aux, dsum)
+            L = lib()
+            wsb = L.capk_gemm_dx_act_colsum_workspace(M, K, N)
+            ws = _ws(wsb, dy.device)
+            check(L.capk_gemm_dx_act_colsum(M, K, N, _p(dy), dy.stride(0), _p(w), w.stride(0), _p(out), out.stride(0),
+                                            int(act_bwd), _p(aux), aux.stride(0), _p(dsum), 0, _p(ws), wsb, _stream()),
+                  "capk_gemm_dx_act_colsum")
+            return out
         gemm(dy, True, w, False, M, K, N, out, lda=dy.stride(0), ldb=w.stride(0), ldc=out.stride(0))
         return act_bwd_colsum(out, aux, act_bwd, dsum)
     gemm(dy, True, w, False, M, K, N, out, lda=dy.stride(0), ldb=w.stride(0), ldc=out.stride(0), beta=beta,

@@ -352,7 +352,9 @@ static int choose_splits(int cfg, int M, int N, int K) {
   }();
   // very long reductions (conv weight gradients: K = B*H*W up to 4e5) with a tiny M x N
   // grid fill the chip only with more than 16 splits (each split still >= 4 K-tiles)
-  const int max_split = max_split_env ? max_split_env : (K >= 65536 ? 64 : 16);
+  // (K >= 16384: the ViT O-projection weight gradient, 768 x 768 = 9 tiles, fills 252 CUs
+  // with 28 splits instead of 144 with 16)
+  const int max_split = max_split_env ? max_split_env : (K >= 65536 ? 64 : K >= 16384 ? 32 : 16);
   const int bk = (cfg == 3 || cfg == 4) ? 32 : 64;
   const int tiles = tiles_of(cfg, M, N), slots = slots_of(cfg);
   const int nk = cdiv(K, bk);
@@ -434,6 +436,7 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
     const int nk64 = cdiv(K, 64), per = cdiv(nk64, splits);
     const bool padded = nk64 % per != 0;
     if (!gemm8q_supports(e, out_dtype == CAPK_F32) || per < 2 || (padded && (a_kmajor || b_kmajor)) ||
+        tiles_of(6, M, N) * splits <= 256 ||  // one round: the non-persistent kernel
         ((act & 15) && !(act & CAPK_ACT_BWD) && splits == 1 && !(a_kmajor && b_kmajor)))
       cfg = 5;
   }
@@ -515,6 +518,42 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
     CAPK_LAUNCH_CHECK("splitk_reduce_kernel");
   }
   return CAPK_OK;
+}
+
+// dX = dY W times act'(pre) with the column sums of the result (the pre-LN FFN backward:
+// dPre of fc1 and fc1's bias gradient, modeling_vit.py:249-254).  Persistent grids take the
+// fused kernel (gemm8q DSUM: column-sum partials from the register epilogue + one finish
+// launch); others the plain product + capk_act_bwd_colsum.
+extern "C" size_t capk_gemm_dx_act_colsum_workspace(int M, int N, int K) {
+  const size_t g = capk_gemm_workspace(CAPK_BF16, CAPK_BF16, M, N, K);
+  const size_t c = capk_colsum_workspace(M, N);
+  const size_t d = (size_t)cdiv(M, 256) * 2 * N * sizeof(float);
+  return std::max(g, std::max(c, d));
+}
+
+extern "C" int capk_gemm_dx_act_colsum(int M, int N, int K, const void* dY, int64_t ldy, const void* W, int64_t ldw,
+                                       void* C, int64_t ldc, int act, const void* aux, int64_t ldx, float* db,
+                                       int accumulate, void* ws, size_t ws_bytes, void* stream) {
+  CAPK_CHECK_ARG(M > 0 && N > 0 && K > 0 && dY && W && C && aux && db && (act & 15),
+                 "capk_gemm_dx_act_colsum: bad arguments");
+  CAPK_CHECK_ARG(ws && ws_bytes >= capk_gemm_dx_act_colsum_workspace(M, N, K),
+                 "capk_gemm_dx_act_colsum: workspace too small");
+  const int act_bwd = CAPK_ACT_BWD | act;
+  Epi e{C, ldc, 1.f, 0.f, nullptr, nullptr, 0, act_bwd, nullptr, aux, ldx, M, N, make_drop(0.f, 0)};
+  const int cfg = choose_cfg(M, N, K, 1, 0, act_bwd);
+  const int splits = choose_splits(cfg, M, N, K);
+  const bool fused = (cfg == 5 || cfg == 6) && splits == 1 && (act & CAPK_ACT_DERIV) && K % 32 == 0 &&
+                     tiles_of(6, M, N) > 256 && gemm8q_supports(e, false) && K >= 128;
+  if (fused) {
+    g_last_cfg = 6;
+    const int rc = launch_gemm8q(true, false, false, dY, ldy, W, ldw, M, N, K, 1, e, nullptr, S(stream), (float*)ws);
+    if (rc != CAPK_OK) return rc;
+    return launch_colsum_finish(cdiv(M, 256) * 2, N, (const float*)ws, db, accumulate, S(stream));
+  }
+  int rc = capk_gemm(CAPK_BF16, CAPK_BF16, M, N, K, dY, ldy, 1, W, ldw, 0, C, ldc, 1.f, 0.f, nullptr, nullptr, 0, 0,
+                     nullptr, nullptr, 0, 0.f, 0, ws, ws_bytes, stream);
+  if (rc != CAPK_OK) return rc;
+  return capk_act_bwd_colsum(CAPK_BF16, M, N, C, ldc, aux, ldx, act, db, accumulate, ws, ws_bytes, stream);
 }
 
 // fp8 GEMM (config 5): C = epilogue((diag(2^sa) A8) (diag(2^sb) B8)^T), A8 [M][K], B8 [N][K]

@@ -1,31 +1,36 @@
-// Persistent 256x256 bf16 GEMM with a register-direct epilogue (round 3) — the large-grid
-// kernel of capk_gemm.  Same tile, waves, LDS images and phased main loop as gemm8p.hip;
-// what changes is everything around the main loop:
+// Persistent 256x256 bf16 GEMM (round 3) -- the large-grid kernel of capk_gemm for grids
+// of more than one round.  The main loop is gemm8p.hip's: 256x256x64 tiles, 8 waves (2 x 4),
+// four 16-KiB half-tiles per K-tile staged by LDS-DMA through two 64-KiB stages, two phases
+// of 32 v_mfma_f32_16x16x32_bf16 per K-tile, waves 4-7 one barrier behind waves 0-3, static
+// vmcnt counts.  What changes is everything around it:
 //
-//  * Persistent grid: min(tiles x splits, 256) workgroups, one per CU; WG b takes items
-//    j*256 + (b & 7)*32 + (b >> 3) (j = 0, 1, ...) -- every XCD works on 32 consecutive items
-//    of the row-major tile order at a time, so an XCD's L2 holds the A rows and B columns
-//    they share.
-//  * One continuous K-tile pipeline over ALL of the WG's items: the loads of item j+1's first
-//    two K-tiles are issued during item j's last two K-tiles (exactly where the steady-state
-//    schedule issues them), so no item pays a prologue; only the WG's first item does.
-//  * Register-direct epilogue: no LDS staging.  The MFMAs run with the operands swapped
-//    (B fragment first), so a lane's accumulator holds 4 consecutive columns of one row;
-//    one v_permlane16_swap per register pair turns the two 16-column blocks of a 32-column
-//    strip into 8 consecutive columns per lane, stored as one 16-byte buffer store (each
-//    store instruction writes 16 rows x 64 contiguous bytes).  Bias comes from a 1-KiB LDS
-//    slot filled by LDS-DMA when the item's first K-tile is loaded; the side operand
-//    (residual / aux / C) by 16 buffer loads.  Out-of-range rows and columns go through the
-//    buffer descriptors' range checks (no branches: every wave issues the same number of
-//    memory instructions, which the vmcnt ledger below relies on).
-//  * The epilogue's stores are NOT waited for: they drain while the next item's first K-tile
-//    computes (its operands were loaded before the stores were issued).  vmcnt counts loads,
-//    LDS-DMA and stores together in issue order, so every wait is computed at run time from a
-//    per-wave ledger of issued memory instructions (`ops` and the issue marks of each group)
-//    instead of the fixed counts of gemm8p.
+//  * Persistent grid of 256 workgroups (one per CU).  WG b takes items first + 256 j with
+//    first = (b & 7) * 32 + (b >> 3): the 32 WGs of an XCD work on 32 consecutive items of
+//    the row-major tile order at a time, so that XCD's L2 holds the A rows and B columns
+//    they share.  Every item has the same number of K-tiles nk (>= 2).
+//  * ONE continuous K-tile sequence over all of the WG's items (step u = item j's K-tile
+//    u - j nk): the LDS-DMA schedule of gemm8p (phase Q1 of step u issues half A1 of step
+//    u+1, Q2 issues A0/B0/B1 of step u+2) runs across item boundaries, so the next item's
+//    first two K-tiles are loaded under the current item's last two and only the WG's
+//    first item pays a prologue.
+//  * Register-direct epilogue (no LDS staging: the stages hold the next item's K-tiles).
+//    The MFMAs take the B fragment first, so a lane's accumulator holds 4 consecutive
+//    columns of one row; one v_permlane16_swap per register pair turns the two 16-column
+//    blocks of a 32-column strip into 8 consecutive columns per lane, written by one 16-B
+//    buffer store (16 rows x 64 contiguous bytes per store instruction).  The item's bias
+//    (the wave's 64 columns) is LDS-DMA-ed with the item's first K-tile into a per-wave
+//    slot; a side operand (residual / aux / C) is loaded per half by 8 buffer loads.
+//    Rows and columns past M / N go through the buffer descriptors' range checks, so every
+//    wave issues the same memory instructions.
+//  * The epilogue's stores are left in flight: they drain while the next item's first
+//    K-tile computes.  vmcnt counts loads, LDS-DMA and stores together in issue order, so
+//    the two waits after an epilogue add its store count S (a compile-time function of the
+//    instantiation and the run-time output kind); every other wait is gemm8p's count (+1
+//    where the phase issued a bias DMA).  Too small a count is safe (it only waits longer),
+//    so the run-time counts are rounded down to the encodings wait_le() has.
 //
 // Epilogue: alpha, bias, forward activation (+ pre-activation or act' side output), backward
-// activation (x act'(aux) or x aux), dropout, residual, beta*C -- with at most ONE of
+// activation (x aux = act'(pre)), dropout, residual, beta*C -- with at most ONE of
 // aux / residual / C (gemm8q_supports); split-K items write fp32 slabs that
 // splitk_reduce_kernel finishes.
 #include <type_traits>
@@ -37,37 +42,6 @@ namespace capk {
 namespace {
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
-
-// s_waitcnt vmcnt(n) for a run-time, wave-uniform n (clamped to the field's 63)
-__device__ __forceinline__ void vm_wait_switch(int n);
-__device__ __forceinline__ void vm_wait(int n) {
-#if defined(CAPK_DIAG_VM0)  // diagnostic build: drain every wait
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  return;
-#endif
-  // the steady-state counts inline; the rest (the two phases after an epilogue, the tail)
-  // through the full switch
-  if (n == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if (n == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else vm_wait_switch(n);
-}
-__device__ __forceinline__ void vm_wait_switch(int n) {
-  n = n > 63 ? 63 : n;
-  switch (n) {
-#define CAPK_VMW(N) \
-  case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-    CAPK_VMW(0) CAPK_VMW(1) CAPK_VMW(2) CAPK_VMW(3) CAPK_VMW(4) CAPK_VMW(5) CAPK_VMW(6) CAPK_VMW(7)
-    CAPK_VMW(8) CAPK_VMW(9) CAPK_VMW(10) CAPK_VMW(11) CAPK_VMW(12) CAPK_VMW(13) CAPK_VMW(14) CAPK_VMW(15)
-    CAPK_VMW(16) CAPK_VMW(17) CAPK_VMW(18) CAPK_VMW(19) CAPK_VMW(20) CAPK_VMW(21) CAPK_VMW(22) CAPK_VMW(23)
-    CAPK_VMW(24) CAPK_VMW(25) CAPK_VMW(26) CAPK_VMW(27) CAPK_VMW(28) CAPK_VMW(29) CAPK_VMW(30) CAPK_VMW(31)
-    CAPK_VMW(32) CAPK_VMW(33) CAPK_VMW(34) CAPK_VMW(35) CAPK_VMW(36) CAPK_VMW(37) CAPK_VMW(38) CAPK_VMW(39)
-    CAPK_VMW(40) CAPK_VMW(41) CAPK_VMW(42) CAPK_VMW(43) CAPK_VMW(44) CAPK_VMW(45) CAPK_VMW(46) CAPK_VMW(47)
-    CAPK_VMW(48) CAPK_VMW(49) CAPK_VMW(50) CAPK_VMW(51) CAPK_VMW(52) CAPK_VMW(53) CAPK_VMW(54) CAPK_VMW(55)
-    CAPK_VMW(56) CAPK_VMW(57) CAPK_VMW(58) CAPK_VMW(59) CAPK_VMW(60) CAPK_VMW(61) CAPK_VMW(62)
-    default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
-#undef CAPK_VMW
-  }
-}
 
 // One segment of the side operand (8 elements of one row) loaded by an asm buffer load that
 // hipcc does not count; the epilogue waits for all of them with one vmcnt(0) statement that
@@ -131,50 +105,61 @@ struct Epi8q {
   int side_kind, act;  // act: CAPK_ACT_* kind | CAPK_ACT_BWD | CAPK_ACT_DERIV
   Drop drop;
   int dropN;  // Epi::N (the dropout mask index is m * dropN + n)
+  float* dsum;  // DSUM kernels: column-sum partials [2 * tile rows][N]
 };
 
+// s_waitcnt vmcnt(<= n) for a wave-uniform run-time n: the largest encoded count <= n
+__device__ __forceinline__ void wait_le(int n) {
+#define CAPK_W(N) \
+  if (n >= N) { asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); return; }
+  CAPK_W(40) CAPK_W(39) CAPK_W(38) CAPK_W(34) CAPK_W(33) CAPK_W(32) CAPK_W(24) CAPK_W(23) CAPK_W(22)
+  CAPK_W(18) CAPK_W(17) CAPK_W(16) CAPK_W(15) CAPK_W(14) CAPK_W(10) CAPK_W(9) CAPK_W(8) CAPK_W(7) CAPK_W(6)
+  CAPK_W(4) CAPK_W(3) CAPK_W(2) CAPK_W(1)
+#undef CAPK_W
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // ACT: the forward activation the epilogue evaluates (CAPK_ACT_* kind, 0 = none), a template
-// parameter so each of the 16 unrolled epilogue segments carries only its own code
-// SIDE: the epilogue reads a side operand (residual / aux / C); a template parameter so the
-// kernels without one do not reserve its 64 registers
-template <bool AK, bool BK, typename OutT, int ACT, bool SIDE>
+// parameter so each of the 16 unrolled epilogue segments carries only its own code.
+// SIDE: the epilogue reads a side operand (residual / aux / C).
+// DSUM: also the column sums of the final values (the bias gradient of the Linear whose
+// output gradient this dX is): per (tile row, wm) partial rows [2 ntm][N] into e.dsum,
+// summed in a fixed order by colsum_finish (capk_gemm_dx_act_colsum).
+template <bool AK, bool BK, typename OutT, int ACT, bool SIDE, bool DSUM = false>
 __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A, int64_t lda,
                                                      const void* __restrict__ B, int64_t ldb, int M, int N, int K,
                                                      int splits, Epi8q e, float* __restrict__ ws) {
   constexpr int HALF = 128 * 64 * 2, STAGE = 4 * HALF, BIAS0 = 2 * STAGE;
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 4 * 1024];  // stages + 4 bias slots
+  // two stages + bias slots [item parity][wave] of 64 fp32 (the wave's columns)
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 2 * 8 * 256];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   const bool lag = wave >= 4;  // waves 4-7 run one barrier behind
-  const int ntm = (M + 255) / 256, ntn = (N + 255) / 256, ntiles = ntm * ntn, items = ntiles * splits;
-  const int nk_all = (K + 63) / 64, kt_per = (nk_all + splits - 1) / splits;
-  const int G = gridDim.x, bid = blockIdx.x;
+  const int ntn = (N + 255) / 256, ntiles = ((M + 255) / 256) * ntn, items = ntiles * splits;
+  const int nk = ((K + 63) / 64 + splits - 1) / splits;  // K-tiles per item (>= 2: host)
+  const int first = (blockIdx.x & 7) * 32 + (blockIdx.x >> 3);  // grid = 256
+  const int nmine = first < items ? (items - first + 255) >> 8 : 0;
+  if (nmine == 0) return;
+  const int total = nmine * nk;  // K-tile steps of this WG
 
   const __amdgpu_buffer_rsrc_t rsA = rsrc_of(A, (AK ? (int64_t)M * lda : (int64_t)K * lda) * 2);
   const __amdgpu_buffer_rsrc_t rsB = rsrc_of(B, (BK ? (int64_t)N * ldb : (int64_t)K * ldb) * 2);
   const uint32_t kstepA = AK ? 128u : (uint32_t)(64 * lda * 2);
   const uint32_t kstepB = BK ? 128u : (uint32_t)(64 * ldb * 2);
+  const uint32_t rowA = AK ? (uint32_t)(lda * 2) : 2u, rowB = BK ? (uint32_t)(ldb * 2) : 2u;
 
-  // ---- work items: (split, tile), each kt_per K-tiles (the last split's K-tiles past K read
-  // zeros: split-K runs on MN-major operands only, whose K rows end at the descriptor range)
-  const int nk = kt_per;  // >= 2 (the host routes shorter reductions to gemm8p)
   struct Item {
-    int m0, n0, split;  // split < 0: no such item
+    int m0, n0, kb;  // tile origin, first K-tile of the item's split
   };
   auto item_at = [&](int j) -> Item {
-    int it;
-    if (items <= G) it = j == 0 ? xcd_remap(bid, G) : -1;
-    else {
-      it = j * G + (bid & 7) * (G >> 3) + (bid >> 3);
-      it = it < items ? it : -1;
-    }
-    if (it < 0) return Item{0, 0, -1};
-    const int split = it / ntiles, tile = it - split * ntiles;
-    return Item{(tile / ntn) * 256, (tile % ntn) * 256, split};
+    const int it = first + (j << 8);
+    const int sp = it / ntiles, tile = it - sp * ntiles, tm = tile / ntn;
+    return Item{tm * 256, (tile - tm * ntn) * 256, sp * nk};
   };
 
   // per-lane byte offsets of this wave's two 1-KiB pieces of each half (h: A0 A1 B0 B1) at
-  // row0 = 0, k0 = 0; an item's rows / columns and the K-tile enter as the scalar offset
+  // row / column 0, k 0 (no clamp: rows / columns past M / N only feed outputs that are
+  // never stored, and the descriptor range check zeroes reads past the operand)
   uint32_t vo[4][2];
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
@@ -183,46 +168,42 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     vo[2][p] = piece_voff<BK, 2>(wave * 2 + p, lane, 0, 1 << 30, ldb);
     vo[3][p] = piece_voff<BK, 2>(wave * 2 + p, lane, 128, 1 << 30, ldb);
   }
-  const uint32_t rowA = AK ? (uint32_t)(lda * 2) : 2u, rowB = BK ? (uint32_t)(ldb * 2) : 2u;  // bytes per row / col
-  // K-tile (item it, local k) -> stage slot of global step t; h = 0..3
-  auto dma = [&](auto hc, const Item& it, int k, int t) {
-    constexpr int h = decltype(hc)::value;
-    char* dst = smem + (t & 1) * STAGE + h * HALF;
-    // the whole offset goes in the VGPR operand: the descriptor's range check (rows past M /
-    // N, K rows past K read as zero) must see it
-    const uint32_t so = (h < 2 ? (uint32_t)it.m0 * rowA : (uint32_t)it.n0 * rowB) +
-                        (uint32_t)(it.split * kt_per + k) * (h < 2 ? kstepA : kstepB);
+  auto load = [&](int h, const Item& it, int k, int u) {
+    char* dst = smem + (u & 1) * STAGE + h * HALF;
+#if defined(CAPK_DIAG_ROW0)  // diagnostic build: every item reads the A rows of tile row 0 (L2-resident)
+    const uint32_t so = h < 2 ? (uint32_t)(it.kb + k) * kstepA : (uint32_t)it.n0 * rowB + (uint32_t)(it.kb + k) * kstepB;
+#else
+    const uint32_t so = h < 2 ? (uint32_t)it.m0 * rowA + (uint32_t)(it.kb + k) * kstepA
+                              : (uint32_t)it.n0 * rowB + (uint32_t)(it.kb + k) * kstepB;
+#endif
 #pragma unroll
     for (int p = 0; p < 2; ++p)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(h < 2 ? rsA : rsB,
                                                (__attribute__((address_space(3))) void*)(dst + (wave * 2 + p) * 1024),
                                                16, vo[h][p] + so, 0, 0, 0);
   };
-  using H0 = std::integral_constant<int, 0>;
-  using H1 = std::integral_constant<int, 1>;
-  using H2 = std::integral_constant<int, 2>;
-  using H3 = std::integral_constant<int, 3>;
-  // bias of an item: 256 fp32 columns = one 16-B-per-lane LDS-DMA by wave 0 into slot j & 3
+  const bool has_bias = e.bias != nullptr && ws == nullptr;
+  // the wave's 64 bias columns of item j (lane l: column (l >> 5) * 128 + wn * 32 + (l & 31))
   auto bias_dma = [&](const Item& it, int j) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(
-        rsrc_of(e.bias, (int64_t)N * 4), (__attribute__((address_space(3))) void*)(smem + BIAS0 + (j & 3) * 1024), 16,
-        (uint32_t)lane * 16u + (uint32_t)it.n0 * 4u, 0, 0, 0);
+        rsrc_of(e.bias, (int64_t)N * 4),
+        (__attribute__((address_space(3))) void*)(smem + BIAS0 + ((j & 1) * 8 + wave) * 256), 4,
+        (uint32_t)(it.n0 + (lane >> 5) * 128 + wn * 32 + (lane & 31)) * 4u, 0, 0, 0);
   };
-  const bool has_bias = e.bias != nullptr && ws == nullptr;
   const int side_kind = (!SIDE || ws) ? SIDE_NONE : e.side_kind;
   const bool has_pre = ACT != 0 && !ws && e.pre != nullptr;
 
   // ---- fragments and MFMAs (B fragment first: lane = row, registers = 4 consecutive columns)
-  auto half = [&](int t, int h) -> const char* { return smem + (t & 1) * STAGE + h * HALF; };
-  auto readA = [&](bf16x8 (&f)[2][4], int t, int h) {
-    const char* base = half(t, h);
+  auto half = [&](int u, int h) -> const char* { return smem + (u & 1) * STAGE + h * HALF; };
+  auto readA = [&](bf16x8 (&f)[2][4], int u, int h) {
+    const char* base = half(u, h);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int i = 0; i < 4; ++i) f[s][i] = frag<AK>(base, wm * 64 + i * 16, s, lane);
   };
-  auto readB = [&](bf16x8 (&f)[2][2], int t, int h) {
-    const char* base = half(t, h);
+  auto readB = [&](bf16x8 (&f)[2][2], int u, int h) {
+    const char* base = half(u, h);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -240,14 +221,12 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
           for (int j = 0; j < 2; ++j) acc[a][b][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   };
   auto mma = [&](const bf16x8 (&fa)[2][4], const bf16x8 (&fb)[2][2], f32x4 (&c)[4][2]) {
-    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[s][j], fa[s][i], c[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
   };
   auto fence = [] { __builtin_amdgcn_sched_barrier(0); };
   auto bar = [&] {
@@ -268,28 +247,24 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
   // lane byte offset of (row m0 + lrow, column n0 + qn*128 + lcol) in a [rows][ld] matrix of
   // element size es; columns past N -> OOR (rows past M fail the range check by themselves)
   auto this_lane_off = [&](const Item& c, int64_t ld, int es, int qn) -> uint32_t {
-#if defined(CAPK_DIAG_L2STORE)  // diagnostic build: every item stores over tile (0, 0) (L2-resident)
-    const int n = qn * 128 + lcol;
-    return n < N ? (uint32_t)(((int64_t)lrow * ld + n) * es) : OOR;
-#else
     const int n = c.n0 + qn * 128 + lcol;
     return n < N ? (uint32_t)(((int64_t)(c.m0 + lrow) * ld + n) * es) : OOR;
-#endif
   };
   // the segment (qm, i) adds (qm*128 + i*16) rows: one v_add of a wave-uniform constant
   auto seg_add = [&](int64_t ld, int es, int qm, int i) -> uint32_t { return (uint32_t)((qm * 128 + i * 16) * ld * es); };
   // One half of an item's epilogue: the 8 segments of quadrant row QM (acc[QM]).
-  auto epi_body = [&](const Item& c, int j, const SideSeg<OutT> (&side)[2][2][4], auto qmc) -> int {
+  auto epi_body = [&](const Item& c, int j, const SideSeg<OutT> (&side)[2][2][4], float (&cs)[2][8],
+                      auto qmc) -> int {
     constexpr int QM = decltype(qmc)::value;
     auto lane_off = [&](int64_t ld, int es, int qn) -> uint32_t { return this_lane_off(c, ld, es, qn); };
-    // this item's bias (LDS slot j & 3): the lane's 8 columns of each column quadrant
+    // this item's bias (the wave's slot of item parity j & 1): the lane's 8 columns per quadrant
     f32x4 bias[2][2];
     if (has_bias) {
-      const float* slot = (const float*)(smem + BIAS0 + (j & 3) * 1024);
+      const float* slot = (const float*)(smem + BIAS0 + ((j & 1) * 8 + wave) * 256);
 #pragma unroll
       for (int qn = 0; qn < 2; ++qn) {
-        bias[qn][0] = *(const f32x4*)(slot + qn * 128 + lcol);
-        bias[qn][1] = *(const f32x4*)(slot + qn * 128 + lcol + 4);
+        bias[qn][0] = *(const f32x4*)(slot + qn * 32 + qq * 8);
+        bias[qn][1] = *(const f32x4*)(slot + qn * 32 + qq * 8 + 4);
       }
     }
     const __amdgpu_buffer_rsrc_t rsC = ws ? rsrc_of(ws, (int64_t)splits * M * N * 4) : rsrc_of(e.C, (int64_t)M * e.ldc * ESZ);
@@ -300,7 +275,7 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     const int eso = ws ? 4 : ESZ;
     uint32_t o0 = lane_off(ldo, eso, 0), o1 = lane_off(ldo, eso, 1);
     if (ws) {
-      const uint32_t sl = (uint32_t)((int64_t)c.split * M * N * 4);
+      const uint32_t sl = (uint32_t)((int64_t)(c.kb / nk) * M * N * 4);
       o0 = o0 == OOR ? OOR : o0 + sl;
       o1 = o1 == OOR ? OOR : o1 + sl;
     }
@@ -308,15 +283,15 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     const bool unit_alpha = e.alpha == 1.0f;
     // one 16-row x 32-column segment (qm, qn, i), unrolled by hand (the 16 bodies exceed the
     // unroller's budget, and a rolled loop would index the accumulators dynamically)
-    auto segment = [&](auto qmc, auto qnc, auto ic) {
-      constexpr int qm = decltype(qmc)::value, qn = decltype(qnc)::value, i = decltype(ic)::value;
+    auto segment = [&](auto qmc2, auto qnc, auto ic) {
+      constexpr int qm = decltype(qmc2)::value, qn = decltype(qnc)::value, i = decltype(ic)::value;
       // blocks j = 0, 1 (columns 0-15, 16-31 of the strip): lane has columns 4*g4 + r of each;
       // one swap of rows 1,3 of X with rows 0,2 of Y gives 8 consecutive columns
       float v[8];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         // (no __builtin_bit_cast of a vector-element expression: ROCm 7.2's clang folds
-        // bit_cast(acc[r]) to element 0 for every r -- tools/gemm_layout_probe.py found it)
+        // bit_cast(acc[r]) to element 0 for every r)
         const float x = acc[qm][qn][i][0][r], y = acc[qm][qn][i][1][r];
         const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
         const unsigned sx = sw[0], sy = sw[1];
@@ -371,7 +346,15 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] += sd.get(k);
       }
+      if constexpr (DSUM) {  // rows past M hold bias / zero-operand values: not summed
+#pragma unroll
+        for (int k = 0; k < 8; ++k) cs[qn][k] += row_ok ? v[k] : 0.f;
+      }
+#if defined(CAPK_DIAG_NOSTORE)  // diagnostic build: the stores issue but are dropped (range check)
+      store8(rsC, OOR, v, (OutT*)nullptr);
+#else
       store8(rsC, ob == OOR ? OOR : ob + seg_add(e.ldc, ESZ, qm, i), v, (OutT*)nullptr);
+#endif
       if (ACT != 0 && has_pre) {
         const uint32_t pb = qn ? p1 : p0;
         store8(rsPre, pb == OOR ? OOR : pb + seg_add(e.ldp, ESZ, qm, i), pre, (OutT*)nullptr);
@@ -415,112 +398,128 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     };
     using QA = std::integral_constant<int, 0>;
     using QB = std::integral_constant<int, 1>;
+    float cs[2][8];
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) cs[qn][k] = 0.f;
     load_side(QA{});
-    const int n0 = epi_body(c, j, side, QA{});
+    const int n0 = epi_body(c, j, side, cs, QA{});
     load_side(QB{});
-    const int n1 = epi_body(c, j, side, QB{});
-    return (SIDE && ESZ == 2 && side_kind != SIDE_NONE) ? n1 : n0 + n1;
-  };
-  auto zero_half = [&](auto qmc) {
-    constexpr int QM = decltype(qmc)::value;
+    const int n1 = epi_body(c, j, side, cs, QB{});
+    int nd = 0;
+    if constexpr (DSUM) {
+      // the lane's 8 columns summed over its 8 rows; now over the 16 lanes of its column
+      // group (lane & 15 = row), then one 8-column partial per (tile row, wm) and quadrant
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+      for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int k = 0; k < 8; ++k) {
+          float x = cs[qn][k];
+          x += __shfl_xor(x, 1, 16);
+          x += __shfl_xor(x, 2, 16);
+          x += __shfl_xor(x, 4, 16);
+          x += __shfl_xor(x, 8, 16);
+          cs[qn][k] = x;
+        }
+      const __amdgpu_buffer_rsrc_t rsD = rsrc_of(e.dsum, (int64_t)((M + 255) / 256) * 2 * N * 4);
+      const int64_t prow = (int64_t)(c.m0 / 256) * 2 + wm;
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj) acc[QM][b][i][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int qn = 0; qn < 2; ++qn) {
+        const int n = c.n0 + qn * 128 + lcol;
+        const uint32_t off = ((lane & 15) == 0 && n < N) ? (uint32_t)((prow * N + n) * 4) : OOR;
+        store8(rsD, off, cs[qn], (float*)nullptr);
+      }
+      nd = 4;  // two 16-B stores per quadrant column
+    }
+    return ((SIDE && ESZ == 2 && side_kind != SIDE_NONE) ? n1 : n0 + n1) + nd;
   };
 
-  // ---- main loop: four phases per K-tile, one C quadrant (16 MFMAs) each ----
-  //   phase  quadrant  ds_read (L)       LDS-DMA issued (L)   waits for (L, read next phase)
-  //   P1     (0,0)     A0(t) B0(t)       A1(t+1)              B1(t)
-  //   P2     (0,1)     B1(t)             A0(t+2)              A1(t)
-  //   P3     (1,1)     A1(t)             B0(t+2)              -
-  //   P4     (1,0)     - (B0 kept)       B1(t+2)              A0(t+1) B0(t+1)
-  // A half is refilled in the phase after its last read (LDS WAR), waited for one phase before
-  // its first read (RAW: wait, barrier, read); in steady state each wait leaves the four
-  // younger groups (8 instructions) in flight.  Step t of this WG is K-tile k = t mod nk of
-  // its item j = t / nk; `cur` is item j, `nxt` item j+1 (nk >= 2: steps t+1, t+2 lie in one
-  // of the two).  Every wait is computed from the per-wave ledger (ops, issue marks).
+  // ---- main loop: gemm8p's two phases per K-tile over the continuous step sequence ----
+  //   phase  quadrants          ds_read (L)           LDS-DMA issued (L)              wait (L)
+  //   Q1     (0,0) (0,1)        A0(u) B0(u) B1(u)     A1(u+1)                         A1(u)
+  //   Q2     (1,1) (1,0)        A1(u)                 A0 B0 B1 (+bias) (u+2)          A0 B0 B1 (+bias) (u+1)
+  // Step u is K-tile k of item j (u = j nk + k); steps u+1, u+2 lie in item j or j+1 (nk >= 2).
+  // Wait counts: Q1(u) leaves Q2(u-1)'s loads (6, +1 with a bias DMA) younger, Q2(u) leaves
+  // Q1(u)'s 2; both + S when the epilogue of item j-1 ran since the awaited issue (k == 0).
   int j = 0, k = 0;
-  Item cur = item_at(0), nxt = item_at(1);
-  if (cur.split < 0) return;  // (the host never launches an idle WG)
+  Item cur = item_at(0), nxt = item_at(nmine > 1 ? 1 : 0);
   zero_acc();
-  int ops = 0;  // memory instructions this wave has issued (loads, LDS-DMA, stores), in order
-  // issue half h of K-tile `ahead` steps after (item cur, local k); returns the issue mark
-  auto issue = [&](auto hc, int ahead, int t) -> int {
-    const bool same = k + ahead < nk;
-    const Item& it = same ? cur : nxt;
-    if (it.split >= 0) {
-      const int kk = same ? k + ahead : k + ahead - nk;
-      dma(hc, it, kk, t + ahead);
-      ops += 2;
-      if (decltype(hc)::value == 2 && kk == 0 && has_bias && wave == 0) {  // the item's bias, with B0 of its first K-tile
-        bias_dma(it, (t + ahead) / nk);
-        ops += 1;
-      }
-    }
-    return ops;
-  };
-  // prologue: A0 B0 B1 A1 of K-tile 0, A0 B0 B1 of K-tile 1
-  issue(H0{}, 0, 0);
-  int mB0 = issue(H2{}, 0, 0);  // (B0(t) and A0(t) are read together: one mark)
-  int mB1 = issue(H3{}, 0, 0);
-  int mA1 = issue(H1{}, 0, 0);
-  issue(H0{}, 1, 0);
-  int mB0n = issue(H2{}, 1, 0);
-  int mB1n = issue(H3{}, 1, 0);
-  vm_wait(ops - mB0);
+  // prologue: A0 B0 B1 (+bias) of step 0, A1 of step 0, A0 B0 B1 of step 1
+  load(0, cur, 0, 0);
+  load(2, cur, 0, 0);
+  load(3, cur, 0, 0);
+  if (has_bias) bias_dma(cur, 0);
+  load(1, cur, 0, 0);
+  load(0, cur, 1, 1);
+  load(2, cur, 1, 1);
+  load(3, cur, 1, 1);
+  wait_vmc<8>();  // A0 B0 B1 (+bias) of step 0: A1(0) and step 1's three halves younger
   bar();
   if (lag) bar();  // waves 4-7 fall one barrier behind
+  int S = 0;        // stores left in flight by the last epilogue (k == 0 phases only)
+  int q2prev = 6;   // loads issued by the previous Q2 (prologue: step 1's three halves)
 
   bf16x8 fa[2][4], fb0[2][2], fb1[2][2];
-  for (int t = 0;; ++t) {
-    // P1: (0,0).  L: [epilogue of the previous item] read A0, B0 (t); wait B1 (t); issue A1 (t+1)
-    readA(fa, t, 0);
-    readB(fb0, t, 2);
-    vm_wait(ops - mB1);
-    const int mA1n = issue(H1{}, 1, t);
+  for (int u = 0;; ++u) {
+    const bool has1 = u + 1 < total, has2 = u + 2 < total;
+    // Q1: (0,0), (0,1).  L: read A0, B0, B1 (u); wait A1 (u); issue A1 (u+1)
+    readA(fa, u, 0);
+    readB(fb0, u, 2);
+    readB(fb1, u, 3);
+    const int e1 = k == 0 ? S : 0;
+    {
+      const int n1 = q2prev + e1;  // steady state: 6, +1 with a bias DMA in that phase
+      if (n1 == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+      else if (n1 == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else wait_le(n1);
+    }
+    if (has1) {
+      if (k + 1 < nk) load(1, cur, k + 1, u + 1);
+      else load(1, nxt, 0, u + 1);
+    }
     lds_done();
     bar();
+    __builtin_amdgcn_s_setprio(1);
     mma(fa, fb0, acc[0][0]);
-    bar();
-    // P2: (0,1).  L: read B1 (t); wait A1 (t); issue A0 (t+2)
-    readB(fb1, t, 3);
-    vm_wait(ops - mA1);
-    issue(H0{}, 2, t);
-    lds_done();
-    bar();
     mma(fa, fb1, acc[0][1]);
+    __builtin_amdgcn_s_setprio(0);
     bar();
-    // P3: (1,1).  L: read A1 (t); issue B0 (t+2)
-    readA(fa, t, 1);
-    const int mB0nn = issue(H2{}, 2, t);
+    // Q2: (1,1), (1,0).  L: read A1 (u); wait A0 B0 B1 (+bias) (u+1); issue A0 B0 B1 (+bias) (u+2)
+    readA(fa, u, 1);
+    const int q1n = has1 ? 2 : 0;
+    if (q1n + e1 == 2) wait_vmc<2>();
+    else wait_le(q1n + e1);
+    q2prev = 0;
+    if (has2) {
+      const bool same = k + 2 < nk;
+      const int k2 = same ? k + 2 : k + 2 - nk;
+      const Item& t2 = same ? cur : nxt;
+      load(0, t2, k2, u + 2);
+      load(2, t2, k2, u + 2);
+      load(3, t2, k2, u + 2);
+      q2prev = 6;
+      if (k2 == 0 && has_bias) {
+        bias_dma(t2, j + 1);
+        q2prev = 7;
+      }
+    }
     lds_done();
     bar();
+    __builtin_amdgcn_s_setprio(1);
     mma(fa, fb1, acc[1][1]);
-    bar();
-    // P4: (1,0).  L: wait A0 B0 (t+1); issue B1 (t+2)
-    vm_wait(ops - mB0n);
-    const int mB1nn = issue(H3{}, 2, t);
-    fence();
-    bar();
     mma(fa, fb0, acc[1][0]);
+    __builtin_amdgcn_s_setprio(0);
     bar();
-    mB1 = mB1n;
-    mB1n = mB1nn;
-    mB0n = mB0nn;
-    mA1 = mA1n;
     if (++k == nk) {  // the item's last K-tile: epilogue, stores left in flight
       fence();
-      ops += epilogue(cur, j);
+      S = epilogue(cur, j);
       zero_acc();
       fence();
+      if (++j == nmine) break;
       k = 0;
-      ++j;
       cur = nxt;
-      if (cur.split < 0) break;
-      nxt = item_at(j + 1);
+      nxt = item_at(j + 1 < nmine ? j + 1 : j);
     }
   }
   if (!lag) bar();  // realign the two groups (every barrier is matched)
@@ -542,7 +541,7 @@ bool gemm8q_supports(const Epi& e, bool out_f32) {
 }
 
 int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int64_t lda, const void* B, int64_t ldb,
-                  int M, int N, int K, int splits, const Epi& e, float* slab, hipStream_t st) {
+                  int M, int N, int K, int splits, const Epi& e, float* slab, hipStream_t st, float* dsum) {
   CAPK_CHECK_ARG((a_kmajor ? (int64_t)M * lda : (int64_t)K * lda) * 2 < (1ll << 31) &&
                      (b_kmajor ? (int64_t)N * ldb : (int64_t)K * ldb) * 2 < (1ll << 31),
                  "capk_gemm(bf16, 256x256): operand larger than 2 GiB");
@@ -580,7 +579,8 @@ int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int
                      (!p.side || (int64_t)M * p.lds * esz < (1ll << 31)),
                  "capk_gemm(bf16, 256x256): output or side operand larger than 2 GiB");
   const int items = cdiv(M, 256) * cdiv(N, 256) * splits;
-  const int grid = items <= 256 ? items : 256;
+  CAPK_CHECK_ARG(items > 256, "capk_gemm(gemm8q): persistent kernel for grids of more than 256 items");
+  const int grid = 256;
 #define L8(AK, BKM, OT, ACTK, SD)                                                                                 \
   hipLaunchKernelGGL((gemm8q_kernel<AK, BKM, OT, ACTK, SD>), dim3(grid), dim3(512), 0, st, A, lda, B, ldb, M, N, K, \
                      splits, p, slab)
@@ -605,7 +605,13 @@ int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int
   }
   CAPK_CHECK_ARG(!fwd_act || slab || (a_kmajor && b_kmajor), "capk_gemm(gemm8q): forward activations need K-major operands");
   const bool side = !slab && p.side_kind != SIDE_NONE;
-  if (out_f32) {
+  if (dsum) {  // dX with the backward-activation multiply + column sums (capk_gemm_dx_act_colsum)
+    CAPK_CHECK_ARG(a_kmajor && !b_kmajor && !out_f32 && side && p.side_kind == SIDE_AUX,
+                   "capk_gemm(gemm8q): column sums only on the dX x act' product");
+    p.dsum = dsum;
+    hipLaunchKernelGGL((gemm8q_kernel<true, false, bf16, 0, true, true>), dim3(grid), dim3(512), 0, st, A, lda, B, ldb,
+                       M, N, K, splits, p, slab);
+  } else if (out_f32) {
     // fp32 outputs: no activation, no side operand (gemm8q_supports)
     if (a_kmajor && b_kmajor) L8(true, true, float, 0, false);
     else if (a_kmajor) L8(true, false, float, 0, false);

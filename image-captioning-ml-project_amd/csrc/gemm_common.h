@@ -336,7 +336,11 @@ int launch_gemm8p_f8(bool out_f32, int grid, const void* A, int64_t lda, const u
                      hipStream_t st);
 // gemm8q.hip: the persistent 256x256 kernel (grid = min(tiles * splits, 256))
 bool gemm8q_supports(const Epi& e, bool out_f32);
+// misc.hip: out[n] (+)= sum over `parts` partial rows part[r][n] (fixed order)
+int launch_colsum_finish(int parts, int N, const float* part, float* out, int accumulate, hipStream_t st);
+// dsum != nullptr: the dX x act' product also writes per-(tile row, wave row) column-sum
+// partials [2 * cdiv(M, 256)][N] fp32 there (capk_gemm_dx_act_colsum)
 int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int64_t lda, const void* B, int64_t ldb,
-                  int M, int N, int K, int splits, const Epi& e, float* slab, hipStream_t st);
+                  int M, int N, int K, int splits, const Epi& e, float* slab, hipStream_t st, float* dsum = nullptr);
 
 }  // namespace capk

@@ -424,6 +424,12 @@ static int grid_for(int64_t work, int per_block = 256) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(8192, (work + per_block - 1) / per_block));
 }
 
+int launch_colsum_finish(int parts, int N, const float* part, float* out, int accumulate, hipStream_t st) {
+  hipLaunchKernelGGL(colsum_finish_kernel, dim3(cdiv(N, 16)), dim3(1024), 0, st, parts, N, part, out, accumulate);
+  CAPK_LAUNCH_CHECK("colsum_finish_kernel");
+  return CAPK_OK;
+}
+
 }  // namespace capk
 
 using namespace capk;

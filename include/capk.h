@@ -228,6 +228,16 @@ int capk_colsum(int dtype, int M, int N, const void* dy, int64_t ldy, float* db,
  * ws: capk_colsum_workspace(M, N). */
 int capk_act_bwd_colsum(int dtype, int M, int N, void* C, int64_t ldc, const void* aux, int64_t ldx, int act,
                         float* db, int accumulate, void* ws, size_t ws_bytes, void* stream);
+/* C[M,N] = (dY[M,K] W[K,N]) * act'(pre) (act | CAPK_ACT_DERIV: * aux) and db (+)= the column
+ * sums of C -- the FFN backward of a pre-LN block in one call: fc2's dX product, the GELU
+ * backward and fc1's bias gradient (ViTMLP, modeling_vit.py:249-254).  bf16
+ * operands (dY K-major with ldy, W [K][N] with ldw), bf16 C / aux, fp32 db.  Large grids run
+ * the persistent GEMM with the column sums taken from its register epilogue; others the
+ * product + capk_act_bwd_colsum.  ws: capk_gemm_dx_act_colsum_workspace(M, N, K). */
+size_t capk_gemm_dx_act_colsum_workspace(int M, int N, int K);
+int capk_gemm_dx_act_colsum(int M, int N, int K, const void* dY, int64_t ldy, const void* W, int64_t ldw, void* C,
+                            int64_t ldc, int act, const void* aux, int64_t ldx, float* db, int accumulate, void* ws,
+                            size_t ws_bytes, void* stream);
 /* elementwise casts / copies */
 int capk_cast(int in_dtype, int out_dtype, int64_t n, const void* x, void* y, void* stream);
 int capk_copy_rows(int dtype, int rows, int cols, const void* x, int64_t ldx, void* y, int64_t ldy, void* stream);

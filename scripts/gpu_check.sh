@@ -20,6 +20,10 @@ for step in "$@"; do
     gemmtests) run gemmtests 400 python -u -m pytest tests/test_gpu_gemm.py tests/test_gpu_kernels.py -q -rf --timeout 120 --timeout-method thread ;;
     gemm5) GEMM_GRAPH=1 GEMM_ONLY=${SHAPES:-vit_qkv_fwd,vit_o_fwd,vit_fc1_fwd_plain,vit_fc1_fwd_gelu_deriv,vit_fc2_fwd,vit_qkv_dx,vit_fc1_dx,vit_fc2_dx_gelu_deriv,vit_o_dw,vit_fc1_dw,vit_qkv_dw,lm_head_fwd,lm_head_dw,bf16_4k,bf16_8k} run gemm5 300 python tools/gemm_bench.py ;;
     gemm6) CAPK_GEMM_8Q=1 GEMM_GRAPH=1 GEMM_ONLY=${SHAPES:-vit_qkv_fwd,vit_o_fwd,vit_fc1_fwd_plain,vit_fc1_fwd_gelu_deriv,vit_fc2_fwd,vit_qkv_dx,vit_fc1_dx,vit_fc2_dx_gelu_deriv,vit_o_dw,vit_fc1_dw,vit_qkv_dw,lm_head_fwd,lm_head_dw,bf16_4k,bf16_8k} run gemm6 300 python tools/gemm_bench.py ;;
+    gemmpf) for pf in ${PFS:-0 3 4 6}; do CAPK_GEMM_PF=$pf CAPK_GEMM_8Q=1 GEMM_GRAPH=1 GEMM_ONLY=${SHAPES:-vit_qkv_fwd,vit_o_fwd,vit_fc1_fwd_plain,vit_fc2_fwd,vit_qkv_dx,vit_fc1_dx,vit_fc2_dx_gelu_deriv,lm_head_fwd,bf16_4k} run gemmpf$pf 200 python tools/gemm_bench.py; done ;;
+    bench3q) CAPK_GEMM_8Q=1 run bench_config3_8q 480 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --beam-batch 0 ;;
+    diag) for d in ${DIAGS:-nostore row0}; do CAPK_LIB_PATH=$PWD/image-captioning-ml-project_amd/capk/libcapk_diag_$d.so CAPK_GEMM_8Q=1 GEMM_GRAPH=1 GEMM_ONLY=${SHAPES:-vit_qkv_fwd,vit_o_fwd,vit_fc1_fwd_plain,vit_fc1_fwd_gelu_deriv,vit_fc2_fwd,vit_qkv_dx,lm_head_fwd,bf16_4k} run diag_$d 200 python tools/gemm_bench.py; done ;;
+    vit) run vit 600 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_config4.py tests/test_gpu_fp8.py tests/test_gpu_kernels.py tests/test_gpu_gemm.py -q -rf --timeout 240 --timeout-method thread ;;
     plugins) run plugins 400 python -u -m pytest tests/test_gpu_plugins.py tests/test_gpu_checkpoint.py -q -rf --timeout 240 --timeout-method thread ;;
     tests) run tests 600 python -u -m pytest tests -m gpu -q -rf --timeout 240 --timeout-method thread ;;
     smoke) run smoke 240 python -c "import __graft_entry__ as g; g.smoke()" ;;

@@ -158,3 +158,26 @@ def test_epilogue_variants_exact_layout(ops):
     wt = torch.randn(N, N, device="cuda", generator=g).bfloat16() / 16
     dx = ops.linear_dx(dy, wt, act_bwd=ACT_GELU_ERF | ACT_DERIV, aux=pre)
     assert _rel(dx, (dy.float() @ wt.float()) * pre.float()) < 1e-2
+
+
+@cuda
+@pytest.mark.parametrize("M", [6400 - 24, 1000])
+def test_dx_act_colsum_fused(M):
+    """capk_gemm_dx_act_colsum: C = (dY W) * act'(pre) with db = column sums of C, vs torch fp32
+    on the bf16 inputs.  M = 6376 x N = 3072 is a persistent grid (25 x 12 items: the fused
+    register-epilogue column sums, a ragged last tile row); M = 1000 takes the product +
+    act_bwd_colsum route."""
+    from capk import ops
+    from capk._lib import ACT_DERIV, ACT_GELU_ERF
+    g = torch.Generator(device="cuda").manual_seed(M)
+    N, K = 3072, 768  # dX [M, N] = dY [M, K] @ W [K, N]
+    dy = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(K, N, device="cuda", generator=g) / math.sqrt(K)).bfloat16()
+    aux = torch.rand(M, N, device="cuda", generator=g).bfloat16()  # act'(pre) in [0, 1)
+    db = torch.full((N,), 7.0, device="cuda")
+    out = ops.linear_dx(dy, w, act_bwd=ACT_GELU_ERF | ACT_DERIV, aux=aux, dsum=db)
+    ref = (dy.float() @ w.float()) * aux.float()
+    assert _rel(out, ref) < 1e-2
+    refb = out.float().sum(0)  # the sums of the values actually stored (bf16-rounded) ...
+    assert _rel(db, ref.sum(0)) < 2e-3  # ... and of the exact product
+    assert _rel(db, refb) < 2e-3
