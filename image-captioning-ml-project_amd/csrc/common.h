@@ -1,5 +1,6 @@
 // Shared device/host helpers for libcapk (gfx950 only).
 #pragma once
+#include <type_traits>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -162,20 +163,25 @@ __device__ __forceinline__ float gelu_sig(float x, float u) {  // sigmoid(z), u 
   const float z = x * fmaf(u, kGeluC1, kGeluC0);
   return __frcp_rn(1.0f + __expf(-z));
 }
+// T: the storage type of the values; fp32 storage (the parity path's passes) keeps the exact
+// erf forms.
+template <typename T>
 __device__ __forceinline__ float act_fwd_fast(int act, float x) {
-  if (act == CAPK_ACT_GELU_ERF) return x * gelu_sig(x, x * x);
+  if (act == CAPK_ACT_GELU_ERF && !std::is_same<T, float>::value) return x * gelu_sig(x, x * x);
   return act_fwd(act, x);
 }
+template <typename T>
 __device__ __forceinline__ float act_grad_fast(int act, float x) {
-  if (act == CAPK_ACT_GELU_ERF) {
+  if (act == CAPK_ACT_GELU_ERF && !std::is_same<T, float>::value) {
     const float u = x * x, s = gelu_sig(x, u);
     return fmaf(x * fmaf(-s, s, s), fmaf(u, 3.0f * kGeluC1, kGeluC0), s);  // s + x s (1 - s) z'
   }
   return act_grad(act, x);
 }
 // act(x) and act'(x) together (one sigmoid evaluation for GELU): CAPK_ACT_DERIV epilogues
+template <typename T>
 __device__ __forceinline__ float act_fwd_grad_fast(int act, float x, float& d) {
-  if (act == CAPK_ACT_GELU_ERF) {
+  if (act == CAPK_ACT_GELU_ERF && !std::is_same<T, float>::value) {
     const float u = x * x, s = gelu_sig(x, u);
     d = fmaf(x * fmaf(-s, s, s), fmaf(u, 3.0f * kGeluC1, kGeluC0), s);
     return x * s;

@@ -146,8 +146,8 @@ __global__ __launch_bounds__(256) void act_pass_kernel(int M, int N, OutT* __res
       Vec8<OutT>::load(pre + (i + stride) * 8, w);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        v[k] = act_fwd_fast(a, v[k]);
-        w[k] = act_fwd_fast(a, w[k]);
+        v[k] = act_fwd_fast<OutT>(a, v[k]);
+        w[k] = act_fwd_fast<OutT>(a, w[k]);
       }
       Vec8<OutT>::store(C + i * 8, v);
       Vec8<OutT>::store(C + (i + stride) * 8, w);
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void act_pass_kernel(int M, int N, OutT* __res
       float v[8];
       Vec8<OutT>::load(pre + i * 8, v);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = act_fwd_fast(a, v[k]);
+      for (int k = 0; k < 8; ++k) v[k] = act_fwd_fast<OutT>(a, v[k]);
       Vec8<OutT>::store(C + i * 8, v);
     }
     return;
@@ -175,8 +175,8 @@ __global__ __launch_bounds__(256) void act_pass_kernel(int M, int N, OutT* __res
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        v[k] *= (act & CAPK_ACT_DERIV) ? g[k] : act_grad_fast(a, g[k]);
-        if (two) w[k] *= (act & CAPK_ACT_DERIV) ? h[k] : act_grad_fast(a, h[k]);
+        v[k] *= (act & CAPK_ACT_DERIV) ? g[k] : act_grad_fast<OutT>(a, g[k]);
+        if (two) w[k] *= (act & CAPK_ACT_DERIV) ? h[k] : act_grad_fast<OutT>(a, h[k]);
       }
       Vec8<OutT>::store(C + i * 8, v);
       if (two) Vec8<OutT>::store(C + (i + stride) * 8, w);
@@ -189,7 +189,7 @@ __global__ __launch_bounds__(256) void act_pass_kernel(int M, int N, OutT* __res
     if (from_pre) {
       Vec8<OutT>::load(pre + (int64_t)m * ldx + n, v);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = act_fwd_fast(a, v[k]);
+      for (int k = 0; k < 8; ++k) v[k] = act_fwd_fast<OutT>(a, v[k]);
       Vec8<OutT>::store(C + (int64_t)m * ldc + n, v);
       continue;
     }
@@ -198,16 +198,16 @@ __global__ __launch_bounds__(256) void act_pass_kernel(int M, int N, OutT* __res
       float g[8];
       Vec8<OutT>::load(aux + (int64_t)m * ldx + n, g);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] *= (act & CAPK_ACT_DERIV) ? g[k] : act_grad_fast(a, g[k]);
+      for (int k = 0; k < 8; ++k) v[k] *= (act & CAPK_ACT_DERIV) ? g[k] : act_grad_fast<OutT>(a, g[k]);
     } else if (pre && (act & CAPK_ACT_DERIV)) {
       float d[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = act_fwd_grad_fast(a, v[k], d[k]);
+      for (int k = 0; k < 8; ++k) v[k] = act_fwd_grad_fast<OutT>(a, v[k], d[k]);
       Vec8<OutT>::store(pre + (int64_t)m * ldx + n, d);
     } else {
       if (pre) Vec8<OutT>::store(pre + (int64_t)m * ldx + n, v);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = act_fwd_fast(a, v[k]);
+      for (int k = 0; k < 8; ++k) v[k] = act_fwd_fast<OutT>(a, v[k]);
     }
     Vec8<OutT>::store(C + (int64_t)m * ldc + n, v);
   }
@@ -324,11 +324,12 @@ static int choose_cfg(int M, int N, int K, int a_kmajor, int b_kmajor, int act) 
   // the 256x256 phased kernel (gemm8p.hip) whenever its grid (x split-K for the weight
   // gradients) fills most of the chip: measured faster than the 128-row tiles on every
   // config-3 shape of that size (tools/gemm_bench.py, profiles/round2/)
-  // (the persistent gemm8q variant, cfg 6, measured slower in the full config-3 step:
-  // 50 vs 40 ms of GEMM per step, profiles/round3 -- CAPK_GEMM_8Q=1 selects it for A/B)
+  // grids of more than one round take the persistent kernel (cfg 6, gemm8q.hip; the host
+  // routes one-round grids and the epilogues it lacks to gemm8p).  CAPK_GEMM_8Q=0 keeps
+  // every large grid on gemm8p (A/B: profiles/round3/gemm_shapes_*).
   static const int big = [] {
     const char* v = getenv("CAPK_GEMM_8Q");
-    return v && v[0] == '1' ? 6 : 5;
+    return v && v[0] == '0' ? 5 : 6;
   }();
   if (M >= 256 && N >= 256) {
     const int t5 = tiles_of(5, M, N);

@@ -327,12 +327,12 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
       } else if constexpr (ACT != 0) {
         if (e.act & CAPK_ACT_DERIV) {
 #pragma unroll
-          for (int k = 0; k < 8; ++k) v[k] = act_fwd_grad_fast(ACT, v[k], pre[k]);
+          for (int k = 0; k < 8; ++k) v[k] = act_fwd_grad_fast<OutT>(ACT, v[k], pre[k]);
         } else {
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
             pre[k] = v[k];
-            v[k] = act_fwd_fast(ACT, v[k]);
+            v[k] = act_fwd_fast<OutT>(ACT, v[k]);
           }
         }
       }
@@ -376,6 +376,17 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
   // memory instructions it leaves in flight (the second half's stores, + the first's without
   // a side operand).
   auto epilogue = [&](const Item& c, int j) -> int {
+#if defined(CAPK_DIAG_NOEPI)  // diagnostic build: no epilogue at all (accumulators kept live)
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) asm volatile("" ::"v"(acc[a][b][i][jj]));
+    return 0;
+#endif
     SideSeg<OutT> side[2][2][4];
     auto load_side = [&](auto qmc) {
       constexpr int QM = decltype(qmc)::value;

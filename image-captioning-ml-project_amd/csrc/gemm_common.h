@@ -72,19 +72,19 @@ __device__ __forceinline__ void epilogue8(const Epi& e, int m, int n, float (&v)
       for (int i = 0; i < 8; ++i) v[i] *= a[i];
     } else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] *= act_grad_fast(act, a[i]);
+      for (int i = 0; i < 8; ++i) v[i] *= act_grad_fast<OutT>(act, a[i]);
     }
   } else if (e.act) {
     const int act = e.act & 15;
     if (e.pre && (e.act & CAPK_ACT_DERIV)) {
       float d[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = act_fwd_grad_fast(act, v[i], d[i]);
+      for (int i = 0; i < 8; ++i) v[i] = act_fwd_grad_fast<OutT>(act, v[i], d[i]);
       Vec8<OutT>::store((OutT*)e.pre + (int64_t)m * e.ldx + n, d);
     } else {
       if (e.pre) Vec8<OutT>::store((OutT*)e.pre + (int64_t)m * e.ldx + n, v);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = act_fwd_fast(act, v[i]);
+      for (int i = 0; i < 8; ++i) v[i] = act_fwd_fast<OutT>(act, v[i]);
     }
   }
   if (e.drop.on()) {

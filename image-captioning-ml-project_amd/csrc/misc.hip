@@ -274,8 +274,8 @@ __global__ __launch_bounds__(256) void act_bwd_colsum_kernel(int M, int N, T* __
       Vec8<T>::load(aux + (int64_t)(m + 4) * ldx + c * 8, g1);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        v0[i] *= deriv ? g0[i] : act_grad_fast(a, g0[i]);
-        v1[i] *= deriv ? g1[i] : act_grad_fast(a, g1[i]);
+        v0[i] *= deriv ? g0[i] : act_grad_fast<T>(a, g0[i]);
+        v1[i] *= deriv ? g1[i] : act_grad_fast<T>(a, g1[i]);
         acc[i] += v0[i] + v1[i];
       }
       Vec8<T>::store(C + (int64_t)m * ldc + c * 8, v0);
@@ -287,7 +287,7 @@ __global__ __launch_bounds__(256) void act_bwd_colsum_kernel(int M, int N, T* __
       Vec8<T>::load(aux + (int64_t)m * ldx + c * 8, g);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        v[i] *= deriv ? g[i] : act_grad_fast(a, g[i]);
+        v[i] *= deriv ? g[i] : act_grad_fast<T>(a, g[i]);
         acc[i] += v[i];
       }
       Vec8<T>::store(C + (int64_t)m * ldc + c * 8, v);
