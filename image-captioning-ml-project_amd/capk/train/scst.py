@@ -24,6 +24,9 @@ _calculate_rewards (src/train/trainer.py:319-484) with the SURVEY fixes:
         re-decode of the prefix computes the same last-position logits (no dropout in the
         sampler, the hidden state of a prefix does not depend on later tokens).
 """
+import threading
+import time
+
 import numpy as np
 import torch
 
@@ -194,12 +197,11 @@ def scst_step(model, images, references, optimizer, lr, seed, max_length=20, bas
     `lr` = None uses the optimizer's scheduled rate.  Returns (loss, mean sample reward,
     mean baseline reward).
 
-    The rewards are needed only by the loss: the sampled / baseline ids are copied to pinned
-    host memory right after the searches, the teacher-forced forward is queued behind the
-    copy, and the host scores CIDEr-D while the GPU runs that forward.  ``phase_times``
+    The rewards are needed only by the loss: the sampled ids are copied to pinned host memory
+    right after sampling and scored on a host thread while the GPU runs the baseline search;
+    the baseline ids likewise while it runs the teacher-forced forward.  ``phase_times``
     (dict, optional) accumulates the GPU milliseconds of each phase (encoder, sample,
     baseline, forward, loss_backward, optimizer) and the host scoring time."""
-    import time
     dec = model.decoder
     ph = _Phases(phase_times)
     ph.mark("start")
@@ -208,16 +210,34 @@ def scst_step(model, images, references, optimizer, lr, seed, max_length=20, bas
     enc_nograd = {k: (v.detach() if torch.is_tensor(v) else v) for k, v in enc.items()}
     ids, _ = sample_captions(dec, enc_nograd, max_length, seed)
     ph.mark("sample")
+    eos, pad, bos = dec.eos_token_id, dec.pad_token_id, dec.bos_token_id
+    refs = [[list(x) for x in rs] for rs in references]
+    host = {"ms": 0.0}
+
+    def score_async(dev_ids):
+        """copy ids to pinned memory behind the work queued so far and score them on a host
+        thread (the C++ scorer releases the GIL) while the GPU runs what comes next"""
+        h = torch.empty(dev_ids.shape, dtype=dev_ids.dtype, pin_memory=True)
+        h.copy_(dev_ids, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        out = {}
+
+        def run():
+            ev.synchronize()
+            t0 = time.perf_counter()
+            out["r"] = cider_d([strip_special(r, eos, pad, bos) for r in h.tolist()], refs)
+            host["ms"] += (time.perf_counter() - t0) * 1e3
+
+        th = threading.Thread(target=run)
+        th.start()
+        return th, out
+
+    th_s, out_s = score_async(ids)  # the samples are scored during the baseline search
     with torch.no_grad():
         base_ids, _ = dec.generate(enc_nograd, max_length, **(baseline_kwargs or {}))
     ph.mark("baseline")
-    eos, pad, bos = dec.eos_token_id, dec.pad_token_id, dec.bos_token_id
-    ids_h = torch.empty(ids.shape, dtype=ids.dtype, pin_memory=True)
-    base_h = torch.empty(base_ids.shape, dtype=base_ids.dtype, pin_memory=True)
-    ids_h.copy_(ids, non_blocking=True)
-    base_h.copy_(base_ids, non_blocking=True)
-    copied = torch.cuda.Event()
-    copied.record()
+    th_b, out_b = score_async(base_ids)  # the baselines during the teacher-forced forward
     from ..models.decoders import GPT2Decoder, LSTMDecoder
     if isinstance(dec, GPT2Decoder):
         logits = dec.forward_logits(enc["pooled_features"], ids, use_pad_mask=False)
@@ -226,14 +246,11 @@ def scst_step(model, images, references, optimizer, lr, seed, max_length=20, bas
     else:
         logits, _ = dec.forward_logits(enc["features"], ids, use_pad_mask=False)
     ph.mark("forward")
-    copied.synchronize()  # the ids only; the forward keeps running
-    t0 = time.perf_counter()
-    samp = [strip_special(r, eos, pad, bos) for r in ids_h.tolist()]
-    base = [strip_special(r, eos, pad, bos) for r in base_h.tolist()]
-    refs = [[list(x) for x in rs] for rs in references]
-    r_s, r_b = cider_d(samp, refs), cider_d(base, refs)
+    th_s.join()
+    th_b.join()
+    r_s, r_b = out_s["r"], out_b["r"]
+    host_ms = host["ms"]
     adv_h = torch.from_numpy((r_s - r_b).astype(np.float32)).pin_memory()
-    host_ms = (time.perf_counter() - t0) * 1e3
     adv = adv_h.to(ids.device, non_blocking=True)
     loss = policy_gradient_loss(logits, ids, adv, eos)
     loss.backward()

@@ -21,6 +21,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <unordered_map>
@@ -122,17 +123,18 @@ void sim(const Vec& h, const Vec& r, int nmax, double sigma, double* out) {
 }
 
 template <typename F>
-void parallel_for(int64_t n, int threads, F&& f) {
-  if (threads <= 1 || n < 64) {
+void parallel_for(int64_t n, int threads, F&& f, int64_t min_n = 64) {
+  if (threads <= 1 || n < min_n) {
     for (int64_t i = 0; i < n; ++i) f(i);
     return;
   }
   std::atomic<int64_t> next{0};
   std::vector<std::thread> pool;
+  const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(16, n / (2 * (int64_t)threads)));
   for (int t = 0; t < threads; ++t)
     pool.emplace_back([&] {
-      for (int64_t i; (i = next.fetch_add(16)) < n;)
-        for (int64_t k = i; k < std::min(n, i + 16); ++k) f(k);
+      for (int64_t i; (i = next.fetch_add(chunk)) < n;)
+        for (int64_t k = i; k < std::min(n, i + chunk); ++k) f(k);
     });
   for (auto& th : pool) th.join();
 }
@@ -145,25 +147,40 @@ extern "C" int capk_cider_d(int n_cand, const int32_t* cand_tok, const int64_t* 
   if (n_cand < 0 || n_max < 1 || n_max > NMAX || !scores || (n_cand > 0 && (!cand_off || !ref_off || !ref_img)))
     return CAPK_EINVAL;
   if (n_cand == 0) return CAPK_OK;
-  if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
+  if (threads <= 0) {
+    // the process's CPU share, not the node's: a GPU box exposes every core of the node
+    // (hardware_concurrency 256) to a 16-CPU cgroup, and one std::thread per core per
+    // parallel_for costs more than the scoring itself
+    threads = (int)std::max(1u, std::thread::hardware_concurrency());
+    if (const char* e = getenv("OMP_NUM_THREADS")) threads = std::min(threads, std::max(1, atoi(e)));
+    threads = std::min(threads, 16);
+  }
   const int64_t n_ref = ref_img[n_cand];
   std::vector<Cooked> rc(n_ref);
   parallel_for(n_ref, threads, [&](int64_t r) { cook(ref_tok + ref_off[r], ref_off[r + 1] - ref_off[r], n_max, rc[r]); });
   // document frequency: once per image for every n-gram in the union of its references
+  // (per order: each image's unique keys, all images' lists sorted together and counted)
   DF df[NMAX];
-  {
-    std::vector<Key> u;
-    for (int n = 0; n < n_max; ++n) {
-      for (int i = 0; i < n_cand; ++i) {
-        u.clear();
-        for (int64_t r = ref_img[i]; r < ref_img[i + 1]; ++r)
-          for (const auto& kv : rc[r].g[n]) u.push_back(kv.first);
-        std::sort(u.begin(), u.end());
-        u.erase(std::unique(u.begin(), u.end()), u.end());
-        for (const Key& k : u) df[n][k] += 1.0;
-      }
+  parallel_for(
+      n_max, std::min(threads, n_max), [&](int64_t n) {
+    std::vector<Key> all, u;
+    for (int i = 0; i < n_cand; ++i) {
+      u.clear();
+      for (int64_t r = ref_img[i]; r < ref_img[i + 1]; ++r)
+        for (const auto& kv : rc[r].g[n]) u.push_back(kv.first);
+      std::sort(u.begin(), u.end());
+      u.erase(std::unique(u.begin(), u.end()), u.end());
+      all.insert(all.end(), u.begin(), u.end());
     }
-  }
+    std::sort(all.begin(), all.end());
+    df[n].reserve(all.size());
+    for (size_t i = 0; i < all.size();) {
+      size_t j = i;
+      while (j < all.size() && all[j] == all[i]) ++j;
+      df[n].emplace(all[i], (double)(j - i));
+      i = j;
+    }
+  }, 1);
   const double ref_len = std::log((double)n_cand);
   parallel_for(n_cand, threads, [&](int64_t i) {
     Cooked c;

@@ -159,31 +159,57 @@ __device__ __forceinline__ float act_grad(int act, float x) {
 // CU's MFMAs idle, so its VALU count is exposed time.
 constexpr float kGeluC0 = 1.5957691216057308f;               // 2 sqrt(2/pi)
 constexpr float kGeluC1 = 0.0713548162726f;                  // 2 sqrt(2/pi) 0.044715
+constexpr float kLog2eF = 1.4426950408889634f;
 __device__ __forceinline__ float gelu_sig(float x, float u) {  // sigmoid(z), u = x^2
-  const float z = x * fmaf(u, kGeluC1, kGeluC0);
-  return __frcp_rn(1.0f + __expf(-z));
+  // v_exp_f32 (2^t) and v_rcp_f32 (1 ulp) directly: __expf / __frcp_rn expand to range
+  // reduction and a correctly rounded division (10 more instructions per element)
+  const float t = x * fmaf(u, kGeluC1 * kLog2eF, kGeluC0 * kLog2eF);
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-t));
+}
+__device__ __forceinline__ float sig_fast(float x) {  // 1 / (1 + e^-x) on v_exp_f32 / v_rcp_f32
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-x * kLog2eF));
+}
+// The GELU-family activations for bf16 storage: s = the logistic factor, z' = d(arg)/dx;
+// act = x s, act' = s + x s (1 - s) z'.  GELU_TANH (GPT-2 gelu_new) IS this form exactly;
+// GELU_ERF uses it as above; QUICK_GELU (CLIP) is x sigmoid(1.702 x).
+__device__ __forceinline__ bool fast_family(int act) {
+  return act == CAPK_ACT_GELU_ERF || act == CAPK_ACT_GELU_TANH || act == CAPK_ACT_QUICK_GELU;
+}
+__device__ __forceinline__ float fast_sig(int act, float x, float& zp) {
+  if (act == CAPK_ACT_QUICK_GELU) {
+    zp = 1.702f;
+    return sig_fast(1.702f * x);
+  }
+  const float u = x * x;
+  zp = fmaf(u, 3.0f * kGeluC1, kGeluC0);
+  return gelu_sig(x, u);
 }
 // T: the storage type of the values; fp32 storage (the parity path's passes) keeps the exact
-// erf forms.
+// forms (erff, tanhf, expf).
 template <typename T>
 __device__ __forceinline__ float act_fwd_fast(int act, float x) {
-  if (act == CAPK_ACT_GELU_ERF && !std::is_same<T, float>::value) return x * gelu_sig(x, x * x);
+  if (!std::is_same<T, float>::value && fast_family(act)) {
+    float zp;
+    return x * fast_sig(act, x, zp);
+  }
   return act_fwd(act, x);
 }
 template <typename T>
 __device__ __forceinline__ float act_grad_fast(int act, float x) {
-  if (act == CAPK_ACT_GELU_ERF && !std::is_same<T, float>::value) {
-    const float u = x * x, s = gelu_sig(x, u);
-    return fmaf(x * fmaf(-s, s, s), fmaf(u, 3.0f * kGeluC1, kGeluC0), s);  // s + x s (1 - s) z'
+  if (!std::is_same<T, float>::value && fast_family(act)) {
+    float zp;
+    const float s = fast_sig(act, x, zp);
+    return fmaf(x * fmaf(-s, s, s), zp, s);  // s + x s (1 - s) z'
   }
   return act_grad(act, x);
 }
-// act(x) and act'(x) together (one sigmoid evaluation for GELU): CAPK_ACT_DERIV epilogues
+// act(x) and act'(x) together (one logistic evaluation): CAPK_ACT_DERIV epilogues
 template <typename T>
 __device__ __forceinline__ float act_fwd_grad_fast(int act, float x, float& d) {
-  if (act == CAPK_ACT_GELU_ERF && !std::is_same<T, float>::value) {
-    const float u = x * x, s = gelu_sig(x, u);
-    d = fmaf(x * fmaf(-s, s, s), fmaf(u, 3.0f * kGeluC1, kGeluC0), s);
+  if (!std::is_same<T, float>::value && fast_family(act)) {
+    float zp;
+    const float s = fast_sig(act, x, zp);
+    d = fmaf(x * fmaf(-s, s, s), zp, s);
     return x * s;
   }
   d = act_grad(act, x);

@@ -24,6 +24,7 @@ for step in "$@"; do
     bench3p) CAPK_GEMM_8Q=0 run bench_config3_8p 480 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --beam-batch 0 ;;
     diag) for d in ${DIAGS:-nostore row0}; do CAPK_LIB_PATH=$PWD/image-captioning-ml-project_amd/capk/libcapk_diag_$d.so CAPK_GEMM_8Q=1 GEMM_GRAPH=1 GEMM_ONLY=${SHAPES:-vit_qkv_fwd,vit_o_fwd,vit_fc1_fwd_plain,vit_fc1_fwd_gelu_deriv,vit_fc2_fwd,vit_qkv_dx,lm_head_fwd,bf16_4k} run diag_$d 200 python tools/gemm_bench.py; done ;;
     vit) run vit 600 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_config4.py tests/test_gpu_fp8.py tests/test_gpu_kernels.py tests/test_gpu_gemm.py -q -rf --timeout 240 --timeout-method thread ;;
+    scst) run scst 600 python -u -m pytest tests/test_gpu_scst.py tests/test_gpu_config4.py tests/test_gpu_plugins.py -q -rf --timeout 240 --timeout-method thread ;;
     plugins) run plugins 400 python -u -m pytest tests/test_gpu_plugins.py tests/test_gpu_checkpoint.py -q -rf --timeout 240 --timeout-method thread ;;
     tests) run tests 600 python -u -m pytest tests -m gpu -q -rf --timeout 240 --timeout-method thread ;;
     smoke) run smoke 240 python -c "import __graft_entry__ as g; g.smoke()" ;;
