@@ -56,8 +56,8 @@ def beam_bench(model, batch, reps, device, rank):
     return dt, gem, int(ids.shape[1])
 
 
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "round2", "gemm_traffic.json")
-KERNEL_SOURCES = ["gemm.hip", "gemm8p.hip", "gemm_common.h", "common.h"]
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "round3", "gemm_traffic.json")
+KERNEL_SOURCES = ["gemm.hip", "gemm8p.hip", "gemm8q.hip", "gemm_common.h", "common.h"]
 
 
 def kernel_source_hash():

@@ -260,9 +260,17 @@ def linear_dx(dy, w, *, out=None, act_bwd=0, aux=None, beta=0.0, drop=NO_DROP, d
             L = lib()
             wsb = L.capk_gemm_dx_act_colsum_workspace(M, K, N)
             ws = _ws(wsb, dy.device)
+            timed = GEMM_TIMER.enabled and not torch.cuda.is_current_stream_capturing()
+            if timed:
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev0.record()
             check(L.capk_gemm_dx_act_colsum(M, K, N, _p(dy), dy.stride(0), _p(w), w.stride(0), _p(out), out.stride(0),
                                             int(act_bwd), _p(aux), aux.stride(0), _p(dsum), 0, _p(ws), wsb, _stream()),
                   "capk_gemm_dx_act_colsum")
+            if timed:  # A, B, aux read once; C written once
+                ev1.record()
+                GEMM_TIMER.records.append((ev0, ev1, 2.0 * M * K * N, dtype_code(dy), 2 * (M * N + N * K + 2 * M * K), 0))
             return out
         gemm(dy, True, w, False, M, K, N, out, lda=dy.stride(0), ldb=w.stride(0), ldc=out.stride(0))
         return act_bwd_colsum(out, aux, act_bwd, dsum)

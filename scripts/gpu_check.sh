@@ -25,6 +25,8 @@ for step in "$@"; do
     diag) for d in ${DIAGS:-nostore row0}; do CAPK_LIB_PATH=$PWD/image-captioning-ml-project_amd/capk/libcapk_diag_$d.so CAPK_GEMM_8Q=1 GEMM_GRAPH=1 GEMM_ONLY=${SHAPES:-vit_qkv_fwd,vit_o_fwd,vit_fc1_fwd_plain,vit_fc1_fwd_gelu_deriv,vit_fc2_fwd,vit_qkv_dx,lm_head_fwd,bf16_4k} run diag_$d 200 python tools/gemm_bench.py; done ;;
     vit) run vit 600 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_config4.py tests/test_gpu_fp8.py tests/test_gpu_kernels.py tests/test_gpu_gemm.py -q -rf --timeout 240 --timeout-method thread ;;
     scst) run scst 600 python -u -m pytest tests/test_gpu_scst.py tests/test_gpu_config4.py tests/test_gpu_plugins.py -q -rf --timeout 240 --timeout-method thread ;;
+    decsweep) for c in ${CFGS:-1 2 3 4}; do CAPK_GEMM_CFG=$c GEMM_GRAPH=1 GEMM_ONLY=dec256_cattn,dec256_cproj,dec256_fc,dec256_proj2,dec1280_cattn,dec1280_cproj,dec1280_fc,dec1280_proj2,tdec1280_qkv,tdec1280_fc1,tdec1280_fc2 run dec_cfg$c 200 python tools/gemm_bench.py; done
+             for ms in ${SPLITS:-1 2 4}; do CAPK_GEMM_MAXSPLIT=$ms GEMM_GRAPH=1 GEMM_ONLY=dec256_cattn,dec256_cproj,dec256_fc,dec256_proj2,dec1280_cattn,dec1280_cproj,dec1280_fc,dec1280_proj2 run dec_split$ms 200 python tools/gemm_bench.py; done ;;
     plugins) run plugins 400 python -u -m pytest tests/test_gpu_plugins.py tests/test_gpu_checkpoint.py -q -rf --timeout 240 --timeout-method thread ;;
     tests) run tests 600 python -u -m pytest tests -m gpu -q -rf --timeout 240 --timeout-method thread ;;
     smoke) run smoke 240 python -c "import __graft_entry__ as g; g.smoke()" ;;

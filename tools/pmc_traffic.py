@@ -11,7 +11,6 @@ Infinity-Cache hits are counted, so tile re-reads absorbed on-die still show up 
 usage: pmc_traffic.py FETCH_DIR WRITE_DIR [--match ...] [--out FILE] [--cmd TEXT]
 The output records src_hash (bench.kernel_source_hash() of this tree): bench.py reports the
 traffic only while the GEMM sources still hash to it.
-(Cijk_* = hipBLASLt's GEMM kernels, the library route of capk_gemm)
 """
 import argparse
 import csv
@@ -41,7 +40,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
-    ap.add_argument("--match", default="gemm_bf16_kernel,gemm8p_kernel,Cijk_,act_pass_kernel,splitk_reduce_kernel")
+    ap.add_argument("--match", default="gemm_bf16_kernel,gemm8p_kernel,gemm8q_kernel,act_pass_kernel,splitk_reduce_kernel,colsum_finish_kernel")
     ap.add_argument("--out")
     ap.add_argument("--cmd", default="")
     a = ap.parse_args()
@@ -49,8 +48,15 @@ def main():
     fv, fn = per_dispatch(a.fetch_dir, "FETCH_SIZE", match)
     wv, _ = per_dispatch(a.write_dir, "WRITE_SIZE", match)
     nf, nw = len(fv), len(wv)
-    fetch = 2.0 * 1024.0 * sum(fv.values()) / max(nf, 1)
-    write = 1024.0 * sum(wv.values()) / max(nw, 1)
+    # per GEMM launch: all matched dispatches' bytes (the GEMM kernel and its companions -- the
+    # split-K reduce, the column-sum finish, the activation pass) over the number of GEMM-kernel
+    # dispatches, i.e. one capk_gemm call's HBM traffic
+    primary = ("gemm_bf16_kernel", "gemm8p_kernel", "gemm8q_kernel")
+    npf = sum(1 for k in fv if any(m in fn[k] for m in primary)) or nf
+    _, wn = per_dispatch(a.write_dir, "WRITE_SIZE", match)
+    npw = sum(1 for k in wv if any(m in wn[k] for m in primary)) or nw
+    fetch = 2.0 * 1024.0 * sum(fv.values()) / max(npf, 1)
+    write = 1024.0 * sum(wv.values()) / max(npw, 1)
     by_kernel = defaultdict(lambda: [0, 0.0])
     for k, v in fv.items():
         e = by_kernel[fn[k][:90]]
@@ -64,6 +70,7 @@ def main():
     res = {"counters": ["FETCH_SIZE", "WRITE_SIZE"], "kernels_matched": match, "command": a.cmd,
            "src_hash": bench.kernel_source_hash(),
            "dispatches_fetch_pass": nf, "dispatches_write_pass": nw,
+           "gemm_launches_fetch_pass": npf, "gemm_launches_write_pass": npw,
            "avg_fetch_bytes": fetch, "avg_write_bytes": write, "avg_hbm_bytes": fetch + write,
            "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 reports half of 16-B/lane streaming reads); WRITE_SIZE KiB x1024",
            "fetch_by_kernel": {k: {"dispatches": n, "avg_fetch_bytes": b / n} for k, (n, b) in sorted(by_kernel.items())}}
