@@ -104,9 +104,11 @@ def gemm(A, a_kmajor, B, b_kmajor, M, N, K, C, *, lda, ldb, ldc, alpha=1.0, beta
     check(rc, "capk_gemm")
     if timed:
         ev1.record()
-        # algorithmic bytes: A and B read once, C written once (+ read when beta != 0)
+        # algorithmic bytes: A and B read once, C written once (+ read when beta != 0), and each
+        # side stream once (residual / aux read, pre-activation written)
         ein, eout = A.element_size(), C.element_size()
-        nbytes = ein * (M * K + N * K) + eout * M * N * (2 if beta else 1)
+        sides = (1 if beta else 0) + (residual is not None) + (aux is not None) + (preact is not None)
+        nbytes = ein * (M * K + N * K) + eout * M * N * (1 + sides)
         GEMM_TIMER.records.append((ev0, ev1, 2.0 * M * N * K, it, nbytes, 0))
     return C
 
