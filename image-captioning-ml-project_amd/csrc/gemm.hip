@@ -437,6 +437,7 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
     const int nk64 = cdiv(K, 64), per = cdiv(nk64, splits);
     const bool padded = nk64 % per != 0;
     if (!gemm8q_supports(e, out_dtype == CAPK_F32) || per < 2 || (padded && (a_kmajor || b_kmajor)) ||
+        splits > 1 ||                          // split-K slabs: gemm8p + splitk_reduce
         tiles_of(6, M, N) * splits <= 256 ||  // one round: the non-persistent kernel
         ((act & 15) && !(act & CAPK_ACT_BWD) && splits == 1 && !(a_kmajor && b_kmajor)))
       cfg = 5;

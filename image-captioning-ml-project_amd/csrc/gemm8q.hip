@@ -29,10 +29,10 @@
 //    where the phase issued a bias DMA).  Too small a count is safe (it only waits longer),
 //    so the run-time counts are rounded down to the encodings wait_le() has.
 //
-// Epilogue: alpha, bias, forward activation (+ pre-activation or act' side output), backward
-// activation (x aux = act'(pre)), dropout, residual, beta*C -- with at most ONE of
-// aux / residual / C (gemm8q_supports); split-K items write fp32 slabs that
-// splitk_reduce_kernel finishes.
+// Epilogue (compile-time forms, gemm8q_supports): bias, a forward GELU-family / ReLU
+// activation with act'(pre) (DV) or pre kept, OR one side operand -- the backward multiply by
+// aux = act'(pre), a residual, or beta*C -- and optionally (DSUM) the column sums of the
+// result.  alpha != 1, dropout and split-K run on gemm8p.
 #include <type_traits>
 
 #include "gemm_common.h"
@@ -101,10 +101,7 @@ struct Epi8q {
   void* pre;
   const float* bias;
   int64_t ldc, lds, ldp;
-  float alpha, beta;
-  int side_kind, act;  // act: CAPK_ACT_* kind | CAPK_ACT_BWD | CAPK_ACT_DERIV
-  Drop drop;
-  int dropN;  // Epi::N (the dropout mask index is m * dropN + n)
+  float beta;
   float* dsum;  // DSUM kernels: column-sum partials [2 * tile rows][N]
 };
 
@@ -125,10 +122,10 @@ __device__ __forceinline__ void wait_le(int n) {
 // DSUM: also the column sums of the final values (the bias gradient of the Linear whose
 // output gradient this dX is): per (tile row, wm) partial rows [2 ntm][N] into e.dsum,
 // summed in a fixed order by colsum_finish (capk_gemm_dx_act_colsum).
-template <bool AK, bool BK, typename OutT, int ACT, bool SIDE, bool DSUM = false>
+template <bool AK, bool BK, typename OutT, int ACT, bool DV, int SK, bool DSUM = false>
 __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A, int64_t lda,
                                                      const void* __restrict__ B, int64_t ldb, int M, int N, int K,
-                                                     int splits, Epi8q e, float* __restrict__ ws) {
+                                                     int splits, Epi8q e) {
   constexpr int HALF = 128 * 64 * 2, STAGE = 4 * HALF, BIAS0 = 2 * STAGE;
   // two stages + bias slots [item parity][wave] of 64 fp32 (the wave's columns)
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 2 * 8 * 256];
@@ -182,7 +179,7 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
                                                (__attribute__((address_space(3))) void*)(dst + (wave * 2 + p) * 1024),
                                                16, vo[h][p] + so, 0, 0, 0);
   };
-  const bool has_bias = e.bias != nullptr && ws == nullptr;
+  const bool has_bias = e.bias != nullptr;
   // the wave's 64 bias columns of item j (lane l: column (l >> 5) * 128 + wn * 32 + (l & 31))
   auto bias_dma = [&](const Item& it, int j) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -190,8 +187,8 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
         (__attribute__((address_space(3))) void*)(smem + BIAS0 + ((j & 1) * 8 + wave) * 256), 4,
         (uint32_t)(it.n0 + (lane >> 5) * 128 + wn * 32 + (lane & 31)) * 4u, 0, 0, 0);
   };
-  const int side_kind = (!SIDE || ws) ? SIDE_NONE : e.side_kind;
-  const bool has_pre = ACT != 0 && !ws && e.pre != nullptr;
+  constexpr bool SIDE = SK != SIDE_NONE;
+  const bool has_pre = ACT != 0 && e.pre != nullptr;
 
   // ---- fragments and MFMAs (B fragment first: lane = row, registers = 4 consecutive columns)
   auto half = [&](int u, int h) -> const char* { return smem + (u & 1) * STAGE + h * HALF; };
@@ -253,6 +250,10 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
   // the segment (qm, i) adds (qm*128 + i*16) rows: one v_add of a wave-uniform constant
   auto seg_add = [&](int64_t ld, int es, int qm, int i) -> uint32_t { return (uint32_t)((qm * 128 + i * 16) * ld * es); };
   // One half of an item's epilogue: the 8 segments of quadrant row QM (acc[QM]).
+  // Lean per-segment work (the epilogue runs while the CU's MFMAs idle): the accumulator
+  // swap, bias (zeros when absent), the compile-time side operand / activation, the store.
+  // Out-of-range rows / columns keep the OOR offset (+ a segment offset < 2^26 stays past
+  // every descriptor range), so there is no per-segment select.
   auto epi_body = [&](const Item& c, int j, const SideSeg<OutT> (&side)[2][2][4], float (&cs)[2][8],
                       auto qmc) -> int {
     constexpr int QM = decltype(qmc)::value;
@@ -266,21 +267,13 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
         bias[qn][0] = *(const f32x4*)(slot + qn * 32 + qq * 8);
         bias[qn][1] = *(const f32x4*)(slot + qn * 32 + qq * 8 + 4);
       }
+    } else {
+#pragma unroll
+      for (int qn = 0; qn < 2; ++qn) bias[qn][0] = bias[qn][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
     }
-    const __amdgpu_buffer_rsrc_t rsC = ws ? rsrc_of(ws, (int64_t)splits * M * N * 4) : rsrc_of(e.C, (int64_t)M * e.ldc * ESZ);
-    const __amdgpu_buffer_rsrc_t rsPre = rsrc_of(e.pre, (int64_t)M * e.ldp * ESZ);
-    // split-K slab rows: split * M + m of [splits * M][N] fp32 (rows past M must not land in
-    // the next split's slab: OOR)
-    const int64_t ldo = ws ? N : e.ldc;
-    const int eso = ws ? 4 : ESZ;
-    uint32_t o0 = lane_off(ldo, eso, 0), o1 = lane_off(ldo, eso, 1);
-    if (ws) {
-      const uint32_t sl = (uint32_t)((int64_t)(c.kb / nk) * M * N * 4);
-      o0 = o0 == OOR ? OOR : o0 + sl;
-      o1 = o1 == OOR ? OOR : o1 + sl;
-    }
-    const uint32_t p0 = has_pre ? lane_off(e.ldp, ESZ, 0) : 0u, p1 = has_pre ? lane_off(e.ldp, ESZ, 1) : 0u;
-    const bool unit_alpha = e.alpha == 1.0f;
+    const __amdgpu_buffer_rsrc_t rsC = rsrc_of(e.C, (int64_t)M * e.ldc * ESZ);
+    const uint32_t o0 = lane_off(e.ldc, ESZ, 0), o1 = lane_off(e.ldc, ESZ, 1);
+    const uint32_t p0 = has_pre ? lane_off(e.ldp, ESZ, 0) : OOR, p1 = has_pre ? lane_off(e.ldp, ESZ, 1) : OOR;
     // one 16-row x 32-column segment (qm, qn, i), unrolled by hand (the 16 bodies exceed the
     // unroller's budget, and a rolled loop would index the accumulators dynamically)
     auto segment = [&](auto qmc2, auto qnc, auto ic) {
@@ -295,37 +288,20 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
         const float x = acc[qm][qn][i][0][r], y = acc[qm][qn][i][1][r];
         const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
         const unsigned sx = sw[0], sy = sw[1];
-        v[r] = __uint_as_float(sx);
-        v[4 + r] = __uint_as_float(sy);
-      }
-      const uint32_t ob = qn ? o1 : o0;
-      const bool row_ok = c.m0 + qm * 128 + i * 16 + lrow < M;  // (split slabs only: rows past M)
-      if (ws) {  // split-K slab: raw fp32 partial sums
-        store8(rsC, (row_ok && ob != OOR) ? ob + seg_add(N, 4, qm, i) : OOR, v, (float*)nullptr);
-        return;
-      }
-      if (!unit_alpha) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] *= e.alpha;
+        v[r] = __uint_as_float(sx) + bias[qn][0][r];
+        v[4 + r] = __uint_as_float(sy) + bias[qn][1][r];
       }
       const SideSeg<OutT>& sd = side[qm][qn][i];
-      if (SIDE && side_kind == SIDE_C) {
+      if constexpr (SK == SIDE_C) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] += e.beta * sd.get(k);
-      }
-      if (has_bias) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          v[k] += bias[qn][0][k];
-          v[4 + k] += bias[qn][1][k];
-        }
+        for (int k = 0; k < 8; ++k) v[k] = fmaf(e.beta, sd.get(k), v[k]);
       }
       float pre[8];
-      if (SIDE && side_kind == SIDE_AUX) {  // backward activation: aux holds act'(pre) (CAPK_ACT_DERIV)
+      if constexpr (SK == SIDE_AUX) {  // backward activation: aux holds act'(pre) (CAPK_ACT_DERIV)
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] *= sd.get(k);
       } else if constexpr (ACT != 0) {
-        if (e.act & CAPK_ACT_DERIV) {
+        if constexpr (DV) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) v[k] = act_fwd_grad_fast<OutT>(ACT, v[k], pre[k]);
         } else {
@@ -336,28 +312,23 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
           }
         }
       }
-      if (e.drop.on()) {
-        const int m = c.m0 + qm * 128 + i * 16 + lrow, n = c.n0 + qn * 128 + lcol;
-        const uint64_t base = (uint64_t)m * e.dropN + n;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] *= e.drop.mul(base + k);
-      }
-      if (SIDE && side_kind == SIDE_RES) {
+      if constexpr (SK == SIDE_RES) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] += sd.get(k);
       }
       if constexpr (DSUM) {  // rows past M hold bias / zero-operand values: not summed
+        const bool row_ok = c.m0 + qm * 128 + i * 16 + lrow < M;
 #pragma unroll
         for (int k = 0; k < 8; ++k) cs[qn][k] += row_ok ? v[k] : 0.f;
       }
 #if defined(CAPK_DIAG_NOSTORE)  // diagnostic build: the stores issue but are dropped (range check)
       store8(rsC, OOR, v, (OutT*)nullptr);
 #else
-      store8(rsC, ob == OOR ? OOR : ob + seg_add(e.ldc, ESZ, qm, i), v, (OutT*)nullptr);
+      store8(rsC, (qn ? o1 : o0) + seg_add(e.ldc, ESZ, qm, i), v, (OutT*)nullptr);
 #endif
-      if (ACT != 0 && has_pre) {
-        const uint32_t pb = qn ? p1 : p0;
-        store8(rsPre, pb == OOR ? OOR : pb + seg_add(e.ldp, ESZ, qm, i), pre, (OutT*)nullptr);
+      if constexpr (ACT != 0) {
+        const __amdgpu_buffer_rsrc_t rsPre = rsrc_of(e.pre, (int64_t)M * e.ldp * ESZ);
+        store8(rsPre, (qn ? p1 : p0) + seg_add(e.ldp, ESZ, qm, i), pre, (OutT*)nullptr);
       }
     };
 #define CAPK_SEG(QN, I) \
@@ -366,9 +337,9 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     CAPK_SEG(1, 0) CAPK_SEG(1, 1) CAPK_SEG(1, 2) CAPK_SEG(1, 3)
 #undef CAPK_SEG
     // memory instructions issued after the last wait (the stores): per segment one (bf16) or
-    // two (fp32) for C, the same again for the pre-activation
+    // two (fp32) for C, the same again for the pre-activation (dropped when not kept)
     constexpr int per = ESZ == 2 ? 1 : 2;
-    return ws ? 8 * 2 : 8 * per * ((ACT != 0 && has_pre) ? 2 : 1);
+    return 8 * per * (ACT != 0 ? 2 : 1);
   };
   // The item's epilogue, one quadrant row (half) at a time; a side operand (residual / aux /
   // C) is loaded per half, 8 segments in flight, one wait (the first also retires the next
@@ -391,7 +362,7 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     auto load_side = [&](auto qmc) {
       constexpr int QM = decltype(qmc)::value;
       if constexpr (SIDE && ESZ == 2) {
-        if (side_kind != SIDE_NONE) {
+        {
           const __amdgpu_buffer_rsrc_t rsSide = rsrc_of(e.side, (int64_t)M * e.lds * ESZ);
           const uint32_t s0 = this_lane_off(c, e.lds, ESZ, 0), s1 = this_lane_off(c, e.lds, ESZ, 1);
 #pragma unroll
@@ -443,7 +414,7 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
       }
       nd = 4;  // two 16-B stores per quadrant column
     }
-    return ((SIDE && ESZ == 2 && side_kind != SIDE_NONE) ? n1 : n0 + n1) + nd;
+    return ((SIDE && ESZ == 2) ? n1 : n0 + n1) + nd;
   };
 
   // ---- main loop: gemm8p's two phases per K-tile over the continuous step sequence ----
@@ -541,13 +512,13 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
 bool gemm8q_supports(const Epi& e, bool out_f32) {
   const int sides = ((e.act & CAPK_ACT_BWD) ? 1 : 0) + (e.res ? 1 : 0) + (e.beta != 0.f ? 1 : 0);
   const int a = e.act & 15;
-  if (a && !(e.act & CAPK_ACT_BWD) && a != CAPK_ACT_GELU_ERF && a != CAPK_ACT_GELU_TANH && a != CAPK_ACT_QUICK_GELU &&
-      a != CAPK_ACT_RELU)
+  const bool fwd_act = a && !(e.act & CAPK_ACT_BWD);
+  if (e.alpha != 1.0f || e.drop.thr != 0) return false;  // (dropout: gemm8p)
+  if (fwd_act && a != CAPK_ACT_GELU_ERF && a != CAPK_ACT_GELU_TANH && a != CAPK_ACT_QUICK_GELU && a != CAPK_ACT_RELU)
     return false;  // (tanh / sigmoid epilogues: pooler-sized products, the 8p kernel)
-  // backward activations only in the multiply-by-aux form (CAPK_ACT_DERIV: aux = act'(pre))
-  // (fp32 outputs take no side operand and no activation here: 16 segments of 8 fp32 would
-  // need 128 VGPRs)
-  if (out_f32 && (a && !(e.act & CAPK_ACT_BWD))) return false;
+  if (fwd_act && (sides || out_f32)) return false;
+  // backward activations only in the multiply-by-aux form (CAPK_ACT_DERIV: aux = act'(pre));
+  // fp32 outputs take no side operand (16 segments of 8 fp32 would need 128 VGPRs)
   return sides <= (out_f32 ? 0 : 1) && (!(e.act & CAPK_ACT_BWD) || (e.act & CAPK_ACT_DERIV));
 }
 
@@ -556,83 +527,81 @@ int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int
   CAPK_CHECK_ARG((a_kmajor ? (int64_t)M * lda : (int64_t)K * lda) * 2 < (1ll << 31) &&
                      (b_kmajor ? (int64_t)N * ldb : (int64_t)K * ldb) * 2 < (1ll << 31),
                  "capk_gemm(bf16, 256x256): operand larger than 2 GiB");
-  CAPK_CHECK_ARG(gemm8q_supports(e, out_f32), "capk_gemm(gemm8q): unsupported epilogue");
+  CAPK_CHECK_ARG(gemm8q_supports(e, out_f32) && splits == 1 && !slab, "capk_gemm(gemm8q): unsupported epilogue");
   const int64_t esz = out_f32 ? 4 : 2;
   Epi8q p{};
   p.C = e.C;
   p.ldc = e.ldc;
-  p.alpha = e.alpha;
   p.beta = e.beta;
   p.bias = e.bias;
-  p.act = e.act;
-  p.drop = e.drop;
-  p.dropN = e.N;
-  const bool fwd_act = (e.act & 15) && !(e.act & CAPK_ACT_BWD);
-  if (fwd_act && e.pre) {
+  const int a = e.act & 15;
+  const bool fwd_act = a && !(e.act & CAPK_ACT_BWD);
+  const bool dv = fwd_act && (e.act & CAPK_ACT_DERIV);
+  if (fwd_act) {
     p.pre = e.pre;
     p.ldp = e.ldx;
   }
+  int sk = SIDE_NONE;
   if (e.act & CAPK_ACT_BWD) {
-    p.side_kind = SIDE_AUX;
+    sk = SIDE_AUX;
     p.side = e.aux;
     p.lds = e.ldx;
   } else if (e.res) {
-    p.side_kind = SIDE_RES;
+    sk = SIDE_RES;
     p.side = e.res;
     p.lds = e.ldr;
   } else if (e.beta != 0.f) {
-    p.side_kind = SIDE_C;
+    sk = SIDE_C;
     p.side = e.C;
     p.lds = e.ldc;
   }
-  CAPK_CHECK_ARG((slab ? (int64_t)splits * M * N * 4 : (int64_t)M * e.ldc * esz) < (1ll << 31) &&
-                     (!p.pre || (int64_t)M * p.ldp * esz < (1ll << 31)) &&
+  CAPK_CHECK_ARG((int64_t)M * e.ldc * esz < (1ll << 31) && (!p.pre || (int64_t)M * p.ldp * esz < (1ll << 31)) &&
                      (!p.side || (int64_t)M * p.lds * esz < (1ll << 31)),
                  "capk_gemm(bf16, 256x256): output or side operand larger than 2 GiB");
-  const int items = cdiv(M, 256) * cdiv(N, 256) * splits;
+  const int items = cdiv(M, 256) * cdiv(N, 256);
   CAPK_CHECK_ARG(items > 256, "capk_gemm(gemm8q): persistent kernel for grids of more than 256 items");
-  const int grid = 256;
-#define L8(AK, BKM, OT, ACTK, SD)                                                                                 \
-  hipLaunchKernelGGL((gemm8q_kernel<AK, BKM, OT, ACTK, SD>), dim3(grid), dim3(512), 0, st, A, lda, B, ldb, M, N, K, \
-                     splits, p, slab)
-#define L8S(AK, BKM, OT, ACTK)          \
-  if (side) L8(AK, BKM, OT, ACTK, true); \
-  else L8(AK, BKM, OT, ACTK, false);
-#define L8D(OT)                                                                    \
-  if (a_kmajor && b_kmajor) {                                                       \
-    switch (fwd_act && !slab ? (e.act & 15) : 0) {                                  \
-      case CAPK_ACT_GELU_ERF: L8S(true, true, OT, CAPK_ACT_GELU_ERF) break;         \
-      case CAPK_ACT_GELU_TANH: L8S(true, true, OT, CAPK_ACT_GELU_TANH) break;       \
-      case CAPK_ACT_QUICK_GELU: L8S(true, true, OT, CAPK_ACT_QUICK_GELU) break;     \
-      case CAPK_ACT_RELU: L8S(true, true, OT, CAPK_ACT_RELU) break;                 \
-      default: L8S(true, true, OT, 0) break;                                        \
-    }                                                                               \
-  } else if (a_kmajor) {                                                            \
-    L8S(true, false, OT, 0)                                                         \
-  } else if (b_kmajor) {                                                            \
-    L8S(false, true, OT, 0)                                                         \
-  } else {                                                                          \
-    L8S(false, false, OT, 0)                                                        \
+  CAPK_CHECK_ARG(!fwd_act || (a_kmajor && b_kmajor), "capk_gemm(gemm8q): forward activations need K-major operands");
+  const dim3 grid(256), block(512);
+#define L8(AK, BKM, OT, ACTK, DVK, SKK, DS) \
+  hipLaunchKernelGGL((gemm8q_kernel<AK, BKM, OT, ACTK, DVK, SKK, DS>), grid, block, 0, st, A, lda, B, ldb, M, N, K, 1, p)
+#define L8SK(AK, BKM)                                      \
+  switch (sk) {                                            \
+    case SIDE_AUX: L8(AK, BKM, bf16, 0, false, SIDE_AUX, false); break; \
+    case SIDE_RES: L8(AK, BKM, bf16, 0, false, SIDE_RES, false); break; \
+    case SIDE_C: L8(AK, BKM, bf16, 0, false, SIDE_C, false); break;     \
+    default: L8(AK, BKM, bf16, 0, false, SIDE_NONE, false); break;      \
   }
-  CAPK_CHECK_ARG(!fwd_act || slab || (a_kmajor && b_kmajor), "capk_gemm(gemm8q): forward activations need K-major operands");
-  const bool side = !slab && p.side_kind != SIDE_NONE;
+#define L8ACT(ACTK)                                        \
+  if (dv) L8(true, true, bf16, ACTK, true, SIDE_NONE, false); \
+  else L8(true, true, bf16, ACTK, false, SIDE_NONE, false);
   if (dsum) {  // dX with the backward-activation multiply + column sums (capk_gemm_dx_act_colsum)
-    CAPK_CHECK_ARG(a_kmajor && !b_kmajor && !out_f32 && side && p.side_kind == SIDE_AUX,
+    CAPK_CHECK_ARG(a_kmajor && !b_kmajor && !out_f32 && sk == SIDE_AUX,
                    "capk_gemm(gemm8q): column sums only on the dX x act' product");
     p.dsum = dsum;
-    hipLaunchKernelGGL((gemm8q_kernel<true, false, bf16, 0, true, true>), dim3(grid), dim3(512), 0, st, A, lda, B, ldb,
-                       M, N, K, splits, p, slab);
-  } else if (out_f32) {
-    // fp32 outputs: no activation, no side operand (gemm8q_supports)
-    if (a_kmajor && b_kmajor) L8(true, true, float, 0, false);
-    else if (a_kmajor) L8(true, false, float, 0, false);
-    else if (b_kmajor) L8(false, true, float, 0, false);
-    else L8(false, false, float, 0, false);
+    L8(true, false, bf16, 0, false, SIDE_AUX, true);
+  } else if (out_f32) {  // fp32 outputs: no activation, no side operand (gemm8q_supports)
+    if (a_kmajor && b_kmajor) L8(true, true, float, 0, false, SIDE_NONE, false);
+    else if (a_kmajor) L8(true, false, float, 0, false, SIDE_NONE, false);
+    else if (b_kmajor) L8(false, true, float, 0, false, SIDE_NONE, false);
+    else L8(false, false, float, 0, false, SIDE_NONE, false);
+  } else if (fwd_act) {
+    switch (a) {
+      case CAPK_ACT_GELU_ERF: L8ACT(CAPK_ACT_GELU_ERF) break;
+      case CAPK_ACT_GELU_TANH: L8ACT(CAPK_ACT_GELU_TANH) break;
+      case CAPK_ACT_QUICK_GELU: L8ACT(CAPK_ACT_QUICK_GELU) break;
+      default: L8ACT(CAPK_ACT_RELU) break;
+    }
+  } else if (a_kmajor && b_kmajor) {
+    L8SK(true, true)
+  } else if (a_kmajor) {
+    L8SK(true, false)
+  } else if (b_kmajor) {
+    L8SK(false, true)
   } else {
-    L8D(bf16)
+    L8SK(false, false)
   }
-#undef L8D
-#undef L8S
+#undef L8ACT
+#undef L8SK
 #undef L8
   CAPK_LAUNCH_CHECK("gemm8q_kernel");
   return CAPK_OK;
