@@ -514,8 +514,9 @@ def main():
     ap.add_argument("--beam-batch", type=int, default=256, help="images per beam-5 batch (0 = skip)")
     ap.add_argument("--beam-reps", type=int, default=3)
     ap.add_argument("--cpu-beam-images", type=int, default=24)
-    ap.add_argument("--grad-exchange", choices=["fp32", "bf16"], default="bf16",
-                    help="DP gradient all-reduce precision (fp32 master weights either way)")
+    ap.add_argument("--grad-exchange", choices=["fp32", "bf16"], default="fp32",
+                    help="DP gradient all-reduce precision (fp32 master weights either way); fp32 = the "
+                         "reference's gradient average exactly, bf16 halves the bytes on xGMI")
     ap.add_argument("--workload", choices=["config3", "config2", "config5"], default="config3",
                     help="config3 (headline: ViT+Transformer CE), config2 (ResNet-101+LSTM CE, bs 128) or "
                          "config5 (CLIP+GPT-2 SCST, fp8)")
