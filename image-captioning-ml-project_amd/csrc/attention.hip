@@ -512,35 +512,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
   float* lse_s = (float*)(dOs + NQP * ST);
   float* del_s = lse_s + NQP;
   const int hoff = h * a.hd;
-  {
-    const StageSrc S[2] = {{Qs, (const bf16*)a.q + (int64_t)b * a.q_bs + hoff, a.q_rs, a.Nq, NQP},
-                           {dOs, (const bf16*)a.dout + (int64_t)b * a.do_bs + hoff, a.do_rs, a.Nq, NQP}};
-    stage_images<HDP, 2, 512, SW>(S, a.hd);
-  }
-  for (int q = threadIdx.x; q < NQP; q += blockDim.x)
-    lse_s[q] = q < a.Nq ? a.lse_in[((int64_t)b * a.H + h) * a.Nq + q] * kLog2e : 0.f;  // log2 domain
-  __syncthreads();
-  // delta_q = sum_d O * dO: 8 lanes per query (chunks c8, c8 + 8, ...), xor-shuffle reduced.
-  // NQP * 8 is a multiple of 64, so every wave runs whole iterations (shuffles see all lanes).
-  for (int idx = threadIdx.x; idx < NQP * 8; idx += blockDim.x) {
-    const int q = idx >> 3, c8 = idx & 7;
-    float s = 0.f;
-#pragma unroll
-    for (int c = c8; c < NCH; c += 8) {
-      if (q < a.Nq && c * 8 < a.hd) {
-        const bf16x8 ov = ld8((const bf16*)a.o + (int64_t)b * a.o_bs + (int64_t)q * a.o_rs + hoff + c * 8);
-        const bf16x8 dv = *(const bf16x8*)(dOs + (SW ? swz_off(q, c * 8) : q * ST + c * 8));
-#pragma unroll
-        for (int i = 0; i < 8; ++i) s += (float)ov[i] * (float)dv[i];
-      }
-    }
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    s += __shfl_xor(s, 4, 64);
-    if (c8 == 0) del_s[q] = s;
-  }
-  __syncthreads();
-  const float sl2 = a.scale * kLog2e;
   const bf16* kbase = (const bf16*)a.k + (int64_t)b * a.k_bs + hoff;
   const bf16* vbase = (const bf16*)a.v + (int64_t)b * a.v_bs + hoff;
   // the wave's own K / V rows; the next key block's are loaded while this one computes
@@ -554,8 +525,53 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
       vf[s] = in ? ld8(vbase + (int64_t)keyl * a.v_rs + d) : zero8();
     }
   };
+  // Prologue: every global load of the workgroup's set-up -- the first key block's K / V
+  // rows, lse, the O chunks of delta and the Q / dO staging -- is issued before the first
+  // wait, so the workgroup pays one memory round trip instead of three (stage, then O,
+  // then K / V).  8 lanes per query for delta (chunks c8, c8 + 8, ...); NQP * 8 is a
+  // multiple of 64, so every wave runs whole iterations (shuffles see all lanes).
   bf16x8 kf[HDP / 32], vf[HDP / 32];
   if (wave < NKP / 16) load_rows(wave, kf, vf);
+  const float lse_r = threadIdx.x < a.Nq ? a.lse_in[((int64_t)b * a.H + h) * a.Nq + threadIdx.x] * kLog2e : 0.f;
+  constexpr int DIT = (256 * 8 + 511) / 512, DCH = (NCH + 7) / 8;  // NQP <= 256, blockDim 512
+  bf16x8 ov[DIT][DCH];
+#pragma unroll
+  for (int it = 0; it < DIT; ++it)
+#pragma unroll
+    for (int j = 0; j < DCH; ++j) {
+      const int idx = threadIdx.x + it * 512, q = idx >> 3, c = (idx & 7) + 8 * j;
+      ov[it][j] = (q < a.Nq && c < NCH && c * 8 < a.hd)
+                      ? ld8((const bf16*)a.o + (int64_t)b * a.o_bs + (int64_t)q * a.o_rs + hoff + c * 8)
+                      : zero8();
+    }
+  {
+    const StageSrc S[2] = {{Qs, (const bf16*)a.q + (int64_t)b * a.q_bs + hoff, a.q_rs, a.Nq, NQP},
+                           {dOs, (const bf16*)a.dout + (int64_t)b * a.do_bs + hoff, a.do_rs, a.Nq, NQP}};
+    stage_images<HDP, 2, 512, SW>(S, a.hd);
+  }
+  if (threadIdx.x < NQP) lse_s[threadIdx.x] = lse_r;  // log2 domain
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < DIT; ++it) {
+    const int idx = threadIdx.x + it * 512, q = idx >> 3;
+    if (it * 512 >= NQP * 8) break;  // uniform over the block
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < DCH; ++j) {
+      const int c = (idx & 7) + 8 * j;
+      if (q < NQP && c < NCH) {
+        const bf16x8 dv = *(const bf16x8*)(dOs + (SW ? swz_off(q, c * 8) : q * ST + c * 8));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s += (float)ov[it][j][i] * (float)dv[i];
+      }
+    }
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    if ((idx & 7) == 0 && q < NQP) del_s[q] = s;
+  }
+  __syncthreads();
+  const float sl2 = a.scale * kLog2e;
   for (int kb = wave; kb < NKP / 16; kb += nwaves) {
     const int keyl = kb * 16 + (lane & 15);
     bf16x8 kn[HDP / 32], vn[HDP / 32];
@@ -629,6 +645,34 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HDP == 64 ?
   bf16* Ks = (bf16*)smem;
   bf16* Vs = Ks + NKP * ST;
   const int hoff = h * a.hd;
+  const bf16* qbase = (const bf16*)a.q + (int64_t)b * a.q_bs + hoff;
+  const bf16* dobase = (const bf16*)a.dout + (int64_t)b * a.do_bs + hoff;
+  const bf16* obase = (const bf16*)a.o + (int64_t)b * a.o_bs + hoff;
+  // the wave's query block operands: Q, dO, O rows (fragment layout) and lse
+  bf16x8 qf[HDP / 32], dof[HDP / 32], of[HDP / 32];
+  float lq = 0.f;
+  auto load_q = [&](int qb) {
+    const int ql = qb * 16 + (lane & 15);
+#pragma unroll
+    for (int s = 0; s < HDP / 32; ++s) {
+      const int d = s * 32 + 8 * (lane >> 4);
+      const bool in = ql < a.Nq && d < a.hd;
+      qf[s] = in ? ld8(qbase + (int64_t)ql * a.q_rs + d) : zero8();
+      dof[s] = in ? ld8(dobase + (int64_t)ql * a.do_rs + d) : zero8();
+    }
+    lq = ql < a.Nq ? a.lse_in[((int64_t)b * a.H + h) * a.Nq + ql] * kLog2e : 0.f;
+  };
+  auto load_o = [&](int qb) {
+    const int ql = qb * 16 + (lane & 15);
+#pragma unroll
+    for (int s = 0; s < HDP / 32; ++s) {
+      const int d = s * 32 + 8 * (lane >> 4);
+      of[s] = ql < a.Nq && d < a.hd ? ld8(obase + (int64_t)ql * a.o_rs + d) : zero8();
+    }
+  };
+  // the first block's Q / dO / lse are requested before the K / V staging (O after it:
+  // holding O across the staging loads spills at the 80-VGPR budget of three WGs per CU)
+  if (wave < NQP / 16) load_q(wave);
   {
     const StageSrc S[2] = {{Ks, (const bf16*)a.k + (int64_t)b * a.k_bs + hoff, a.k_rs, a.Nk, NKP},
                            {Vs, (const bf16*)a.v + (int64_t)b * a.v_bs + hoff, a.v_rs, a.Nk, NKP}};
@@ -636,26 +680,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HDP == 64 ?
   }
   __syncthreads();
   const float sl2 = a.scale * kLog2e;
-  const bf16* qbase = (const bf16*)a.q + (int64_t)b * a.q_bs + hoff;
-  const bf16* dobase = (const bf16*)a.dout + (int64_t)b * a.do_bs + hoff;
-  const bf16* obase = (const bf16*)a.o + (int64_t)b * a.o_bs + hoff;
   for (int qb = wave; qb < NQP / 16; qb += nwaves) {
     const int ql = qb * 16 + (lane & 15);
-    bf16x8 qf[HDP / 32], dof[HDP / 32];
+    if (qb != wave) load_q(qb);
+    load_o(qb);
     float dd = 0.f;  // delta_q = sum_d dO * O, this lane's 8-dim chunks, then over the lane group
 #pragma unroll
-    for (int s = 0; s < HDP / 32; ++s) {
-      const int d = s * 32 + 8 * (lane >> 4);
-      const bool in = ql < a.Nq && d < a.hd;
-      qf[s] = in ? ld8(qbase + (int64_t)ql * a.q_rs + d) : zero8();
-      dof[s] = in ? ld8(dobase + (int64_t)ql * a.do_rs + d) : zero8();
-      const bf16x8 ov = in ? ld8(obase + (int64_t)ql * a.o_rs + d) : zero8();
+    for (int s = 0; s < HDP / 32; ++s)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) dd += (float)ov[i] * (float)dof[s][i];
-    }
+      for (int i = 0; i < 8; ++i) dd += (float)of[s][i] * (float)dof[s][i];
     dd += __shfl_xor(dd, 16, 64);
     dd += __shfl_xor(dd, 32, 64);
-    const float lq = ql < a.Nq ? a.lse_in[((int64_t)b * a.H + h) * a.Nq + ql] * kLog2e : 0.f;
     f32x4 dqt[HDP / 16];
 #pragma unroll
     for (int db = 0; db < HDP / 16; ++db) dqt[db] = (f32x4){0.f, 0.f, 0.f, 0.f};

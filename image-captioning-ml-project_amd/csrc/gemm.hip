@@ -331,16 +331,19 @@ static int choose_cfg(int M, int N, int K, int a_kmajor, int b_kmajor, int act) 
     const char* v = getenv("CAPK_GEMM_8Q");
     return v && v[0] == '0' ? 5 : 6;
   }();
+  // One-round grids of K-major operands (the config-3 decoder's 5120-row QKV / FC1 / FC2-dX
+  // products, 180-240 tiles) measured 30-35 % faster on the 128x64 BK-64 ring than on the
+  // 256x256 kernel, with or without an activation epilogue, and the 3-WG/CU BK-32 ring lost
+  // to it on every activation shape (profiles/round3/decoder_gemm_cfgs.txt); small split-K
+  // weight gradients (a 768 x 768 tile grid x 16 splits) likewise.
   if (M >= 256 && N >= 256) {
     const int t5 = tiles_of(5, M, N);
     if (!a_kmajor && !b_kmajor) {
-      if (t5 * choose_splits(5, M, N, K) >= 128) return big;
-    } else if (t5 >= 160) {
+      if (t5 * choose_splits(5, M, N, K) >= 192) return big;
+    } else if (t5 > 256) {
       return big;
     }
   }
-  // (decode-step rows, M < 2048: the 2-WG/CU BK-64 ring measured faster with an activation too)
-  if (act && (a_kmajor || b_kmajor) && K % 32 == 0 && M >= 2048) return 4;
   if (!a_kmajor && !b_kmajor && tiles_of(4, M, N) < slots_of(4)) return 1;  // split-K dW (cfg 4 measured slower)
   return 1;
 }

@@ -186,6 +186,115 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int cols, const T
   }
 }
 
+// bf16 rows of exactly 768 (ViT-B, the config-3 decoder, GPT-2, CLIP): 4-element (8-B)
+// segments, three per lane, so every lane is busy (the 8-element kernel above leaves half
+// the lanes idle on its second segment), with TWO rows of operands in flight per wave (rows
+// r + stride, r + 2 stride requested while row r reduces): 72 KiB in flight per CU.  Measured 81 us on the ViT LN backward before (3.8 TB/s,
+// 36 KiB in flight per CU); the dependency on HBM latency is what the deeper queue removes.
+template <bool SUM>
+__global__ __launch_bounds__(256) void ln_bwd768_kernel(int rows, const bf16* __restrict__ dy, int64_t lddy,
+                                                        const bf16* __restrict__ x, int64_t ldx,
+                                                        const float* __restrict__ w, const float* __restrict__ mean,
+                                                        const float* __restrict__ rstd, bf16* __restrict__ dx,
+                                                        int64_t lddx, const bf16* __restrict__ dres, int64_t ldres,
+                                                        float* __restrict__ part, Drop drop, bf16* __restrict__ dxd,
+                                                        int64_t lddxd) {
+  constexpr int COLS = 768, NC = 3, NP = SUM ? 3 : 2;
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [4 waves][NP][COLS]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float dw[NC][4], db[NC][4], ds[SUM ? NC : 1][4], wv[NC][4];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const f32x4 t = *(const f32x4*)(w + (lane + 64 * c) * 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      wv[c][i] = t[i];
+      dw[c][i] = db[c][i] = 0.f;
+      if constexpr (SUM) ds[c][i] = 0.f;
+    }
+  }
+  struct Row { bf16x4 x[NC], d[NC], r[NC]; };
+  auto fetch = [&](int row, Row& R) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int col = (lane + 64 * c) * 4;
+      R.x[c] = *(const bf16x4*)(x + (int64_t)row * ldx + col);
+      R.d[c] = *(const bf16x4*)(dy + (int64_t)row * lddy + col);
+      if (dres) R.r[c] = *(const bf16x4*)(dres + (int64_t)row * ldres + col);
+    }
+  };
+  // one row: statistics from R, then R is refilled with row `nxt` (its loads overlap this
+  // row's reductions and stores), then dx
+  auto step = [&](Row& R, int row, int nxt) {
+    const float mu = mean[row], rs = rstd[row];
+    float xh[NC][4], g[NC][4], r[NC][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float d = (float)R.d[c][i];
+        xh[c][i] = ((float)R.x[c][i] - mu) * rs;
+        g[c][i] = d * wv[c][i];
+        r[c][i] = dres ? (float)R.r[c][i] : 0.f;
+        s1 += g[c][i];
+        s2 += g[c][i] * xh[c][i];
+        dw[c][i] += d * xh[c][i];
+        db[c][i] += d;
+      }
+    if (nxt < rows) fetch(nxt, R);
+    const float m1 = wave_sum(s1) * (1.f / COLS), m2 = wave_sum(s2) * (1.f / COLS);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int col = (lane + 64 * c) * 4;
+      float o[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = rs * (g[c][i] - m1 - xh[c][i] * m2);
+      if (dxd) {
+        bf16x4 od;
+        const uint64_t base = (uint64_t)row * COLS + col;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) od[i] = (bf16)(o[i] * drop.mul(base + i));
+        *(bf16x4*)(dxd + (int64_t)row * lddxd + col) = od;
+      }
+      bf16x4 ob;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        o[i] += r[c][i];
+        if constexpr (SUM) ds[c][i] += o[i];
+        ob[i] = (bf16)o[i];
+      }
+      *(bf16x4*)(dx + (int64_t)row * lddx + col) = ob;
+    }
+  };
+  // two row buffers in flight, alternating (no register copies between them: a copy would
+  // wait for the younger buffer's loads)
+  const int stride = gridDim.x * 4;
+  Row A, B;
+  int row = blockIdx.x * 4 + wave;
+  if (row < rows) fetch(row, A);
+  if (row + stride < rows) fetch(row + stride, B);
+  for (; row < rows; row += 2 * stride) {
+    step(A, row, row + 2 * stride);
+    if (row + stride < rows) step(B, row + stride, row + 3 * stride);
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int col = (lane + 64 * c) * 4;
+    *(f32x4*)(red + (wave * NP + 0) * COLS + col) = (f32x4){dw[c][0], dw[c][1], dw[c][2], dw[c][3]};
+    *(f32x4*)(red + (wave * NP + 1) * COLS + col) = (f32x4){db[c][0], db[c][1], db[c][2], db[c][3]};
+    if constexpr (SUM) *(f32x4*)(red + (wave * NP + 2) * COLS + col) = (f32x4){ds[c][0], ds[c][1], ds[c][2], ds[c][3]};
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < NP * COLS; i += 256) {
+    const int which = i / COLS, col = i % COLS;
+    float s = 0.f;
+#pragma unroll
+    for (int wv2 = 0; wv2 < 4; ++wv2) s += red[(wv2 * NP + which) * COLS + col];
+    part[(int64_t)blockIdx.x * NP * COLS + i] = s;
+  }
+}
+
 // sum the per-block partials [nblocks][2*cols] (sum_parts / finish_parts16, common.h)
 __global__ __launch_bounds__(1024) void ln_bwd_finish_kernel(int nblocks, int cols, int np,
                                                              const float* __restrict__ part, float* __restrict__ dw,
@@ -201,6 +310,10 @@ __global__ __launch_bounds__(1024) void ln_bwd_finish_kernel(int nblocks, int co
 
 // (the pipelined kernel holds ~200 VGPRs: 2 waves per SIMD, so 512 blocks are all resident)
 static int ln_bwd_blocks(int rows) { return std::max(1, std::min(512, (rows + 15) / 16)); }
+// ln_bwd768_kernel: 189 VGPRs (two waves per SIMD; held to 168 for three it spills) -> 512
+// resident blocks, each wave with two rows in flight
+static int ln_bwd768_blocks(int rows) { return std::max(1, std::min(512, (rows + 15) / 16)); }
+static bool use768(int dtype, int cols) { return dtype == CAPK_BF16 && cols == 768; }
 
 }  // namespace capk
 
@@ -223,7 +336,7 @@ extern "C" int capk_layernorm_fwd(int dtype, int rows, int cols, const void* x, 
 }
 
 extern "C" size_t capk_layernorm_bwd_workspace(int rows, int cols) {
-  return (size_t)ln_bwd_blocks(rows) * 3 * cols * sizeof(float);
+  return (size_t)std::max(ln_bwd_blocks(rows), cols == 768 ? ln_bwd768_blocks(rows) : 0) * 3 * cols * sizeof(float);
 }
 
 extern "C" int capk_layernorm_bwd(int dtype, int rows, int cols, const void* dy, int64_t lddy, const void* x,
@@ -232,7 +345,9 @@ extern "C" int capk_layernorm_bwd(int dtype, int rows, int cols, const void* dy,
                                   float* dsum, int accumulate, float drop_p, uint32_t drop_seed, void* dx_drop,
                                   int64_t lddx_drop, void* ws, size_t ws_bytes, void* stream) {
   CAPK_CHECK_ARG(rows > 0 && cols > 0 && cols % 8 == 0 && cols <= 2048, "capk_layernorm_bwd: cols=%d", cols);
-  const int nb = ln_bwd_blocks(rows);
+  const bool v768 = use768(dtype, cols) && ldx % 4 == 0 && lddy % 4 == 0 && lddx % 4 == 0 &&
+                    (!dres || ldres % 4 == 0) && (!dx_drop || lddx_drop % 4 == 0);
+  const int nb = v768 ? ln_bwd768_blocks(rows) : ln_bwd_blocks(rows);
   const int np = dsum ? 3 : 2;
   CAPK_CHECK_ARG(ws && ws_bytes >= (size_t)nb * np * cols * sizeof(float), "capk_layernorm_bwd: workspace too small");
   hipStream_t st = S(stream);
@@ -243,11 +358,17 @@ extern "C" int capk_layernorm_bwd(int dtype, int rows, int cols, const void* dy,
                      make_drop(drop_p, drop_seed), (T*)dx_drop, lddx_drop)
 #define LS(T, MC) \
   if (dsum) L(T, MC, true); else L(T, MC, false);
-  if (dtype == CAPK_BF16) { if (cols <= 1024) { LS(bf16, 2) } else { LS(bf16, 4) } }
+#define L768(SM)                                                                                                \
+  hipLaunchKernelGGL((ln_bwd768_kernel<SM>), dim3(nb), dim3(256), shm, st, rows, (const bf16*)dy, lddy,          \
+                     (const bf16*)x, ldx, w, mean, rstd, (bf16*)dx, lddx, (const bf16*)dres, ldres, (float*)ws,    \
+                     make_drop(drop_p, drop_seed), (bf16*)dx_drop, lddx_drop)
+  if (v768) { if (dsum) L768(true); else L768(false); }
+  else if (dtype == CAPK_BF16) { if (cols <= 1024) { LS(bf16, 2) } else { LS(bf16, 4) } }
   else if (dtype == CAPK_F32) { if (cols <= 1024) { LS(float, 2) } else { LS(float, 4) } }
   else { set_error("capk_layernorm_bwd: dtype"); return CAPK_EINVAL; }
 #undef LS
 #undef L
+#undef L768
   CAPK_LAUNCH_CHECK("ln_bwd_kernel");
   hipLaunchKernelGGL(ln_bwd_finish_kernel, dim3(cdiv(np * cols, 16)), dim3(1024), 0, st, nb, cols, np,
                      (const float*)ws, dw, db, dsum, accumulate);

@@ -37,6 +37,12 @@ SHAPES = [  # name, M, N, K, kind
     ("dec1280_fc", 1280, 3072, 768, "c1d_gelu"), ("dec1280_proj2", 1280, 768, 3072, "c1d"),
     ("tdec1280_qkv", 1280, 2304, 768, "fwd"), ("tdec1280_fc1", 1280, 3072, 768, "fwd_gelu"),
     ("tdec1280_fc2", 1280, 768, 3072, "fwd"),
+    # config-3 decoder train shapes (rows B*T = 5120, 8 heads x 96): the N = 768 products
+    ("dec_o_fwd", 5120, 768, 768, "fwd"), ("dec_fc2_fwd", 5120, 768, 3072, "fwd"),
+    ("dec_o_dx", 5120, 768, 768, "dx"), ("dec_qkv_dx", 5120, 768, 2304, "dx"),
+    ("dec_fc1_dx", 5120, 768, 3072, "dx"), ("dec_qkv_fwd", 5120, 2304, 768, "fwd"),
+    ("dec_fc1_fwd_deriv", 5120, 3072, 768, "fwd_gelu_deriv"), ("dec_fc2_dx_deriv", 5120, 3072, 768, "dx_gelu_deriv"),
+    ("dec_o_dw", 5120, 768, 768, "dw"), ("dec_fc1_dw", 5120, 3072, 768, "dw"),
 ]
 
 
