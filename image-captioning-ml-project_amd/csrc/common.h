@@ -203,6 +203,36 @@ __device__ __forceinline__ float act_grad_fast(int act, float x) {
   }
   return act_grad(act, x);
 }
+// Two elements at once on packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two lanes'
+// worth per issue) for the GEMM epilogues, where the GELU-family math runs while the CU's
+// MFMAs idle and its VALU issue count is the epilogue's time; the two transcendentals per
+// element stay scalar.  Same formulas as act_fwd_fast / act_fwd_grad_fast above (bf16 storage
+// only; the fp32 parity path never reaches these).
+__device__ __forceinline__ f32x2 fast_sig2(int act, f32x2 x, f32x2& zp) {
+  f32x2 t;
+  if (act == CAPK_ACT_QUICK_GELU) {
+    zp = (f32x2){1.702f, 1.702f};
+    t = x * (1.702f * kLog2eF);
+  } else {
+    const f32x2 u = x * x;
+    zp = u * (3.0f * kGeluC1) + kGeluC0;
+    t = x * (u * (kGeluC1 * kLog2eF) + kGeluC0 * kLog2eF);
+  }
+  f32x2 e = {__builtin_amdgcn_exp2f(-t[0]), __builtin_amdgcn_exp2f(-t[1])};
+  e = e + 1.0f;
+  return (f32x2){__builtin_amdgcn_rcpf(e[0]), __builtin_amdgcn_rcpf(e[1])};
+}
+__device__ __forceinline__ f32x2 act_fwd_fast2(int act, f32x2 x) {
+  f32x2 zp;
+  return x * fast_sig2(act, x, zp);
+}
+__device__ __forceinline__ f32x2 act_fwd_grad_fast2(int act, f32x2 x, f32x2& d) {
+  f32x2 zp;
+  const f32x2 s = fast_sig2(act, x, zp);
+  d = (x * (s - s * s)) * zp + s;  // s + x s (1 - s) z'
+  return x * s;
+}
+
 // act(x) and act'(x) together (one logistic evaluation): CAPK_ACT_DERIV epilogues
 template <typename T>
 __device__ __forceinline__ float act_fwd_grad_fast(int act, float x, float& d) {

@@ -301,7 +301,22 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] *= sd.get(k);
       } else if constexpr (ACT != 0) {
-        if constexpr (DV) {
+        constexpr bool PK = std::is_same<OutT, bf16>::value &&
+                            (ACT == CAPK_ACT_GELU_ERF || ACT == CAPK_ACT_GELU_TANH || ACT == CAPK_ACT_QUICK_GELU);
+        if constexpr (PK) {  // packed fp32 pairs (common.h act_*_fast2)
+#pragma unroll
+          for (int k = 0; k < 8; k += 2) {
+            const f32x2 x = {v[k], v[k + 1]};
+            f32x2 y, d;
+            if constexpr (DV) y = act_fwd_grad_fast2(ACT, x, d);
+            else {
+              d = x;
+              y = act_fwd_fast2(ACT, x);
+            }
+            v[k] = y[0]; v[k + 1] = y[1];
+            pre[k] = d[0]; pre[k + 1] = d[1];
+          }
+        } else if constexpr (DV) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) v[k] = act_fwd_grad_fast<OutT>(ACT, v[k], pre[k]);
         } else {
@@ -358,24 +373,31 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
           for (int jj = 0; jj < 2; ++jj) asm volatile("" ::"v"(acc[a][b][i][jj]));
     return 0;
 #endif
+    // Both halves' side segments are requested at once (the A / B fragment registers of the
+    // main loop are dead here): the second half's loads fly while the first half computes, so
+    // an item pays one side-operand round trip, not two.  Waits: vmcnt <= 8 leaves exactly
+    // the second half's 8 loads (the first) / the first half's 8 stores (the second) younger.
     SideSeg<OutT> side[2][2][4];
-    auto load_side = [&](auto qmc) {
+    auto issue_side = [&](auto qmc) {
       constexpr int QM = decltype(qmc)::value;
       if constexpr (SIDE && ESZ == 2) {
-        {
-          const __amdgpu_buffer_rsrc_t rsSide = rsrc_of(e.side, (int64_t)M * e.lds * ESZ);
-          const uint32_t s0 = this_lane_off(c, e.lds, ESZ, 0), s1 = this_lane_off(c, e.lds, ESZ, 1);
+        const __amdgpu_buffer_rsrc_t rsSide = rsrc_of(e.side, (int64_t)M * e.lds * ESZ);
+        const uint32_t s0 = this_lane_off(c, e.lds, ESZ, 0), s1 = this_lane_off(c, e.lds, ESZ, 1);
 #pragma unroll
-          for (int qn = 0; qn < 2; ++qn)
+        for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) side[QM][qn][i].load(rsSide, (qn ? s1 : s0) + seg_add(e.lds, ESZ, QM, i));
-          asm volatile("s_waitcnt vmcnt(0)"
-                       : "+v"(side[QM][0][0].a), "+v"(side[QM][0][1].a), "+v"(side[QM][0][2].a), "+v"(side[QM][0][3].a),
-                         "+v"(side[QM][1][0].a), "+v"(side[QM][1][1].a), "+v"(side[QM][1][2].a), "+v"(side[QM][1][3].a)
-                       :
-                       : "memory");
-          fence();
-        }
+          for (int i = 0; i < 4; ++i) side[QM][qn][i].load(rsSide, (qn ? s1 : s0) + seg_add(e.lds, ESZ, QM, i));
+      }
+    };
+    auto wait_side = [&](auto qmc) {
+      constexpr int QM = decltype(qmc)::value;
+      if constexpr (SIDE && ESZ == 2) {
+        asm volatile("s_waitcnt vmcnt(8)"
+                     : "+v"(side[QM][0][0].a), "+v"(side[QM][0][1].a), "+v"(side[QM][0][2].a), "+v"(side[QM][0][3].a),
+                       "+v"(side[QM][1][0].a), "+v"(side[QM][1][1].a), "+v"(side[QM][1][2].a), "+v"(side[QM][1][3].a)
+                     :
+                     : "memory");
+        fence();
       }
     };
     using QA = std::integral_constant<int, 0>;
@@ -385,9 +407,11 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
       for (int k = 0; k < 8; ++k) cs[qn][k] = 0.f;
-    load_side(QA{});
+    issue_side(QA{});
+    issue_side(QB{});
+    wait_side(QA{});
     const int n0 = epi_body(c, j, side, cs, QA{});
-    load_side(QB{});
+    wait_side(QB{});
     const int n1 = epi_body(c, j, side, cs, QB{});
     int nd = 0;
     if constexpr (DSUM) {
@@ -414,7 +438,7 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
       }
       nd = 4;  // two 16-B stores per quadrant column
     }
-    return ((SIDE && ESZ == 2) ? n1 : n0 + n1) + nd;
+    return n0 + n1 + nd;
   };
 
   // ---- main loop: gemm8p's two phases per K-tile over the continuous step sequence ----
