@@ -1004,6 +1004,180 @@ __global__ __launch_bounds__(256) void attn_decode_bf16(AttnArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- decode v2 ---
+// KV-cached decode attention (Nq <= 8 queries per (batch, head): one beam row's query, or the
+// k beams of one image against its shared memory K/V).  The step is HBM-bound on the K/V
+// stream and tiny per (batch, head), so what costs is instructions and round trips, not
+// FLOPs; attn_decode_bf16 above spends ~2000 VALU + ~400 cross-lane shuffles per lane on a
+// 196-key cross step (96 us for 154 MB: 1.6 TB/s).  Here:
+//  * LPR lanes own one key row (LPR = hd / 8 rounded up to 8 or 16: one 16-B chunk each),
+//    KPP = 64 / LPR keys per pass, every K and V chunk of the wave's <= MAXP passes requested
+//    before the first use (one round trip per wave);
+//  * the dot product is reduced inside the key's lane group by DPP (quad_perm,
+//    row_half_mirror, row_mirror: no LDS traffic), so every lane of the group holds the score;
+//  * each wave runs its own softmax over its keys (max / sum across the KPP groups: two to
+//    three xor shuffles per query) and accumulates P V for its chunk; waves of a workgroup
+//    (W = ceil(passes / MAXP), 1 for self-attention steps) merge their (m, l, acc) in LDS
+//    with the flash-decoding rescale.
+// No dropout / causal (decode never needs either); key padding honoured.
+template <int LPR>
+__device__ __forceinline__ float grp_sum(float x) {  // sum over the lane's LPR-lane group (LPR 8 / 16)
+#define CAPK_DPP(v, ctrl) __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xF, 0xF, false))
+  x += CAPK_DPP(x, 0xB1);   // quad_perm [1,0,3,2]
+  x += CAPK_DPP(x, 0x4E);   // quad_perm [2,3,0,1]
+  x += CAPK_DPP(x, 0x141);  // row_half_mirror: lane i <-> 7 - i of its 8
+  if constexpr (LPR == 16) x += CAPK_DPP(x, 0x140);  // row_mirror: lane i <-> 15 - i of its 16
+#undef CAPK_DPP
+  return x;
+}
+template <int LPR, int NQ, int MAXP>
+__global__ __launch_bounds__(512) void attn_decode2_bf16(AttnArgs a, int passes_per_wave) {
+  constexpr int KPP = 64 / LPR;
+  const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, W = blockDim.x >> 6;
+  const int g = lane / LPR, c = lane % LPR;
+  const bool act = c * 8 < a.hd;
+  const int hoff = h * a.hd + c * 8;
+  const int p0 = w * passes_per_wave;  // the wave's first pass (key j = pass * KPP + g)
+  const bf16* kb = (const bf16*)a.k + (int64_t)b * a.k_bs + hoff;
+  const bf16* vb = (const bf16*)a.v + (int64_t)b * a.v_bs + hoff;
+  bf16x8 kr[MAXP], vr[MAXP];
+  float qf[NQ][8];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const bf16x8 t = (act && q < a.Nq) ? ld8((const bf16*)a.q + (int64_t)b * a.q_bs + (int64_t)q * a.q_rs + hoff) : zero8();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) qf[q][i] = (float)t[i];
+  }
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    const int j = (p0 + p) * KPP + g;
+    kr[p] = (act && p < passes_per_wave && j < a.Nk) ? ld8(kb + (int64_t)j * a.k_rs) : zero8();
+  }
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    const int j = (p0 + p) * KPP + g;
+    vr[p] = (act && p < passes_per_wave && j < a.Nk) ? ld8(vb + (int64_t)j * a.v_rs) : zero8();
+  }
+  const float qs = a.scale * kLog2e;
+  float s[MAXP][NQ];
+  float m[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) m[q] = -INFINITY;
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    const int j = (p0 + p) * KPP + g;
+    const bool ok = p < passes_per_wave && j < a.Nk && (!a.key_pad || !a.key_pad[(int64_t)b * a.Nk + j]);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      float d = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d = fmaf(qf[q][i], (float)kr[p][i], d);
+      d = grp_sum<LPR>(d) * qs;
+      s[p][q] = ok ? d : -INFINITY;
+      m[q] = fmaxf(m[q], s[p][q]);
+    }
+  }
+  // the wave's max / sum over its KPP key groups (xor over the group index bits)
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int o = LPR; o < 64; o <<= 1) m[q] = fmaxf(m[q], __shfl_xor(m[q], o, 64));
+  float l[NQ], acc[NQ][8];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    l[q] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[q][i] = 0.f;
+  }
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    float vf[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) vf[i] = (float)vr[p][i];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const float pv = m[q] == -INFINITY ? 0.f : fexp2(s[p][q] - m[q]);
+      l[q] += pv;  // every lane of the group holds the same pv: the group sum is counted once below
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[q][i] = fmaf(pv, vf[i], acc[q][i]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+#pragma unroll
+    for (int o = LPR; o < 64; o <<= 1) {
+      l[q] += __shfl_xor(l[q], o, 64);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[q][i] += __shfl_xor(acc[q][i], o, 64);
+    }
+  }
+  // every lane of chunk c now holds the wave's (m, l, acc) for c; lanes of group 0 publish
+  if (W == 1) {
+    if (g == 0) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        if (q >= a.Nq) break;
+        const float inv = l[q] > 0.f ? 1.f / l[q] : 0.f;
+        if (act) {
+          bf16x8 o;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] = (bf16)(acc[q][i] * inv);
+          *(bf16x8*)((bf16*)a.out + (int64_t)b * a.out_bs + (int64_t)q * a.out_rs + hoff) = o;
+        }
+        if (c == 0) a.lse[((int64_t)b * a.H + h) * a.Nq + q] = l[q] > 0.f ? (m[q] + __log2f(l[q])) * kLn2 : -INFINITY;
+      }
+    }
+    return;
+  }
+  // (m, l) per wave and query, then acc [w][q][128]: dynamic LDS, none for W == 1 launches
+  extern __shared__ __attribute__((aligned(16))) float dsm[];
+  float(*sm)[NQ] = (float(*)[NQ])dsm;
+  float(*sl)[NQ] = (float(*)[NQ])(dsm + 8 * NQ);
+  float(*sacc)[NQ][128] = (float(*)[NQ][128])(dsm + 16 * NQ);
+  if (g == 0) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      if (c == 0) { sm[w][q] = m[q]; sl[w][q] = l[q]; }
+      if (act) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sacc[w][q][c * 8 + i] = acc[q][i];
+      }
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < a.Nq * a.hd; e += blockDim.x) {
+    const int q = e / a.hd, d = e % a.hd;
+    float mt = -INFINITY;
+    for (int ww = 0; ww < W; ++ww) mt = fmaxf(mt, sm[ww][q]);
+    float num = 0.f, den = 0.f;
+    if (mt > -INFINITY) {
+      for (int ww = 0; ww < W; ++ww) {
+        const float f = sm[ww][q] == -INFINITY ? 0.f : fexp2(sm[ww][q] - mt);
+        num += f * sacc[ww][q][d];
+        den += f * sl[ww][q];
+      }
+    }
+    ((bf16*)a.out)[(int64_t)b * a.out_bs + (int64_t)q * a.out_rs + h * a.hd + d] = (bf16)(den > 0.f ? num / den : 0.f);
+    if (d == 0) a.lse[((int64_t)b * a.H + h) * a.Nq + q] = den > 0.f ? (mt + __log2f(den)) * kLn2 : -INFINITY;
+  }
+}
+
+// launch the v2 decode kernel: LPR by head width, W waves so that each wave has <= MAXP passes
+template <int NQ>
+static int launch_decode2(const AttnArgs& a, hipStream_t st) {
+  constexpr int MAXP = 8;
+  const int lpr = a.hd <= 64 ? 8 : 16, kpp = 64 / lpr;
+  const int npass = cdiv(a.Nk, kpp);
+  const int W = std::min(8, cdiv(npass, MAXP)), ppw = cdiv(npass, W);
+  const dim3 g(a.B * a.H), blk(64 * W);
+  const size_t shm = W > 1 ? (size_t)(16 * NQ + 8 * NQ * 128) * sizeof(float) : 0;
+  if (lpr == 8) hipLaunchKernelGGL((attn_decode2_bf16<8, NQ, MAXP>), g, blk, shm, st, a, ppw);
+  else hipLaunchKernelGGL((attn_decode2_bf16<16, NQ, MAXP>), g, blk, shm, st, a, ppw);
+  CAPK_LAUNCH_CHECK("attn_decode2_bf16");
+  return CAPK_OK;
+}
+
 static int hdp_of(int hd) { return hd <= 32 ? 32 : hd <= 64 ? 64 : hd <= 96 ? 96 : 128; }
 
 static int check_common(int dtype, int B, int H, int Nq, int Nk, int hd) {
@@ -1051,7 +1225,20 @@ extern "C" int capk_attention_fwd(int dtype, int B, int H, int Nq, int Nk, int h
   CAPK_CHECK_ARG(q_rs % 8 == 0 && k_rs % 8 == 0 && v_rs % 8 == 0 && o_rs % 4 == 0 && q_bs % 8 == 0 &&
                      k_bs % 8 == 0 && v_bs % 8 == 0,
                  "capk_attention_fwd(bf16): strides must allow 16-B vector access");
-  if (Nq <= 8 && !causal && !(drop_p > 0.f)) {
+  static const bool decode_v1 = [] { const char* e = getenv("CAPK_DECODE_V1"); return e && e[0] == '1'; }();
+  if (Nq <= 8 && !causal && !(drop_p > 0.f) && !decode_v1) {
+    switch (Nq) {
+      case 1: return launch_decode2<1>(a, st);
+      case 2: return launch_decode2<2>(a, st);
+      case 3: return launch_decode2<3>(a, st);
+      case 4: return launch_decode2<4>(a, st);
+      case 5: return launch_decode2<5>(a, st);
+      case 6: return launch_decode2<6>(a, st);
+      case 7: return launch_decode2<7>(a, st);
+      default: return launch_decode2<8>(a, st);
+    }
+  }
+  if (Nq <= 8 && !causal && !(drop_p > 0.f)) {  // CAPK_DECODE_V1=1: the first decode kernel (A/B)
     const dim3 g(B * H), blk(256);
     switch (Nq) {
       case 1: hipLaunchKernelGGL(attn_decode_bf16<1>, g, blk, 0, st, a); break;

@@ -212,9 +212,9 @@ def test_attention_fwd_bwd(ops, dtype, case):
 
 
 @cuda
-@pytest.mark.parametrize("case", ["self_step", "cross_beams", "pad", "hd64_q8"])
+@pytest.mark.parametrize("case", ["self_step", "cross_beams", "pad", "hd64_q8", "gpt2_step", "cross_one"])
 def test_attention_decode_bf16(ops, case):
-    """Small-Nq decode path (attn_decode_bf16, chosen automatically for Nq <= 8): KV-cache
+    """Small-Nq decode path (attn_decode2_bf16, chosen automatically for Nq <= 8): KV-cache
     self-attention (one query, strided cache rows) and beam cross-attention (k beam
     queries of one image against shared memory keys with a CLS gap row)."""
     from capk.ops import HeadView
@@ -229,6 +229,10 @@ def test_attention_decode_bf16(ops, case):
         pad = torch.zeros(B, Nk, dtype=torch.bool, device="cuda")
         pad[1, 30:] = True
         pad[2, 0] = True
+    elif case == "gpt2_step":  # GPT-2 KV cache: 10 prefix slots + 19 tokens, hd 64
+        B, H, Nq, Nk, hd, gap, Lm = 48, 12, 1, 29, 64, 0, 30
+    elif case == "cross_one":  # greedy cross step: one query against 196 memory keys (7 waves merged)
+        B, H, Nq, Nk, hd, gap, Lm = 7, 8, 1, 196, 96, 1, 0
     else:
         B, H, Nq, Nk, hd, gap, Lm = 5, 12, 8, 256, 64, 0, 0
     D = H * hd

@@ -11,11 +11,18 @@ from capk import ops  # noqa: E402
 from capk.ops import HeadView  # noqa: E402
 
 CASES = [("vit", 256, 12, 197, 197, 64, False), ("dec_self", 256, 8, 20, 20, 96, True),
-         ("dec_cross", 256, 8, 20, 196, 96, False)]
+         ("dec_cross", 256, 8, 20, 196, 96, False),
+         # decode steps (forward only): config-3 beam-5 self (1280 rows, 20 keys) and cross (5
+         # beams of 256 images against 196 memory keys), GPT-2 beam-4 / sampling steps (30 keys)
+         ("dstep_self", 1280, 8, 1, 20, 96, False), ("dstep_cross5", 256, 8, 5, 196, 96, False),
+         ("dstep_gpt2_b4", 1024, 12, 1, 30, 64, False), ("dstep_gpt2_s", 256, 12, 1, 30, 64, False)]
+ONLY = os.environ.get("ATTN_ONLY")
 
 
 def main(iters=10):
     for name, B, H, Nq, Nk, hd, causal in CASES:
+        if ONLY and name not in ONLY.split(","):
+            continue
         D = H * hd
         g = torch.Generator(device="cuda").manual_seed(0)
         q = torch.randn(B * Nq, D, device="cuda", generator=g).bfloat16()
@@ -30,7 +37,7 @@ def main(iters=10):
         bwd = lambda: ops.attention_bwd(Q, K, V, O, HeadView(do, 0, Nq * D, D), lse, HeadView(dq, 0, Nq * D, D),
                                         HeadView(dkv, 0, Nk * 2 * D, 2 * D), HeadView(dkv, D, Nk * 2 * D, 2 * D),
                                         B, H, Nq, Nk, hd, sc, causal=causal)
-        for fn, tag, mult in ((fwd, "fwd", 4), (bwd, "bwd", 10)):
+        for fn, tag, mult in ((fwd, "fwd", 4), (bwd, "bwd", 10))[:1 if name.startswith("dstep") else 2]:
             fn()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -41,8 +48,8 @@ def main(iters=10):
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / iters
             fl = mult * B * H * Nq * Nk * hd / (2 if causal else 1)
-            by = (3 if tag == "fwd" else 6) * B * (Nq + 2 * Nk) / 3 * D * 2
-            print(f"{name:10s} {tag}: {ms * 1e3:8.1f} us  {fl / ms / 1e9:7.1f} TFLOP/s  ~{by / ms / 1e9 * 1e-3:6.2f} TB/s", flush=True)
+            by = (2 * B * Nq * D + 2 * B * Nk * D) * 2 * (1 if tag == "fwd" else 2)  # Q, O, K, V (x2 bwd)
+            print(f"{name:10s} {tag}: {ms * 1e3:8.1f} us  {fl / ms / 1e9:7.1f} TFLOP/s  ~{by / ms / 1e9:6.2f} TB/s", flush=True)
 
 
 if __name__ == "__main__":
