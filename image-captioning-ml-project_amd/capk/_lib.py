@@ -50,6 +50,8 @@ SIGNATURES = {
                                 _c_p, _c_p, _c_p, _i, _f, _u32, _c_p, _i64, _c_p, _sz, _c_p]),
     "capk_attention_fwd": (_i, [_i, _i, _i, _i, _i, _i, _f, _i, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _i64,
                                 _i64, _c_p, _c_p, _i64, _i64, _c_p, _f, _u32, _c_p]),
+    "capk_attention_decode_rows": (_i, [_i, _i, _i, _i, _i, _i, _f, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p,
+                                        _i64, _i64, _c_p, _i64, _c_p, _i64, _i64, _c_p, _c_p]),
     "capk_attention_bwd": (_i, [_i, _i, _i, _i, _i, _i, _f, _i,            # dtype B H Nq Nk hd scale causal
                                 _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _i64, _i64,  # q k v
                                 _c_p,                                          # key_pad
@@ -147,7 +149,10 @@ def load(path=LIB_PATH):
             raise CapkError(f"libcapk.so not found at {path}: build it with "
                             f"`make -C image-captioning-ml-project_amd/csrc` (no CPU fallback exists)")
         lib = ctypes.CDLL(path)
+        diag = path != os.path.join(_HERE, "libcapk.so")  # CAPK_LIB_PATH: an older / diagnostic build
         for name, (res, args) in SIGNATURES.items():
+            if diag and not hasattr(lib, name):
+                continue  # (A/B against an older library: entry points it predates stay unbound)
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

@@ -21,11 +21,13 @@ gradient first and the embedding scatter-add on top; the prefix gradient is the 
 over layers of dK + dV of the prefix slots.
 """
 import math
+import os
 
 import torch
 import torch.nn as nn
 
 from .. import ops
+from .transformer import _history_reorder, _history_tables
 from .._lib import ACT_DERIV, ACT_GELU_TANH
 from ..ops import HeadView
 from .common import G, CapkModule, W, heads, next_seed
@@ -327,7 +329,12 @@ class GPT2KVRunner:
         R = B * num_beams
         self.R = R
         shape = (c.n_layer, R, self.Lc, 3 * D)
-        self._bufs = (torch.empty(shape, dtype=dt, device=dev), torch.empty(shape, dtype=dt, device=dev))
+        # beam-history table instead of a reordered cache (transformer.KVDecodeRunner);
+        # CAPK_KV_GATHER=1: the whole-cache gather with ping-pong buffers
+        self.gather_kv = os.environ.get("CAPK_KV_GATHER", "0") == "1"
+        self._bufs = (torch.empty(shape, dtype=dt, device=dev),
+                      torch.empty(shape, dtype=dt, device=dev) if self.gather_kv else None)
+        self.hist, self.hist_tmp, self.hist0 = _history_tables(R, self.Lc, dev)
         self.pref_rep = torch.empty(R, P * D, dtype=dt, device=dev)
         self.rep_idx = torch.arange(R, dtype=torch.int32, device=dev) // num_beams
         wte = m.model.transformer.wte.weight
@@ -354,6 +361,7 @@ class GPT2KVRunner:
 
     def reset(self):
         self.cache, self.spare = self._bufs
+        self.hist.copy_(self.hist0)
 
     def step(self, cur_len, ids, reorder_idx):
         m, dt, D, H, hd, R, P = self.m, self.dt, self.D, self.H, self.hd, self.R, self.P
@@ -362,10 +370,13 @@ class GPT2KVRunner:
         pos = P + t
         Lc3 = self.Lc * 3 * D
         if reorder_idx is not None:
-            c = self.cache
-            nl = c.shape[0]
-            ops.gather_rows(c, reorder_idx, self.spare, nl, R, pos * 3 * D, Lc3, R * Lc3, Lc3, R * Lc3)
-            self.cache, self.spare = self.spare, self.cache
+            if self.gather_kv:
+                c = self.cache
+                nl = c.shape[0]
+                ops.gather_rows(c, reorder_idx, self.spare, nl, R, pos * 3 * D, Lc3, R * Lc3, Lc3, R * Lc3)
+                self.cache, self.spare = self.spare, self.cache
+            else:  # (the 10 prefix positions are the same row content for every beam of an image)
+                _history_reorder(self.hist, self.hist_tmp, reorder_idx, pos)
         x = ops.embedding_fwd(ids.view(R, 1), tr.wte.weight.detach(), tr.wpe.weight.detach(), pos, dt)
         for li, blk in enumerate(tr.h):
             at, mlp = blk.attn, blk.mlp
@@ -373,8 +384,12 @@ class GPT2KVRunner:
             h1, _, _ = ops.layernorm_fwd(x, blk.ln_1.weight.detach(), blk.ln_1.bias.detach(), blk.ln_1.eps)
             ops.conv1d(h1, W(at.c_attn.weight, dt), at.c_attn.bias.detach(), out=cl[:, pos, :])
             a = torch.empty(R, D, dtype=dt, device=x.device)
-            ops.attention_fwd(HeadView(cl, pos * 3 * D, Lc3, 3 * D), HeadView(cl, D, Lc3, 3 * D),
-                              HeadView(cl, 2 * D, Lc3, 3 * D), HeadView(a, 0, D, D), R, H, 1, pos + 1, hd, self.scale)
+            qv, kv_, vv = HeadView(cl, pos * 3 * D, Lc3, 3 * D), HeadView(cl, D, Lc3, 3 * D), HeadView(cl, 2 * D, Lc3, 3 * D)
+            if self.gather_kv:
+                ops.attention_fwd(qv, kv_, vv, HeadView(a, 0, D, D), R, H, 1, pos + 1, hd, self.scale)
+            else:
+                ops.attention_decode_rows(qv, kv_, vv, HeadView(a, 0, D, D), self.hist, R, H, 1, pos + 1, hd,
+                                          self.scale)
             x1 = ops.conv1d(a, W(at.c_proj.weight, dt), at.c_proj.bias.detach(), residual=x)
             h2, _, _ = ops.layernorm_fwd(x1, blk.ln_2.weight.detach(), blk.ln_2.bias.detach(), blk.ln_2.eps)
             f = ops.conv1d(h2, W(mlp.c_fc.weight, dt), mlp.c_fc.bias.detach(), act=ACT_GELU_TANH)

@@ -21,6 +21,7 @@ underlying rows and attention addresses batch b at row b*(S+gap) — no copy.
 """
 import copy
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -289,6 +290,24 @@ def _padded_grad(dlogits, logits_pad, BT, V, Vp):
     return out
 
 
+def _history_tables(R, L, dev):
+    """Beam-history tables [R, L8] int32 (L rounded up to 8 for the 16-B row gather): the live
+    table, a gather target, and the identity (row r holds every position of hypothesis r)."""
+    L8 = (L + 7) // 8 * 8
+    hist0 = torch.arange(R, dtype=torch.int32, device=dev)[:, None].expand(R, L8).contiguous()
+    return hist0.clone(), torch.empty_like(hist0), hist0
+
+
+def _history_reorder(hist, tmp, idx, t):
+    """hist[r, :t] <- hist[idx[r], :t]; columns >= t keep row r (position t is written by row r's
+    own step; position t-1 of the parent is the parent's own row, carried by the copy)."""
+    R, L8 = hist.shape
+    f = hist.view(torch.float32)  # bit copy through the fp32 row gather
+    ops.check(ops.lib().capk_gather_rows(ops.dtype_code(f), 1, R, L8, idx.data_ptr(), f.data_ptr(), L8, 0,
+                                         tmp.data_ptr(), L8, 0, ops._stream()), "capk_gather_rows")
+    hist[:, :t].copy_(tmp[:, :t])
+
+
 class KVDecodeRunner:
     """KV-cached incremental decode of the Transformer decoder for beam search
     (SURVEY §8a A14 on the A4 model; HF's per-step ``past_key_values`` path).
@@ -302,8 +321,13 @@ class KVDecodeRunner:
     * self side: the fused QKV GEMM of the new token writes straight into the layer's
       cache slot ``cache[l, r, t, :]`` (layout [layers, B*k, max_length, 3D]); the
       attention reads keys/values 0..t of row r in place;
-    * after each beam step the caches of all layers are reordered in one gather launch
-      (ping-pong buffers) — HF ``Cache.reorder_cache(beam_idx)`` (utils.py:3479-3489).
+    * HF ``Cache.reorder_cache(beam_idx)`` (utils.py:3479-3489) without moving the cache: a
+      beam-history table ``hist[r, j]`` (int32, the cache row holding position j of
+      hypothesis r) is gathered by the step's parent indices (a few KB per step) and the
+      self-attention reads key j < t from row ``hist[r, j]`` (capk_attention_decode_rows);
+      the cache rows themselves are written once, by the QKV GEMM of their own step.  The
+      former whole-cache gather (R x t x 3D per layer per step, ping-pong buffers) remains
+      behind CAPK_KV_GATHER=1 for A/B and the bit-identity test.
     """
 
     def __init__(self, m, features, num_beams, max_length):
@@ -321,7 +345,10 @@ class KVDecodeRunner:
         R = B * num_beams
         self.R = R
         shape = (nl, R, max_length, 3 * D)
-        self._bufs = (torch.empty(shape, dtype=dt, device=dev), torch.empty(shape, dtype=dt, device=dev))
+        self.gather_kv = os.environ.get("CAPK_KV_GATHER", "0") == "1"
+        self._bufs = (torch.empty(shape, dtype=dt, device=dev),
+                      torch.empty(shape, dtype=dt, device=dev) if self.gather_kv else None)
+        self.hist, self.hist_tmp, self.hist0 = _history_tables(R, max_length, dev)
         ol = m.output_layer
         self.wout = ol.weight._capk_pad_bf16 if dt == torch.bfloat16 else ol.weight._capk_pad_master
         self.bout = _pad_bias(ol)
@@ -345,10 +372,15 @@ class KVDecodeRunner:
 
     def reset(self):
         self.cache, self.spare = self._bufs
+        self.hist.copy_(self.hist0)
 
     def reorder(self, idx, t):
-        """Rows r <- idx[r] for cache positions [0, t) of every layer (one launch)."""
+        """Rows r <- idx[r] for cache positions [0, t): the history table (default), or every
+        layer's cache in one gather launch (CAPK_KV_GATHER=1)."""
         if t <= 0:
+            return
+        if not self.gather_kv:
+            _history_reorder(self.hist, self.hist_tmp, idx, t)
             return
         c = self.cache
         nl, R, Lm, C3 = c.shape
@@ -372,9 +404,13 @@ class KVDecodeRunner:
             cl = self.cache[li]                      # [R, Lm, 3D]
             ops.linear(x, W(sa.in_proj_weight, dt), sa.in_proj_bias.detach(), out=cl[:, t, :])
             a = torch.empty(R, D, dtype=dt, device=x.device)
-            ops.attention_fwd(HeadView(cl, t * 3 * D, rs_cache, 3 * D), HeadView(cl, D, rs_cache, 3 * D),
-                              HeadView(cl, 2 * D, rs_cache, 3 * D), HeadView(a, 0, D, D), R, H, 1, t + 1, hd,
-                              self.scale)
+            qv, kv_, vv = (HeadView(cl, t * 3 * D, rs_cache, 3 * D), HeadView(cl, D, rs_cache, 3 * D),
+                           HeadView(cl, 2 * D, rs_cache, 3 * D))
+            if self.gather_kv:
+                ops.attention_fwd(qv, kv_, vv, HeadView(a, 0, D, D), R, H, 1, t + 1, hd, self.scale)
+            else:
+                ops.attention_decode_rows(qv, kv_, vv, HeadView(a, 0, D, D), self.hist, R, H, 1, t + 1, hd,
+                                          self.scale)
             s1 = ops.linear(a, W(sa.out_proj.weight, dt), sa.out_proj.bias.detach(), residual=x)
             x1, _, _ = ops.layernorm_fwd(s1, L.norm1.weight.detach(), L.norm1.bias.detach(), L.norm1.eps)
             qc = ops.linear(x1, W(ca.in_proj_weight, dt)[:D], ca.in_proj_bias.detach()[:D])

@@ -371,6 +371,19 @@ def attention_fwd(q, k, v, o, B, H, Nq, Nk, hd, scale, causal=False, key_pad=Non
     return lse, kp
 
 
+def attention_decode_rows(q, k, v, o, rows, B, H, Nq, Nk, hd, scale, lse=None):
+    """Decode step over a beam-history table (capk_attention_decode_rows): key j < Nk-1 of batch
+    row b is read from K/V row rows[b, j] (int32 [B, ld]), the last key from row b."""
+    if lse is None:
+        lse = torch.empty(B, H, Nq, dtype=torch.float32, device=q.t.device)
+    if rows.dtype != torch.int32 or rows.dim() != 2 or rows.stride(1) != 1 or rows.shape[0] != B:
+        raise ValueError("attention_decode_rows: rows must be int32 [B, ld] with unit column stride")
+    check(lib().capk_attention_decode_rows(dtype_code(q.t), B, H, Nq, Nk, hd, float(scale), q.ptr(), q.bs, q.rs,
+                                           k.ptr(), k.bs, k.rs, v.ptr(), v.bs, v.rs, rows.data_ptr(), rows.stride(0),
+                                           o.ptr(), o.bs, o.rs, _p(lse), _stream()), "capk_attention_decode_rows")
+    return lse
+
+
 def attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Nq, Nk, hd, scale, causal=False, key_pad_u8=None,
                   drop=NO_DROP):
     check(lib().capk_attention_bwd(dtype_code(q.t), B, H, Nq, Nk, hd, float(scale), int(causal),

@@ -35,7 +35,15 @@ struct AttnArgs {
   void *dq, *dk, *dv;
   int64_t dq_bs, dq_rs, dk_bs, dk_rs, dv_bs, dv_rs;
   Drop drop;  // attention-probability dropout, mask index ((b*H + h)*Nq + q)*Nk + key
+  // decode with a beam-history table (capk_attention_decode_rows): key j < Nk-1 of batch row b
+  // lives in K/V row kv_rows[b * kv_rows_ld + j], the last key (the step's own token) in row b
+  const int* kv_rows;
+  int64_t kv_rows_ld;
 };
+// the K / V batch row holding key j of batch row b
+__device__ __forceinline__ int64_t kv_row(const AttnArgs& a, int b, int j) {
+  return (a.kv_rows && j < a.Nk - 1) ? (int64_t)a.kv_rows[(int64_t)b * a.kv_rows_ld + j] : (int64_t)b;
+}
 __device__ __forceinline__ float pdrop(const AttnArgs& a, int b, int h, int q, int key) {
   return a.drop.mul((((uint64_t)b * a.H + h) * a.Nq + q) * a.Nk + key);
 }
@@ -744,30 +752,33 @@ __global__ __launch_bounds__(64) void attn_fwd_f32(AttnArgs a) {
   if (q >= a.Nq) return;
   const int hoff = h * HD;
   const float* qr = (const float*)a.q + (int64_t)b * a.q_bs + (int64_t)q * a.q_rs + hoff;
-  const float* kb = (const float*)a.k + (int64_t)b * a.k_bs + hoff;
-  const float* vb = (const float*)a.v + (int64_t)b * a.v_bs + hoff;
   float qv[HD], o[HD];
 #pragma unroll
   for (int d = 0; d < HD; ++d) { qv[d] = qr[d]; o[d] = 0.f; }
+  auto krow = [&](int j) { return (const float*)a.k + kv_row(a, b, j) * a.k_bs + hoff + (int64_t)j * a.k_rs; };
+  auto vrow = [&](int j) { return (const float*)a.v + kv_row(a, b, j) * a.v_bs + hoff + (int64_t)j * a.v_rs; };
   float mx = -INFINITY;
   for (int j = 0; j < a.Nk; ++j) {
     if (!key_ok(a, b, j, q)) continue;
+    const float* kr = krow(j);
     float s = 0.f;
 #pragma unroll
-    for (int d = 0; d < HD; ++d) s += qv[d] * kb[(int64_t)j * a.k_rs + d];
+    for (int d = 0; d < HD; ++d) s += qv[d] * kr[d];
     mx = fmaxf(mx, s * a.scale);
   }
   float l = 0.f;
   for (int j = 0; j < a.Nk; ++j) {
     if (!key_ok(a, b, j, q)) continue;
+    const float* kr = krow(j);
+    const float* vr = vrow(j);
     float s = 0.f;
 #pragma unroll
-    for (int d = 0; d < HD; ++d) s += qv[d] * kb[(int64_t)j * a.k_rs + d];
+    for (int d = 0; d < HD; ++d) s += qv[d] * kr[d];
     const float p = expf(s * a.scale - mx);
     l += p;
     const float pd = a.drop.on() ? p * pdrop(a, b, h, q, j) : p;
 #pragma unroll
-    for (int d = 0; d < HD; ++d) o[d] += pd * vb[(int64_t)j * a.v_rs + d];
+    for (int d = 0; d < HD; ++d) o[d] += pd * vr[d];
   }
   float* orow = (float*)a.out + (int64_t)b * a.out_bs + (int64_t)q * a.out_rs + hoff;
 #pragma unroll
@@ -1039,8 +1050,8 @@ __global__ __launch_bounds__(512) void attn_decode2_bf16(AttnArgs a, int passes_
   const bool act = c * 8 < a.hd;
   const int hoff = h * a.hd + c * 8;
   const int p0 = w * passes_per_wave;  // the wave's first pass (key j = pass * KPP + g)
-  const bf16* kb = (const bf16*)a.k + (int64_t)b * a.k_bs + hoff;
-  const bf16* vb = (const bf16*)a.v + (int64_t)b * a.v_bs + hoff;
+  const bf16* kb = (const bf16*)a.k + hoff;
+  const bf16* vb = (const bf16*)a.v + hoff;
   bf16x8 kr[MAXP], vr[MAXP];
   float qf[NQ][8];
 #pragma unroll
@@ -1052,12 +1063,15 @@ __global__ __launch_bounds__(512) void attn_decode2_bf16(AttnArgs a, int passes_
 #pragma unroll
   for (int p = 0; p < MAXP; ++p) {
     const int j = (p0 + p) * KPP + g;
-    kr[p] = (act && p < passes_per_wave && j < a.Nk) ? ld8(kb + (int64_t)j * a.k_rs) : zero8();
-  }
-#pragma unroll
-  for (int p = 0; p < MAXP; ++p) {
-    const int j = (p0 + p) * KPP + g;
-    vr[p] = (act && p < passes_per_wave && j < a.Nk) ? ld8(vb + (int64_t)j * a.v_rs) : zero8();
+    const bool in = act && p < passes_per_wave && j < a.Nk;
+    if (a.kv_rows) {  // (wave-uniform) beam-history table: the row per key
+      const int64_t rb = in ? kv_row(a, b, j) : 0;
+      kr[p] = in ? ld8(kb + rb * a.k_bs + (int64_t)j * a.k_rs) : zero8();
+      vr[p] = in ? ld8(vb + rb * a.v_bs + (int64_t)j * a.v_rs) : zero8();
+    } else {
+      kr[p] = in ? ld8(kb + (int64_t)b * a.k_bs + (int64_t)j * a.k_rs) : zero8();
+      vr[p] = in ? ld8(vb + (int64_t)b * a.v_bs + (int64_t)j * a.v_rs) : zero8();
+    }
   }
   const float qs = a.scale * kLog2e;
   float s[MAXP][NQ];
@@ -1226,7 +1240,7 @@ extern "C" int capk_attention_fwd(int dtype, int B, int H, int Nq, int Nk, int h
                      k_bs % 8 == 0 && v_bs % 8 == 0,
                  "capk_attention_fwd(bf16): strides must allow 16-B vector access");
   static const bool decode_v1 = [] { const char* e = getenv("CAPK_DECODE_V1"); return e && e[0] == '1'; }();
-  if (Nq <= 8 && !causal && !(drop_p > 0.f) && !decode_v1) {
+  if (Nq <= 8 && !causal && !(drop_p > 0.f) && !decode_v1 && o_rs % 8 == 0 && o_bs % 8 == 0) {
     switch (Nq) {
       case 1: return launch_decode2<1>(a, st);
       case 2: return launch_decode2<2>(a, st);
@@ -1271,6 +1285,42 @@ extern "C" int capk_attention_fwd(int dtype, int B, int H, int Nq, int Nk, int h
     default: FWD_M(128)
   }
 #undef FWD_M
+}
+
+extern "C" int capk_attention_decode_rows(int dtype, int B, int H, int Nq, int Nk, int hd, float scale, const void* q,
+                                          int64_t q_bs, int64_t q_rs, const void* k, int64_t k_bs, int64_t k_rs,
+                                          const void* v, int64_t v_bs, int64_t v_rs, const int32_t* kv_rows,
+                                          int64_t kv_rows_ld, void* o, int64_t o_bs, int64_t o_rs, float* lse,
+                                          void* stream) {
+  int rc = check_common(dtype, B, H, Nq, Nk, hd);
+  if (rc) return rc;
+  CAPK_CHECK_ARG(Nq <= 8 && kv_rows && kv_rows_ld >= Nk - 1, "capk_attention_decode_rows: Nq <= 8 and a history table");
+  AttnArgs a{};
+  a.B = B; a.H = H; a.Nq = Nq; a.Nk = Nk; a.hd = hd; a.causal = 0; a.scale = scale;
+  a.q = q; a.k = k; a.v = v; a.q_bs = q_bs; a.q_rs = q_rs; a.k_bs = k_bs; a.k_rs = k_rs; a.v_bs = v_bs; a.v_rs = v_rs;
+  a.out = o; a.out_bs = o_bs; a.out_rs = o_rs; a.lse = lse;
+  a.drop = make_drop(0.f, 0);
+  a.kv_rows = kv_rows; a.kv_rows_ld = kv_rows_ld;
+  hipStream_t st = S(stream);
+  if (dtype == CAPK_F32) {
+    dim3 grid(B * H, cdiv(Nq, 64));
+    F32_HD_DISPATCH(attn_fwd_f32, grid);
+    CAPK_LAUNCH_CHECK("attn_fwd_f32");
+    return CAPK_OK;
+  }
+  CAPK_CHECK_ARG(q_rs % 8 == 0 && k_rs % 8 == 0 && v_rs % 8 == 0 && o_rs % 8 == 0 && q_bs % 8 == 0 &&
+                     k_bs % 8 == 0 && v_bs % 8 == 0 && o_bs % 8 == 0,
+                 "capk_attention_decode_rows(bf16): strides must allow 16-B vector access");
+  switch (Nq) {
+    case 1: return launch_decode2<1>(a, st);
+    case 2: return launch_decode2<2>(a, st);
+    case 3: return launch_decode2<3>(a, st);
+    case 4: return launch_decode2<4>(a, st);
+    case 5: return launch_decode2<5>(a, st);
+    case 6: return launch_decode2<6>(a, st);
+    case 7: return launch_decode2<7>(a, st);
+    default: return launch_decode2<8>(a, st);
+  }
 }
 
 extern "C" int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int hd, float scale, int causal,

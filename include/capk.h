@@ -156,6 +156,18 @@ int capk_attention_fwd(int dtype, int B, int H, int Nq, int Nk, int hd, float sc
                        const uint8_t* key_pad,
                        void* o, int64_t o_bs, int64_t o_rs, float* lse,
                        float drop_p, uint32_t drop_seed, void* stream);
+/* KV-cached decode step over a beam-history table instead of a reordered cache (HF
+ * Cache.reorder_cache, generation/utils.py:3479-3489, without moving the cache): key j <
+ * Nk-1 of batch row b is read from K/V batch row kv_rows[b*kv_rows_ld + j] (int32), the
+ * last key (this step's token, written in place) from row b.  Same arithmetic as
+ * capk_attention_fwd on the reordered cache, bit for bit.  Nq <= 8, no masks / dropout;
+ * bf16 or fp32. */
+int capk_attention_decode_rows(int dtype, int B, int H, int Nq, int Nk, int hd, float scale,
+                               const void* q, int64_t q_bs, int64_t q_rs,
+                               const void* k, int64_t k_bs, int64_t k_rs,
+                               const void* v, int64_t v_bs, int64_t v_rs,
+                               const int32_t* kv_rows, int64_t kv_rows_ld,
+                               void* o, int64_t o_bs, int64_t o_rs, float* lse, void* stream);
 int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int hd, float scale, int causal,
                        const void* q, int64_t q_bs, int64_t q_rs,
                        const void* k, int64_t k_bs, int64_t k_rs,

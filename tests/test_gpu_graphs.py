@@ -142,3 +142,30 @@ def test_short_search_then_full_search_graphs_equal_eager():
     assert ref[1][0].shape[1] < 20 and ref[2][0].shape[1] == 20, [r[0].shape for r in ref]
     for r, g in zip(ref, got):
         _same(r, g)
+
+
+@cuda
+@pytest.mark.parametrize("kind", ["transformer", "gpt2"])
+def test_history_table_equals_cache_gather(kind, monkeypatch):
+    """The beam-history table (capk_attention_decode_rows: key j of hypothesis r read from
+    cache row hist[r, j]) against the whole-cache reorder it replaces (CAPK_KV_GATHER=1,
+    HF Cache.reorder_cache): same keys and values in the same order, so sequences, scores
+    and beam indices are bit-identical, eager and graph-replayed."""
+    from capk import graphs
+    dec = _decoder(kind, seed=6)
+    beams = 5 if kind == "transformer" else 4
+    inputs = [_enc(3, s) for s in (21, 22, 23)]
+
+    def fn(enc):
+        with torch.no_grad():
+            ids, info = dec.generate(enc, 20, num_beams=beams)
+        return [ids.clone(), info["sequences_scores"].clone(), info["beam_indices"].clone()]
+
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("CAPK_KV_GATHER", mode)
+        out[mode] = _eager_then_graphed(fn, inputs)
+    graphs.clear()
+    for a, b in zip(out["1"], out["0"]):
+        for r, g in zip(a, b):
+            _same(r, g)
