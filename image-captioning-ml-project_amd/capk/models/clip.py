@@ -92,6 +92,7 @@ class CLIPEncoderLayer(CapkModule):
     fc2 = property(lambda self: self.mlp.fc2)
 
     def forward(self, x, B, N):
+        self.grad_graph = torch.is_grad_enabled()
         return _ViTLayerFn.apply(x, self.self_attn.out_proj.weight, self, B, N)
 
 

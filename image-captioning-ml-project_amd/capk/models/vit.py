@@ -114,6 +114,7 @@ class ViTLayer(CapkModule):
         return self.mlp.fc2
 
     def forward(self, x, B, N):
+        self.grad_graph = torch.is_grad_enabled()  # (inference: no act'(pre) kept, nothing saved)
         return _ViTLayerFn.apply(x, self.attn.o_proj.weight, self, B, N)
 
 
@@ -223,6 +224,9 @@ class _ViTLayerFn(torch.autograd.Function):
         x1 = ops.linear(o, W(at.o_proj.weight, dt), at.o_proj.bias.detach(), residual=x)
         h2, mu2, rs2 = ops.layernorm_fwd(x1, ln2.weight.detach(), ln2.bias.detach(), L.eps)
         I = fc1.weight.shape[0]
+        if not getattr(L, "grad_graph", True):  # no_grad / inference (encoder of a beam search)
+            f = ops.linear(h2, W(fc1.weight, dt), fc1.bias.detach(), act=act)
+            return ops.linear(f, W(fc2.weight, dt), fc2.bias.detach(), residual=x1)
         f_pre = torch.empty(x.shape[0], I, dtype=x.dtype, device=x.device)
         # f_pre keeps act'(pre) (CAPK_ACT_DERIV): the FC1 epilogue writes GELU(pre) and its
         # derivative together, and the backward's dX epilogue multiplies by it and takes

@@ -1015,6 +1015,134 @@ __global__ __launch_bounds__(256) void attn_decode_bf16(AttnArgs a) {
   }
 }
 
+// ------------------------------------------------- beam cross-attention step ---
+// The k beam queries of one image against its shared memory keys (config-3 beam-5: Nq = 5,
+// Nk = 196, hd 96; 114 launches per 256-image batch) on MFMA.  The VALU decode kernels
+// spend ~1000 VALU issues per wave on 5 x 196 x 96 dot products (88 us per step, 1.9 TB/s);
+// here the same products are 24 MFMAs per wave and the step is a K / V stream:
+//  * 4 waves per (batch, head), each owning 64 keys (Nk <= 256): S^T = K Q^T with K
+//    fragments loaded straight from global memory (16 keys x 32 dims per MFMA, 16-B lane
+//    loads of K rows) and the <= 16 queries as the B operand (one 16-query tile);
+//  * the wave's V rows staged in its own LDS image (row stride HDP + 16) and read as V^T
+//    fragments by ds_read_b64_tr_b16 for O^T = V^T P^T, P^T packed from the S^T registers
+//    (the attn_fwd_bf16 layout: no shuffles between the two products);
+//  * every K, V and Q load of the wave issued before the first wait (one round trip);
+//  * per-wave softmax (m, l, O^T) merged across the 4 waves in LDS with the flash-decoding
+//    rescale.  No dropout / causal; key padding honoured.
+template <int HDP, int MODE>
+__global__ __launch_bounds__(256) void attn_xdec_bf16(AttnArgs a) {
+  constexpr int NW = 4, KPW = 64, ST = HDP + 16, NCH = HDP / 8, NS = HDP / 32, ND = HDP / 16;
+  __shared__ __attribute__((aligned(16))) bf16 vimg[NW][KPW * ST];
+  __shared__ float mm[NW][16], ll[NW][16];
+  const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
+  const int hoff = h * a.hd;
+  const int k0 = w * KPW;  // the wave's first key
+  const bf16* kbase = (const bf16*)a.k + (int64_t)b * a.k_bs + hoff;
+  const bf16* vbase = (const bf16*)a.v + (int64_t)b * a.v_bs + hoff;
+  // Q^T fragments (B operand): query c16, dims s*32 + 8g
+  bf16x8 qf[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int d = s * 32 + 8 * g;
+    qf[s] = (c16 < a.Nq && d < a.hd) ? ld8((const bf16*)a.q + (int64_t)b * a.q_bs + (int64_t)c16 * a.q_rs + hoff + d)
+                                     : zero8();
+  }
+  // K fragments (A operand): key k0 + 16 kb + c16, dims s*32 + 8g
+  bf16x8 kf[KPW / 16][NS];
+#pragma unroll
+  for (int kb = 0; kb < KPW / 16; ++kb)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int key = k0 + kb * 16 + c16, d = s * 32 + 8 * g;
+      kf[kb][s] = (key < a.Nk && d < a.hd) ? ld8(kbase + (int64_t)key * a.k_rs + d) : zero8();
+    }
+  // V rows of the wave -> registers -> its LDS image (chunk ch = lane + 64 i: row ch / NCH)
+  constexpr int VIT = KPW * NCH / 64;
+  bf16x8 vr[VIT];
+#pragma unroll
+  for (int i = 0; i < VIT; ++i) {
+    const int ch = lane + 64 * i, row = ch / NCH, col = (ch % NCH) * 8;
+    const int key = k0 + row;
+    vr[i] = (key < a.Nk && col < a.hd) ? ld8(vbase + (int64_t)key * a.v_rs + col) : zero8();
+  }
+  bf16* Vs = vimg[w];
+#pragma unroll
+  for (int i = 0; i < VIT; ++i) {
+    const int ch = lane + 64 * i, row = ch / NCH, col = (ch % NCH) * 8;
+    *(bf16x8*)(Vs + row * ST + col) = vr[i];
+  }
+  // S^T = K Q^T, scores in the log2 domain; keys past Nk / padded -> -inf
+  const float sl2 = a.scale * kLog2e;
+  f32x4 sc[KPW / 16];
+  float m = -INFINITY;
+#pragma unroll
+  for (int kb = 0; kb < KPW / 16; ++kb) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NS; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kb][s], qf[s], acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int key = k0 + kb * 16 + 4 * g + r;
+      const bool ok = (MODE & AM_MASK) ? key_ok(a, b, key, c16) : key < a.Nk;
+      acc[r] = ok ? acc[r] * sl2 : -INFINITY;
+      m = fmaxf(m, acc[r]);
+    }
+    sc[kb] = acc;
+  }
+  m = fmaxf(m, __shfl_xor(m, 16, 64));
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  float l = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < KPW / 16; ++kb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float p = m == -INFINITY ? 0.f : fexp2(sc[kb][r] - m);
+      sc[kb][r] = p;
+      l += p;
+    }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own V image is written
+  // O^T = V^T P^T over two 32-key chunks
+  f32x4 o[ND];
+#pragma unroll
+  for (int db = 0; db < ND; ++db) o[db] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < KPW / 32; ++t) {
+    const bf16x8 pb = pack8(sc[2 * t], sc[2 * t + 1]);
+#pragma unroll
+    for (int db = 0; db < ND; ++db)
+      o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_read8(Vs, ST, 32 * t, db * 16, lane), pb, o[db], 0, 0, 0);
+  }
+  // merge the 4 waves: (m, l) per query, O^T partials into the (now free) V images as fp32
+  __syncthreads();  // every wave is done reading its V image
+  float* op = (float*)vimg[w];  // [16 queries][HDP] fp32 (fits in the wave's image)
+#pragma unroll
+  for (int db = 0; db < ND; ++db)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) op[c16 * HDP + db * 16 + 4 * g + r] = o[db][r];
+  if (g == 0) { mm[w][c16] = m; ll[w][c16] = l; }
+  __syncthreads();
+  for (int e = threadIdx.x; e < a.Nq * a.hd; e += blockDim.x) {
+    const int q = e / a.hd, d = e % a.hd;
+    float mt = -INFINITY;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) mt = fmaxf(mt, mm[ww][q]);
+    float num = 0.f, den = 0.f;
+    if (mt > -INFINITY) {
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) {
+        const float f = mm[ww][q] == -INFINITY ? 0.f : fexp2(mm[ww][q] - mt);
+        num += f * ((const float*)vimg[ww])[q * HDP + d];
+        den += f * ll[ww][q];
+      }
+    }
+    ((bf16*)a.out)[(int64_t)b * a.out_bs + (int64_t)q * a.out_rs + hoff + d] = (bf16)(den > 0.f ? num / den : 0.f);
+    if (d == 0) a.lse[((int64_t)b * a.H + h) * a.Nq + q] = den > 0.f ? (mt + __log2f(den)) * kLn2 : -INFINITY;
+  }
+}
+
 // ---------------------------------------------------------------- decode v2 ---
 // KV-cached decode attention (Nq <= 8 queries per (batch, head): one beam row's query, or the
 // k beams of one image against its shared memory K/V).  The step is HBM-bound on the K/V
@@ -1240,6 +1368,21 @@ extern "C" int capk_attention_fwd(int dtype, int B, int H, int Nq, int Nk, int h
                      k_bs % 8 == 0 && v_bs % 8 == 0,
                  "capk_attention_fwd(bf16): strides must allow 16-B vector access");
   static const bool decode_v1 = [] { const char* e = getenv("CAPK_DECODE_V1"); return e && e[0] == '1'; }();
+  // beam cross-attention steps (k beams of an image against its memory keys): the MFMA
+  // kernel (CAPK_XDEC=0 keeps them on the VALU decode kernel for A/B)
+  static const bool xdec_on = [] { const char* e = getenv("CAPK_XDEC"); return !(e && e[0] == '0'); }();
+  if (xdec_on && !decode_v1 && Nq >= 2 && Nq <= 16 && Nk > 64 && Nk <= 256 && !causal && !(drop_p > 0.f) &&
+      (hd == 64 || hd == 96 || hd == 128)) {
+    const dim3 g(B * H), blk(256);
+    const int xm = key_pad ? AM_MASK : 0;
+#define XD(HD)                                                                                          \
+  if (xm) hipLaunchKernelGGL((attn_xdec_bf16<HD, AM_MASK>), g, blk, 0, st, a);                          \
+  else hipLaunchKernelGGL((attn_xdec_bf16<HD, 0>), g, blk, 0, st, a);
+    if (hd == 64) { XD(64) } else if (hd == 96) { XD(96) } else { XD(128) }
+#undef XD
+    CAPK_LAUNCH_CHECK("attn_xdec_bf16");
+    return CAPK_OK;
+  }
   if (Nq <= 8 && !causal && !(drop_p > 0.f) && !decode_v1 && o_rs % 8 == 0 && o_bs % 8 == 0) {
     switch (Nq) {
       case 1: return launch_decode2<1>(a, st);

@@ -212,7 +212,8 @@ def test_attention_fwd_bwd(ops, dtype, case):
 
 
 @cuda
-@pytest.mark.parametrize("case", ["self_step", "cross_beams", "pad", "hd64_q8", "gpt2_step", "cross_one"])
+@pytest.mark.parametrize("case", ["self_step", "cross_beams", "pad", "hd64_q8", "gpt2_step", "cross_one",
+                                  "cross_pad", "cross_hd128_q16"])
 def test_attention_decode_bf16(ops, case):
     """Small-Nq decode path (attn_decode2_bf16, chosen automatically for Nq <= 8): KV-cache
     self-attention (one query, strided cache rows) and beam cross-attention (k beam
@@ -233,6 +234,13 @@ def test_attention_decode_bf16(ops, case):
         B, H, Nq, Nk, hd, gap, Lm = 48, 12, 1, 29, 64, 0, 30
     elif case == "cross_one":  # greedy cross step: one query against 196 memory keys (7 waves merged)
         B, H, Nq, Nk, hd, gap, Lm = 7, 8, 1, 196, 96, 1, 0
+    elif case == "cross_pad":  # MFMA beam-cross kernel (attn_xdec_bf16) with padded memory keys
+        B, H, Nq, Nk, hd, gap, Lm = 4, 8, 5, 150, 96, 0, 0
+        pad = torch.zeros(B, Nk, dtype=torch.bool, device="cuda")
+        pad[1, 70:] = True   # a wave's whole key range padded
+        pad[3, ::3] = True
+    elif case == "cross_hd128_q16":  # 16 queries (one full MFMA query tile), hd 128
+        B, H, Nq, Nk, hd, gap, Lm = 3, 4, 16, 200, 128, 0, 0
     else:
         B, H, Nq, Nk, hd, gap, Lm = 5, 12, 8, 256, 64, 0, 0
     D = H * hd
