@@ -218,6 +218,121 @@ __device__ __forceinline__ void load_q_frags(const AttnArgs& a, const bf16* qsrc
   }
 }
 
+// One 16-query tile of the forward: S^T = K Q^T from the staged K image, online softmax over
+// 32-key chunks, O^T = V^T P^T, O and lse stored.
+template <int HDP, int MODE>
+__device__ __forceinline__ void fwd_qtile(const AttnArgs& a, int b, int h, int qt, int lane, const bf16x8 (&qf)[HDP / 32],
+                                          const bf16* Ks, const bf16* Vs, int NKP) {
+  constexpr bool SW = HDP == 64;
+  constexpr int ST = SW ? 64 : HDP + 16;
+  const int hoff = h * a.hd;
+  const float sl2 = a.scale * kLog2e;  // scores kept in the log2 domain: exp2(s*scale*log2e - max)
+  // Online softmax over 32-key chunks (two 16-key S blocks = one PV MFMA step): only one
+  // chunk of scores is live, so the wave stays far below 128 VGPRs and two workgroups
+  // share a CU (the whole-row version held 16 score blocks and spilled).
+  const int qi = qt * 16 + (lane & 15);
+  // Scores are kept as t = s * sl2 - mref (log2 domain, against a per-query reference
+  // mref).  The reference is set from the first chunk holding a valid key and only moves
+  // when some score exceeds it by more than 8 (p = 2^t <= 256 otherwise): the common chunk
+  // costs one fma + max per score and a wave ballot -- no cross-lane shuffles; the rare
+  // move path reduces the chunk maximum over the query's four lane groups and rescales.
+  // Without dropout the row sum l comes from the PV MFMA itself (an all-ones A operand
+  // against the same bf16 P^T), so no per-score adds either.
+  constexpr bool MFMA_L = !dropm<MODE>();
+  bool have = false;  // the query has a reference (uniform over its lane groups)
+  float mref = 0.f, l = 0.f;
+  f32x4 o[HDP / 16], lacc = {0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.f;
+#pragma unroll
+  for (int db = 0; db < HDP / 16; ++db) o[db] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t * 32 < NKP; ++t) {
+    f32x4 sc[2];
+    const bool hi = (2 * t + 1) * 16 < NKP;  // the chunk's upper 16 keys are staged
+    float lm = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int kb = 2 * t + c;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      if (c == 0 || hi) {
+#pragma unroll
+        for (int s = 0; s < HDP / 32; ++s) {
+          const int row = kb * 16 + (lane & 15), col = s * 32 + 8 * (lane >> 4);
+          bf16x8 kf = *(const bf16x8*)(Ks + (SW ? swz_off(row, col) : row * ST + col));
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s], acc, 0, 0, 0);
+        }
+      }
+      if (!fullk<MODE>(a, kb)) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kb * 16 + (lane >> 4) * 4 + r;
+          acc[r] = kok<MODE>(a, b, key, qi) ? acc[r] : -INFINITY;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        acc[r] = fmaf(acc[r], sl2, -mref);
+        lm = fmaxf(lm, acc[r]);
+      }
+      sc[c] = acc;
+    }
+    if (__builtin_amdgcn_ballot_w64(lm > 8.f || (!have && lm > -INFINITY))) {
+      float cm = lm;
+      cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+      cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+      const bool move = cm > 8.f || (!have && cm > -INFINITY);
+      if (move) {  // new reference mref + cm: rescale what was accumulated against the old one
+        const float alpha = have ? fexp2(-cm) : 0.f;
+        mref += cm;
+        have = true;
+        l *= alpha;
+        lacc *= alpha;
+#pragma unroll
+        for (int db = 0; db < HDP / 16; ++db) o[db] *= alpha;
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sc[c][r] -= cm;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = fexp2(sc[c][r]);
+        if constexpr (!MFMA_L) {
+          l += p;  // the normaliser excludes dropout
+          sc[c][r] = p * pdrop(a, b, h, qi, (2 * t + c) * 16 + (lane >> 4) * 4 + r);
+        } else {
+          sc[c][r] = p;
+        }
+      }
+    const bf16x8 pb = pack8(sc[0], sc[1]);
+#pragma unroll
+    for (int db = 0; db < HDP / 16; ++db)  // O^T += V^T P^T, V^T fragments by transposed LDS reads
+      o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+          SW ? tr_read8_sw(Vs, 32 * t, db * 16, lane, hi) : tr_read8(Vs, ST, 32 * t, db * 16, lane), pb, o[db], 0, 0, 0);
+    if constexpr (MFMA_L) lacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb, lacc, 0, 0, 0);
+  }
+  if constexpr (MFMA_L) {
+    l = lacc[0];  // every row of the ones product holds the query's sum over all keys
+  } else {
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+  }
+  if (qi < a.Nq) {
+    const float inv = 1.f / l;
+    bf16* orow = (bf16*)a.out + (int64_t)b * a.out_bs + (int64_t)qi * a.out_rs + hoff;
+#pragma unroll
+    for (int db = 0; db < HDP / 16; ++db) {
+      const int d0 = db * 16 + (lane >> 4) * 4;
+      if (d0 < a.hd) store4(orow + d0, o[db], inv);
+    }
+    if ((lane >> 4) == 0) a.lse[((int64_t)b * a.H + h) * a.Nq + qi] = (mref + __log2f(l)) * kLn2;
+  }
+}
+
 // 8 waves over the 16-query tiles; HDP 64 is held to 80 VGPRs so that three workgroups
 // (52 KiB of swizzled K/V each) share a CU.  (Measured: one wave per tile -- 13-wave
 // workgroups, two per CU -- 130 us vs 101 us on the ViT layer: fewer, longer-staging
@@ -245,113 +360,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HDP == 64 ?
   }
   __syncthreads();
 
-  const float sl2 = a.scale * kLog2e;  // scores kept in the log2 domain: exp2(s*scale*log2e - max)
-  // Online softmax over 32-key chunks (two 16-key S blocks = one PV MFMA step): only one
-  // chunk of scores is live, so the wave stays far below 128 VGPRs and two workgroups
-  // share a CU (the whole-row version held 16 score blocks and spilled).
   for (int qt = wave; qt * 16 < a.Nq; qt += nwaves) {
     if (qt != wave) load_q_frags<HDP>(a, qsrc, qt, lane, qf);
-    const int qi = qt * 16 + (lane & 15);
-    // Scores are kept as t = s * sl2 - mref (log2 domain, against a per-query reference
-    // mref).  The reference is set from the first chunk holding a valid key and only moves
-    // when some score exceeds it by more than 8 (p = 2^t <= 256 otherwise): the common chunk
-    // costs one fma + max per score and a wave ballot -- no cross-lane shuffles; the rare
-    // move path reduces the chunk maximum over the query's four lane groups and rescales.
-    // Without dropout the row sum l comes from the PV MFMA itself (an all-ones A operand
-    // against the same bf16 P^T), so no per-score adds either.
-    constexpr bool MFMA_L = !dropm<MODE>();
-    bool have = false;  // the query has a reference (uniform over its lane groups)
-    float mref = 0.f, l = 0.f;
-    f32x4 o[HDP / 16], lacc = {0.f, 0.f, 0.f, 0.f};
-    bf16x8 ones;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.f;
-#pragma unroll
-    for (int db = 0; db < HDP / 16; ++db) o[db] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    for (int t = 0; t * 32 < NKP; ++t) {
-      f32x4 sc[2];
-      const bool hi = (2 * t + 1) * 16 < NKP;  // the chunk's upper 16 keys are staged
-      float lm = -INFINITY;
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int kb = 2 * t + c;
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        if (c == 0 || hi) {
-#pragma unroll
-          for (int s = 0; s < HDP / 32; ++s) {
-            const int row = kb * 16 + (lane & 15), col = s * 32 + 8 * (lane >> 4);
-            bf16x8 kf = *(const bf16x8*)(Ks + (SW ? swz_off(row, col) : row * ST + col));
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s], acc, 0, 0, 0);
-          }
-        }
-        if (!fullk<MODE>(a, kb)) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int key = kb * 16 + (lane >> 4) * 4 + r;
-            acc[r] = kok<MODE>(a, b, key, qi) ? acc[r] : -INFINITY;
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          acc[r] = fmaf(acc[r], sl2, -mref);
-          lm = fmaxf(lm, acc[r]);
-        }
-        sc[c] = acc;
-      }
-      if (__builtin_amdgcn_ballot_w64(lm > 8.f || (!have && lm > -INFINITY))) {
-        float cm = lm;
-        cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
-        cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
-        const bool move = cm > 8.f || (!have && cm > -INFINITY);
-        if (move) {  // new reference mref + cm: rescale what was accumulated against the old one
-          const float alpha = have ? fexp2(-cm) : 0.f;
-          mref += cm;
-          have = true;
-          l *= alpha;
-          lacc *= alpha;
-#pragma unroll
-          for (int db = 0; db < HDP / 16; ++db) o[db] *= alpha;
-#pragma unroll
-          for (int c = 0; c < 2; ++c)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) sc[c][r] -= cm;
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = fexp2(sc[c][r]);
-          if constexpr (!MFMA_L) {
-            l += p;  // the normaliser excludes dropout
-            sc[c][r] = p * pdrop(a, b, h, qi, (2 * t + c) * 16 + (lane >> 4) * 4 + r);
-          } else {
-            sc[c][r] = p;
-          }
-        }
-      const bf16x8 pb = pack8(sc[0], sc[1]);
-#pragma unroll
-      for (int db = 0; db < HDP / 16; ++db)  // O^T += V^T P^T, V^T fragments by transposed LDS reads
-        o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-            SW ? tr_read8_sw(Vs, 32 * t, db * 16, lane, hi) : tr_read8(Vs, ST, 32 * t, db * 16, lane), pb, o[db], 0, 0, 0);
-      if constexpr (MFMA_L) lacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb, lacc, 0, 0, 0);
-    }
-    if constexpr (MFMA_L) {
-      l = lacc[0];  // every row of the ones product holds the query's sum over all keys
-    } else {
-      l += __shfl_xor(l, 16, 64);
-      l += __shfl_xor(l, 32, 64);
-    }
-    if (qi < a.Nq) {
-      const float inv = 1.f / l;
-      bf16* orow = (bf16*)a.out + (int64_t)b * a.out_bs + (int64_t)qi * a.out_rs + hoff;
-#pragma unroll
-      for (int db = 0; db < HDP / 16; ++db) {
-        const int d0 = db * 16 + (lane >> 4) * 4;
-        if (d0 < a.hd) store4(orow + d0, o[db], inv);
-      }
-      if ((lane >> 4) == 0) a.lse[((int64_t)b * a.H + h) * a.Nq + qi] = (mref + __log2f(l)) * kLn2;
-    }
+    fwd_qtile<HDP, MODE>(a, b, h, qt, lane, qf, Ks, Vs, NKP);
   }
 }
 

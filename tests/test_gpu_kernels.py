@@ -144,10 +144,10 @@ def _attn_ref(q, k, v, scale, causal, key_pad):
 @cuda
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("case", ["vit", "dec_self", "dec_cross_gap", "clip", "vit_stream", "pad_stream",
-                                  "causal_stream"])
+                                  "causal_stream", "clip_stream_gap"])
 def test_attention_fwd_bwd(ops, dtype, case):
-    """*_stream cases have >= 1024 (batch, head) pairs: the bf16 forward runs the persistent
-    streaming kernel (attn_fwd_stream_bf16); the others the per-head kernel."""
+    """Per-(batch, head) kernels at the config shapes and at >= 1024 (batch, head) pairs
+    (*_stream; clip_stream_gap: a gap row between images, Nq = 50)."""
     from capk.ops import HeadView
     g = torch.Generator(device="cuda").manual_seed(5)
     if case == "vit_stream":
@@ -156,6 +156,8 @@ def test_attention_fwd_bwd(ops, dtype, case):
         B, H, Nq, Nk, hd, causal, gap = 128, 8, 50, 50, 64, False, 1
     elif case == "causal_stream":
         B, H, Nq, Nk, hd, causal, gap = 128, 8, 40, 40, 64, True, 0
+    elif case == "clip_stream_gap":
+        B, H, Nq, Nk, hd, causal, gap = 90, 12, 50, 50, 64, False, 1
     elif case == "vit":
         B, H, Nq, Nk, hd, causal, gap = 3, 4, 197, 197, 64, False, 0
     elif case == "dec_self":
