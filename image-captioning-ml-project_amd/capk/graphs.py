@@ -24,6 +24,7 @@ What a replay relies on:
 CAPK_GRAPHS=0 disables the replay (the eager loops run; results are identical).
 """
 import os
+import threading
 from collections import OrderedDict
 
 import torch
@@ -35,6 +36,7 @@ ENABLED = os.environ.get("CAPK_GRAPHS", "1") != "0"
 CHUNK = 4
 MAX_RUNNERS = 6
 _RUNNERS = OrderedDict()
+_CAPTURE_LOCK = threading.Lock()
 
 
 def active():
@@ -75,12 +77,16 @@ def _replay(runner, key, body):
     chunks before it really left live."""
     ent = runner.graphs.get(key)
     if ent is None:
-        if runner.pool is None:
-            runner.pool = torch.cuda.graph_pool_handle()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=runner.pool):
-            body()
-        ent = runner.graphs[key] = (g, _host_state(runner))
+        # thread_local + one capture at a time: the SCST update runs the baseline search on a
+        # side thread while the main thread keeps launching the sampler on its own stream
+        # (capk.train.scst); two captures in flight at once are refused by the runtime
+        with _CAPTURE_LOCK:
+            if runner.pool is None:
+                runner.pool = torch.cuda.graph_pool_handle()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=runner.pool, capture_error_mode="thread_local"):
+                body()
+            ent = runner.graphs[key] = (g, _host_state(runner))
     g, after = ent
     g.replay()
     if after[0] is not None:

@@ -24,6 +24,7 @@ _calculate_rewards (src/train/trainer.py:319-484) with the SURVEY fixes:
         re-decode of the prefix computes the same last-position logits (no dropout in the
         sampler, the hidden state of a prefix does not depend on later tokens).
 """
+import os
 import threading
 import time
 
@@ -35,6 +36,19 @@ from ..cider import cider_d
 from .losses import _padded_base
 
 EOS_CHECK_EVERY = 4  # sampled steps between host checks of the all-EOS stop rule
+# the baseline search runs on a side stream (its own host thread) concurrently with the
+# sampler: both decode loops are chains of small latency-bound launches that leave most CUs
+# idle (CAPK_SCST_CONCURRENT=0: one after the other)
+CONCURRENT = os.environ.get("CAPK_SCST_CONCURRENT", "1") != "0"
+_SIDE = {}
+_WARM = set()
+
+
+def _side_stream(dev):
+    s = _SIDE.get(dev)
+    if s is None:
+        s = _SIDE[dev] = torch.cuda.Stream(device=dev)
+    return s
 
 PG_IGNORE = -100
 
@@ -208,8 +222,35 @@ def scst_step(model, images, references, optimizer, lr, seed, max_length=20, bas
     enc = model.encoder(images)
     ph.mark("encoder")
     enc_nograd = {k: (v.detach() if torch.is_tensor(v) else v) for k, v in enc.items()}
+    # Concurrent decode loops once this decoder's runners, graphs and fp8 weight copies exist
+    # (the first update runs them one after the other: lazily created state is never shared
+    # between the two threads); the stale fp8 copies are re-quantised here, before the fork.
+    key = (id(dec), images.device)
+    concurrent = CONCURRENT and images.is_cuda and key in _WARM
+    side_out = {}
+    if concurrent:
+        ops.FP8.refresh()
+        main = torch.cuda.current_stream()
+        side = _side_stream(images.device)
+        side.wait_stream(main)
+
+        def run_baseline():
+            try:
+                with torch.cuda.stream(side), torch.no_grad():
+                    side_out["ids"] = dec.generate(enc_nograd, max_length, **(baseline_kwargs or {}))[0]
+            except BaseException as ex:  # re-raised on the main thread
+                side_out["err"] = ex
+
+        th_base = threading.Thread(target=run_baseline)
+        th_base.start()
     ids, _ = sample_captions(dec, enc_nograd, max_length, seed)
     ph.mark("sample")
+    if concurrent:
+        th_base.join()
+        if "err" in side_out:
+            raise side_out["err"]
+        main.wait_stream(side)
+        side_out["ids"].record_stream(main)
     eos, pad, bos = dec.eos_token_id, dec.pad_token_id, dec.bos_token_id
     refs = [[list(x) for x in rs] for rs in references]
     host = {"ms": 0.0}
@@ -234,8 +275,11 @@ def scst_step(model, images, references, optimizer, lr, seed, max_length=20, bas
         return th, out
 
     th_s, out_s = score_async(ids)  # the samples are scored during the baseline search
-    with torch.no_grad():
-        base_ids, _ = dec.generate(enc_nograd, max_length, **(baseline_kwargs or {}))
+    if concurrent:
+        base_ids = side_out["ids"]
+    else:
+        with torch.no_grad():
+            base_ids, _ = dec.generate(enc_nograd, max_length, **(baseline_kwargs or {}))
     ph.mark("baseline")
     th_b, out_b = score_async(base_ids)  # the baselines during the teacher-forced forward
     from ..models.decoders import GPT2Decoder, LSTMDecoder
@@ -260,4 +304,5 @@ def scst_step(model, images, references, optimizer, lr, seed, max_length=20, bas
     optimizer.step(lr=lr)
     ph.mark("optimizer")
     ph.close(host_ms)
+    _WARM.add(key)
     return loss.detach(), float(np.mean(r_s)), float(np.mean(r_b))

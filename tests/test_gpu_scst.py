@@ -141,3 +141,35 @@ def test_scst_sampling_and_update_vs_oracle():
         gref = pr[n].grad
         torch.testing.assert_close(prm._capk_grad.cpu(), gref, rtol=2e-3, atol=2e-3 * float(gref.abs().max()) + 1e-8,
                                    msg=lambda m: f"{n}: {m}")
+
+
+@cuda
+def test_scst_concurrent_baseline_equals_sequential():
+    """The baseline search on a side stream / host thread, concurrent with the sampler
+    (capk.train.scst.CONCURRENT, from a decoder's second update on), gives exactly the
+    sequential update: same losses and rewards over three updates (eager first, then graph
+    capture and replay of both decode loops while the other runs)."""
+    from capk import graphs
+    from capk.train import CapkAdamW
+    from capk.train import scst as S
+    refs = [[[3, 5, 7, 9]], [[1, 2, 3]], [[4, 4, 8, 15, 16]]]
+    out = {}
+    old = S.CONCURRENT
+    try:
+        for mode in (False, True):
+            S.CONCURRENT = mode
+            S._WARM.clear()
+            graphs.clear()
+            z, model, store, cfg = _tiny()
+            images = torch.from_numpy(z["in/images"]).cuda()
+            opt = CapkAdamW(store, lr=1e-3, weight_decay=0.0)
+            res = []
+            for it in range(3):
+                loss, rs, rb = S.scst_step(model, images, refs, opt, lr=1e-3, max_length=9, seed=100 + it)
+                res.append((float(loss), rs, rb))
+            out[mode] = res
+    finally:
+        S.CONCURRENT = old
+        S._WARM.clear()
+        graphs.clear()
+    assert out[True] == out[False], out
