@@ -384,9 +384,10 @@ def run_config5(args, world, rank, device):
                      "gemm_share_of_step": round(gem["total_ms"] / (elapsed * 1e3), 3)},
         "model_flops": {"per_image": fpi, "tflops": round(fpi * value / world / 1e12, 1)},
         "phases_ms": dict(phase_ms, note="GPU ms per update between HIP events on the compute stream (2 extra "
-                                         "untimed updates); cider_host = host CIDEr-D scoring on two host threads, "
-                                         "overlapped with the baseline search (samples) and the "
-                                         "teacher-forced forward (baselines)"),
+                                         "untimed updates); the beam-4 baseline search runs on a side stream "
+                                         "concurrently with the sampler, so 'baseline' is only its tail after "
+                                         "sampling ends; cider_host = host CIDEr-D scoring on two host threads, "
+                                         "overlapped with the rest of the update"),
         "final_loss": round(float(loss), 5), "reward_sample": round(rs, 4), "reward_baseline": round(rb, 4),
         "process_group": process_group(world),
     }
