@@ -225,13 +225,14 @@ def scst_step(model, images, references, optimizer, lr, seed, max_length=20, bas
     # Concurrent decode loops once this decoder's runners, graphs and fp8 weight copies exist
     # (the first update runs them one after the other: lazily created state is never shared
     # between the two threads); the stale fp8 copies are re-quantised here, before the fork.
-    key = (id(dec), images.device)
-    concurrent = CONCURRENT and images.is_cuda and key in _WARM
+    dev = next(v.device for v in enc_nograd.values() if torch.is_tensor(v))  # (images may be None: a stub encoder)
+    key = (id(dec), dev)
+    concurrent = CONCURRENT and dev.type == "cuda" and key in _WARM
     side_out = {}
     if concurrent:
         ops.FP8.refresh()
         main = torch.cuda.current_stream()
-        side = _side_stream(images.device)
+        side = _side_stream(dev)
         side.wait_stream(main)
 
         def run_baseline():
