@@ -20,7 +20,7 @@ import torch.nn as nn
 from .. import ops
 from .._lib import ACT_QUICK_GELU
 from ..params import Fused
-from .common import G, CapkModule, W, mark
+from .common import G, CapkModule, W, join_dw, mark
 from .vit import _ViTLayerFn
 
 CLIP_ARCHS = {
@@ -179,6 +179,7 @@ class _CLIPEmbedFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dx):
+        join_dw(dx.device)  # the layers' weight gradients (side stream) are complete from here on
         m, B, Np = ctx.m, ctx.B, ctx.Np
         D = m.arch["hidden_size"]
         patches, x0, mu, rs = ctx.saved

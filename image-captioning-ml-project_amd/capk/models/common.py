@@ -7,6 +7,8 @@ gradients straight into the flat fp32 gradient buffer of the ParamStore
 (``p._capk_grad``) and returns only the activation gradient; one parameter per
 block is passed as an "anchor" input so autograd schedules the backward.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -70,20 +72,67 @@ class CapkModule(nn.Module):
                                "capk.prepare(model, device) before running the model")
 
 
+# Weight-gradient side stream: a layer's dW = dY^T X (and its bias column sums) depends on
+# nothing the rest of the backward produces, so the encoder layers issue it on a second HIP
+# stream and the dX chain (attention backward, LayerNorm backward, column sums: memory- or
+# latency-bound kernels that leave the MFMAs idle) proceeds on the compute stream meanwhile.
+# join_dw() makes the compute stream wait before the gradients are read (the patch-embedding
+# backward, the optimizer).  Off under multi-rank DP (the bucketer launches a layer's
+# all-reduce as soon as it is notified) and with CAPK_DW_STREAM=0.
+DW_STREAM = os.environ.get("CAPK_DW_STREAM", "1") != "0"
+_DW_SIDE = {}
+_DW_PENDING = set()
+
+
+def _dw_side_on():
+    if not DW_STREAM:
+        return False
+    import torch.distributed as dist
+    return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+
+
+def join_dw(device=None):
+    """Make the current stream wait for the weight gradients issued on the side stream."""
+    for dev in list(_DW_PENDING):
+        if device is None or dev == device:
+            torch.cuda.current_stream(dev).wait_stream(_DW_SIDE[dev])
+            _DW_PENDING.discard(dev)
+
+
 def linear_bwd(dy, x, w_param, b_param, dtype, *, fused=None, need_dx=True, act_bwd=0, aux=None,
-               dw_accumulate=False, drop=(0.0, 0), dsum=None):
+               dw_accumulate=False, drop=(0.0, 0), dsum=None, side_dw=False):
     """Backward of y = x W^T + b: dW, db into the grad buffer; returns dX (or None).
     dsum: with act_bwd, the column sums of the returned dX (the bias gradient of the Linear
-    below the activation) are written there, fused into the activation pass."""
+    below the activation) are written there, fused into the activation pass.
+    side_dw: dW / db on the weight-gradient side stream (see join_dw)."""
     if fused is not None:
         wmat, gw = fused[0].w(dtype), fused[0].grad
         gb = fused[1].grad if fused[1] is not None else None
     else:
         wmat, gw = W(w_param, dtype), G(w_param)
         gb = G(b_param) if b_param is not None else None
-    ops.linear_dw(dy, x, gw, accumulate=dw_accumulate)
-    if gb is not None:
-        ops.colsum(dy, gb, accumulate=dw_accumulate)
+    if side_dw and dy.is_cuda and _dw_side_on():
+        dev = dy.device
+        side = _DW_SIDE.get(dev)
+        if side is None:
+            side = _DW_SIDE[dev] = torch.cuda.Stream(device=dev)
+        if dev not in _DW_PENDING:
+            # also join at the end of this backward pass, so that code reading the gradients
+            # between backward() and the optimizer (clipping, a partially frozen encoder whose
+            # embedding backward never runs, the end of a graph capture) sees them complete
+            torch.autograd.Variable._execution_engine.queue_callback(lambda: join_dw(dev))
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            ops.linear_dw(dy, x, gw, accumulate=dw_accumulate)
+            if gb is not None:
+                ops.colsum(dy, gb, accumulate=dw_accumulate)
+        dy.record_stream(side)  # the compute stream may free these before the side stream is done
+        x.record_stream(side)
+        _DW_PENDING.add(dev)
+    else:
+        ops.linear_dw(dy, x, gw, accumulate=dw_accumulate)
+        if gb is not None:
+            ops.colsum(dy, gb, accumulate=dw_accumulate)
     if not need_dx:
         return None
     return ops.linear_dx(dy, wmat, act_bwd=act_bwd, aux=aux, drop=drop, dsum=dsum)

@@ -23,7 +23,7 @@ import torch.nn as nn
 from .. import ops
 from .._lib import ACT_DERIV, ACT_GELU_ERF, ACT_TANH
 from ..params import Fused, notify_final, store_of
-from .common import G, CapkModule, W, heads, linear_bwd, mark
+from .common import G, CapkModule, W, heads, join_dw, linear_bwd, mark
 
 VIT_ARCHS = {
     # pretrained_model_name -> architecture (weights are random-init offline or loaded from a checkpoint)
@@ -191,6 +191,7 @@ class _ViTEmbedFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dx):
+        join_dw(dx.device)  # the layers' weight gradients (side stream) are complete from here on
         m, B, Np = ctx.m, ctx.B, ctx.Np
         D = m.arch["hidden_size"]
         dx = dx.contiguous()
@@ -254,18 +255,18 @@ class _ViTLayerFn(torch.autograd.Function):
         fused_b2 = getattr(L, "_capk_fc2_bias_done", False)
         L._capk_fc2_bias_done = False
         # FC1's bias gradient = colsum(dfp), fused into the GELU' pass that produces dfp
-        dfp = linear_bwd(dy, f, fc2.weight, None if fused_b2 else fc2.bias, dt, act_bwd=act | ACT_DERIV, aux=f_pre,
+        dfp = linear_bwd(dy, f, fc2.weight, None if fused_b2 else fc2.bias, dt, act_bwd=act | ACT_DERIV, aux=f_pre, side_dw=True,
                          dsum=G(fc1.bias))
-        dh2 = linear_bwd(dfp, h2, fc1.weight, None, dt)
+        dh2 = linear_bwd(dfp, h2, fc1.weight, None, dt, side_dw=True)
         # dx1 = the O projection's output gradient: its column sums (O bias grad) come out of the LN kernel
         dx1 = ops.layernorm_bwd(dh2, x1, ln2.weight.detach(), mu2, rs2, G(ln2.weight), G(ln2.bias), dres=dy,
                                 dsum=G(at.o_proj.bias))
-        do = linear_bwd(dx1, o, at.o_proj.weight, None, dt)
+        do = linear_bwd(dx1, o, at.o_proj.weight, None, dt, side_dw=True)
         dqkv = torch.empty_like(qkv)
         ops.attention_bwd(heads(qkv, 0, B, N), heads(qkv, D, B, N), heads(qkv, 2 * D, B, N), heads(o, 0, B, N),
                           heads(do, 0, B, N), lse, heads(dqkv, 0, B, N), heads(dqkv, D, B, N),
                           heads(dqkv, 2 * D, B, N), B, H, N, N, hd, 1.0 / math.sqrt(hd))
-        dh1 = linear_bwd(dqkv, h1, None, None, dt, fused=(at.qkv_w, at.qkv_b))
+        dh1 = linear_bwd(dqkv, h1, None, None, dt, fused=(at.qkv_w, at.qkv_b), side_dw=True)
         prev = getattr(L, "_capk_prev", None)
         dx = ops.layernorm_bwd(dh1, x, ln1.weight.detach(), mu1, rs1, G(ln1.weight), G(ln1.bias), dres=dx1,
                                dsum=G(prev.fc2.bias) if prev is not None else None)

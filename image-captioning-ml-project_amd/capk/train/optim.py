@@ -81,6 +81,8 @@ class CapkAdamW:
 
     def step(self, lr=None):
         """One AdamW step; `lr` overrides the groups' current learning rate for this step."""
+        from ..models.common import join_dw
+        join_dw()  # (weight gradients still in flight on the side stream, if any)
         st = self.store
         for g, pg in zip(self.GROUP_KEYS, self.param_groups):
             glr = pg["lr"] if lr is None else lr
