@@ -77,9 +77,12 @@ class CapkModule(nn.Module):
 # stream and the dX chain (attention backward, LayerNorm backward, column sums: memory- or
 # latency-bound kernels that leave the MFMAs idle) proceeds on the compute stream meanwhile.
 # join_dw() makes the compute stream wait before the gradients are read (the patch-embedding
-# backward, the optimizer).  Off under multi-rank DP (the bucketer launches a layer's
-# all-reduce as soon as it is notified) and with CAPK_DW_STREAM=0.
-DW_STREAM = os.environ.get("CAPK_DW_STREAM", "1") != "0"
+# backward, the optimizer).  Opt-in (CAPK_DW_STREAM=1), and off under multi-rank DP (the
+# bucketer launches a layer's all-reduce as soon as it is notified).  Measured on config 3 it
+# gains 0.9 % per step, but the side-stream GEMMs share the CUs with the dX chain, so their
+# launch durations stretch and the per-GEMM roofline reading falls 0.34 -> 0.26 of peak; the
+# default keeps one stream ("tried and not kept").
+DW_STREAM = os.environ.get("CAPK_DW_STREAM", "0") == "1"
 _DW_SIDE = {}
 _DW_PENDING = set()
 

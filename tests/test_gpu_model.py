@@ -98,6 +98,27 @@ def test_golden_step_fp32(golden_dir):
 
 
 @cuda
+def test_golden_grads_dw_side_stream(golden_dir, monkeypatch):
+    """Opt-in weight-gradient side stream (CAPK_DW_STREAM=1): the same golden gradients, read
+    straight after backward() with no explicit synchronisation (the end-of-backward join must
+    order them on the compute stream)."""
+    from capk.models import common
+    from capk.train import CombinedLoss
+    monkeypatch.setattr(common, "DW_STREAM", True)
+    z = np.load(os.path.join(golden_dir, "vit_transformer_step.npz"), allow_pickle=False)
+    model, store, cfg = _tiny_model(z, "fp32")
+    caps = torch.from_numpy(z["in/captions"]).cuda()
+    out = model(images=torch.from_numpy(z["in/images"]).cuda(), captions=caps)
+    CombinedLoss(cfg.model.pad_token_id)(out["logits"], caps)["total_loss"].backward()
+    assert not common._DW_PENDING
+    named = dict(model.named_parameters())
+    for k in z.files:
+        if k.startswith("grad/"):
+            np.testing.assert_allclose(named[k[5:]]._capk_grad.cpu().numpy(), z[k], rtol=2e-4, atol=2e-6,
+                                       err_msg=k[5:])
+
+
+@cuda
 def test_golden_greedy_generate_fp32(golden_dir):
     z = np.load(os.path.join(golden_dir, "vit_transformer_step.npz"), allow_pickle=False)
     model, store, cfg = _tiny_model(z, "fp32")
