@@ -43,6 +43,8 @@ SHAPES = [  # name, M, N, K, kind
     ("dec_fc1_dx", 5120, 768, 3072, "dx"), ("dec_qkv_fwd", 5120, 2304, 768, "fwd"),
     ("dec_fc1_fwd_deriv", 5120, 3072, 768, "fwd_gelu_deriv"), ("dec_fc2_dx_deriv", 5120, 3072, 768, "dx_gelu_deriv"),
     ("dec_o_dw", 5120, 768, 768, "dw"), ("dec_fc1_dw", 5120, 3072, 768, "dw"),
+    # config-2 LSTM cell step (B = 128, hidden 768, 4 gates): gates = h W_hh^T, dh = dG W_hh
+    ("lstm_gates_fwd", 128, 3072, 768, "fwd"), ("lstm_dh_dx", 128, 768, 3072, "dx"),
 ]
 
 
