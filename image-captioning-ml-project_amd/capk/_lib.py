@@ -94,6 +94,8 @@ SIGNATURES = {
                                _c_p, _c_p, _c_p]),
     "capk_attention_probs_mean": (_i, [_i, _i, _i, _i, _i, _i, _f, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _c_p,
                                        _c_p, _c_p]),
+    "capk_attention_probs_mean_bwd": (_i, [_i, _i, _i, _i, _i, _i, _f, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p,
+                                           _c_p, _c_p, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p]),
     "capk_beam_state_bytes": (_sz, [_i, _i, _i]),
     "capk_beam_init": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _sz, _c_p]),
     "capk_beam_step": (_i, [_i, _i, _i, _i, _i, _i64, _c_p, _i, _i64, _f, _f, _i, _c_p, _sz, _c_p, _c_p, _c_p]),

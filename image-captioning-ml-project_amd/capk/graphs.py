@@ -37,6 +37,7 @@ CHUNK = 4
 MAX_RUNNERS = 6
 _RUNNERS = OrderedDict()
 _CAPTURE_LOCK = threading.Lock()
+_RUNNERS_LOCK = threading.RLock()  # the SCST sampler and the baseline-search thread share the cache
 
 
 def active():
@@ -46,20 +47,25 @@ def active():
 def runner_for(m, key, make):
     """The cached runner of decoder `m` for `key` (created by `make()` on first use)."""
     k = (id(m), key)
-    r = _RUNNERS.get(k)
-    if r is None:
-        r = make()
-        r.graphs, r.pool, r.warm, r.owner = {}, None, False, m
-        _RUNNERS[k] = r
-        while len(_RUNNERS) > MAX_RUNNERS:
-            _RUNNERS.popitem(last=False)
-    else:
-        _RUNNERS.move_to_end(k)
-    return r
+    with _RUNNERS_LOCK:
+        r = _RUNNERS.get(k)
+        if r is not None and r.owner is not m:  # id() reused by a new decoder: stale entry
+            del _RUNNERS[k]
+            r = None
+        if r is None:
+            r = make()
+            r.graphs, r.pool, r.warm, r.owner = {}, None, False, m
+            _RUNNERS[k] = r
+            while len(_RUNNERS) > MAX_RUNNERS:
+                _RUNNERS.popitem(last=False)
+        else:
+            _RUNNERS.move_to_end(k)
+        return r
 
 
 def clear():
-    _RUNNERS.clear()
+    with _RUNNERS_LOCK:
+        _RUNNERS.clear()
 
 
 def _host_state(runner):

@@ -13,8 +13,9 @@ step (the reference recomputes it every step; the values are identical):
   step_bwd(H, t, dctx, ...)            its backward, accumulating key/value grads
   finish_bwd(H, Q)                     per-image backward        -> d features
 
-``forward(query, key, value, key_padding_mask)`` keeps the reference's standalone
-contract (one query per image) via the same protocol.
+``forward(query, key, value, key_padding_mask, **kw)`` keeps the reference's standalone
+contract (query [B, D] or [B, Q, D], key-padding mask, AdaptiveAttention's memory_state /
+cell_state, differentiable returned weights) via the same protocol, one step per query.
 """
 import torch
 import torch.nn as nn
@@ -93,7 +94,7 @@ class SoftAttention(AttentionMechanism, CapkModule):
         H.dbe = torch.zeros(B, dtype=torch.float32, device=dev)
         H.dqp = torch.empty_like(H.qp)
 
-    def step_bwd(self, H, t, dctx, dq_out, dq_residual=None, dc_mem_out=None, dw=None):
+    def step_bwd(self, H, t, dctx, dq_out, dq_residual=None, dc_mem_out=None, dw=None, dh_mem_out=None):
         """Writes dq_out = d(query) (+ dq_residual).  Soft attention does not read the LSTM states.
         dw: optional gradient on the returned weights (fp32 [B, S])."""
         dt = self.cdtype
@@ -138,50 +139,67 @@ class SoftAttention(AttentionMechanism, CapkModule):
 
 
 def _standalone(mod, query, key, value, key_padding_mask, kw):
+    """AttentionMechanism.forward contract (attention.py:12-35): query [B, D] or [B, Q, D],
+    key / value [B, S, D], key_padding_mask bool [B, S] (True = padding); returns
+    (context [B, (Q,) D], weights [B, (Q,) S]).  The Q queries of an image run as Q steps of
+    the hoisted step protocol (the key / value projections are computed once per call),
+    which restates the reference's [B, Q, S, D] broadcast per query."""
     squeeze = query.dim() == 2
-    q = query if squeeze else query.reshape(query.shape[0], -1)
-    if not squeeze and query.shape[1] != 1:
-        raise NotImplementedError("capk attention modules: one query per image (the LSTM decode step)")
-    ctx, w = _StandaloneFn.apply(q.contiguous(), key, value, mod.query_proj.weight, mod, key_padding_mask,
-                                 kw.get("memory_state"), kw.get("cell_state"))
-    if not squeeze:
-        return ctx[:, None], w[:, None]
+    q3 = query[:, None] if squeeze else query
+    if q3.dim() != 3 or key.dim() != 3 or value.dim() != 3:
+        raise ValueError("attention: query [B, D] | [B, Q, D], key / value [B, S, D]")
+    h_mem, c_mem = kw.get("memory_state"), kw.get("cell_state")
+    anchor = next(mod.parameters())
+    ctx, w = _StandaloneFn.apply(q3, key, value, h_mem, c_mem, anchor, mod, key_padding_mask)
+    if squeeze:
+        return ctx[:, 0], w[:, 0]
     return ctx, w
 
 
 class _StandaloneFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx_, q, key, value, anchor, mod, key_padding_mask, h_mem, c_mem):
+    def forward(ctx_, q3, key, value, h_mem, c_mem, anchor, mod, key_padding_mask):
+        dt = mod.cdtype
+        B, Q, D = q3.shape
         kp = key_padding_mask.to(torch.uint8).contiguous() if key_padding_mask is not None else None
-        same = key.data_ptr() == value.data_ptr() and key.stride() == value.stride()
-        H = mod.hoist(key, key if same else value, kp, 1)
-        B, D = q.shape
-        out = torch.empty(B, D, dtype=q.dtype, device=q.device)
-        w = mod.step_fwd(H, 0, q, h_mem, c_mem, out)
-        ctx_.mod, ctx_.H, ctx_.q, ctx_.same = mod, H, q, same
-        ctx_.shapes = (key.shape, value.shape)
-        w = w.clone()
-        if not isinstance(mod, SoftAttention):
-            ctx_.mark_non_differentiable(w)
-        return out, w
+        same = key.data_ptr() == value.data_ptr() and key.stride() == value.stride() and key.shape == value.shape
+        key_c = key.to(dt)
+        val_c = key_c if same else value.to(dt)
+        qt = q3.to(dt).transpose(0, 1).contiguous()  # step-major [Q, B, D]
+        hm = h_mem.to(dt).contiguous() if h_mem is not None else None
+        cm = c_mem.float().contiguous() if c_mem is not None else None
+        H = mod.hoist(key_c, val_c, kp, Q)
+        out = torch.empty(Q, B, D, dtype=dt, device=q3.device)
+        for t in range(Q):
+            mod.step_fwd(H, t, qt[t], hm, cm, out[t])
+        w = H.w.transpose(0, 1).contiguous()  # [B, Q, S]
+        ctx_.mod, ctx_.H, ctx_.qt, ctx_.same, ctx_.hm, ctx_.cm = mod, H, qt, same, hm, cm
+        ctx_.in_dtypes = (q3.dtype, key.dtype, value.dtype,
+                          h_mem.dtype if h_mem is not None else None, c_mem.dtype if c_mem is not None else None)
+        return out.transpose(0, 1).to(q3.dtype), w
 
     @staticmethod
     def backward(ctx_, dout, dw):
-        mod, H, q = ctx_.mod, ctx_.H, ctx_.q
+        mod, H, qt = ctx_.mod, ctx_.H, ctx_.qt
+        dt = mod.cdtype
+        Q, B, D = qt.shape
         mod.begin_bwd(H)
-        dq = torch.empty_like(q)
-        if dout is None:
-            dout = torch.zeros_like(q)
-        if isinstance(mod, SoftAttention):
-            mod.step_bwd(H, 0, dout.contiguous(), dq, dw=dw.float().contiguous() if dw is not None else None)
-        else:
-            # MultiHeadAttention / AoA return head-averaged weights for inspection; like the LSTM decoder's
-            # use of them, they carry no gradient here (a loss on them needs the soft module)
-            mod.step_bwd(H, 0, dout.contiguous(), dq)
-        dk, dv = mod.finish_bwd(H, q)
+        dq = torch.empty(Q, B, D, dtype=dt, device=qt.device)
+        dh = torch.zeros(B, D, dtype=dt, device=qt.device) if ctx_.hm is not None else None
+        dc = torch.zeros(B, D, dtype=torch.float32, device=qt.device) if ctx_.cm is not None else None
+        dout_t = dout.to(dt).transpose(0, 1).contiguous() if dout is not None else torch.zeros_like(qt)
+        dw_t = dw.float().transpose(0, 1).contiguous() if dw is not None else None
+        for t in range(Q):
+            mod.step_bwd(H, t, dout_t[t], dq[t], dc_mem_out=dc, dh_mem_out=dh,
+                         dw=dw_t[t] if dw_t is not None else None)
+        dk, dv = mod.finish_bwd(H, qt.view(Q * B, D))
+        qd, kd, vd, hd_, cd = ctx_.in_dtypes
+        dq3 = dq.transpose(0, 1).to(qd)
+        dh = dh.to(hd_) if dh is not None else None
+        dc = dc.to(cd) if dc is not None else None
         if ctx_.same:
-            return dq, dk, None, None, None, None, None, None
-        return dq, dk, dv, None, None, None, None, None
+            return dq3, dk.to(kd), None, dh, dc, None, None, None
+        return dq3, dk.to(kd), dv.to(vd), dh, dc, None, None, None
 
 
 class MultiHeadAttention(AttentionMechanism, CapkModule):
@@ -245,7 +263,8 @@ class MultiHeadAttention(AttentionMechanism, CapkModule):
         H.dctx = torch.empty_like(H.o)
         H.do = torch.empty(B, D, dtype=dt, device=dev)
 
-    def step_bwd(self, H, t, dctx, dq_out, dq_residual=None, dc_mem_out=None):
+    def step_bwd(self, H, t, dctx, dq_out, dq_residual=None, dc_mem_out=None, dw=None, dh_mem_out=None):
+        """dw: optional gradient on the returned head-mean weights (fp32 [B, S])."""
         dt = self.cdtype
         B, S, D = H.B, H.S, H.D
         ops.copy_rows(dctx, H.dctx[t])
@@ -254,6 +273,10 @@ class MultiHeadAttention(AttentionMechanism, CapkModule):
         ops.attention_bwd(qv, kv, vv, ov, ops.HeadView(H.do, 0, D, D), H.lse[t], ops.HeadView(H.dqh[t], 0, D, D),
                           ops.HeadView(H.sk, 0, S * D, D), ops.HeadView(H.sv, 0, S * D, D), B, self.num_heads, 1, S,
                           self.head_dim, H.scale, key_pad_u8=H.kpu)
+        if dw is not None:  # attention.py:211 weights.mean(dim=1) is differentiable
+            ops.attention_probs_mean_bwd(qv, kv, H.lse[t], dw, ops.HeadView(H.dqh[t], 0, D, D),
+                                         ops.HeadView(H.dK, 0, S * D, D), B, self.num_heads, 1, S, self.head_dim,
+                                         H.scale, key_pad=H.kpu)
         ops.add_rows(H.sk, H.dK, 1, B * S, D, 0, D, 1, 0, 0, D, True)
         ops.add_rows(H.sv, H.dV, 1, B * S, D, 0, D, 1, 0, 0, D, True)
         ops.gemm(H.dqh[t], True, W(self.query_proj.weight, dt), False, B, D, D, dq_out, lda=D, ldb=D,
@@ -345,7 +368,9 @@ class AdaptiveAttention(AttentionMechanism, CapkModule):
         H.dsgpre = torch.empty(steps, B, D, dtype=dt, device=dev)
         H.dsg = torch.empty(B, D, dtype=dt, device=dev)
 
-    def step_bwd(self, H, t, dctx, dq_out, dq_residual=None, dc_mem_out=None):
+    def step_bwd(self, H, t, dctx, dq_out, dq_residual=None, dc_mem_out=None, dw=None, dh_mem_out=None):
+        """dc_mem_out (fp32) and dh_mem_out ACCUMULATE; without dh_mem_out the memory-state half
+        of the sentinel gate goes to dq_out (the LSTM decoder passes h_top as both)."""
         dt = self.cdtype
         B, D = H.B, H.D
         ops.gate_mix_bwd(H.cat2[t][:, :D], H.cat2[t][:, D:], self.adaptive_weight.weight.detach().view(-1),
@@ -355,11 +380,10 @@ class AdaptiveAttention(AttentionMechanism, CapkModule):
             raise RuntimeError("AdaptiveAttention needs the cell-state gradient buffer")
         ops.tanh_gate_bwd(H.c[t], H.sg[t], dsin, H.dsg, dc_mem_out)
         ops.act_bwd(H.dsg, H.sgpre[t], ops_act.SIGMOID, out=H.dsgpre[t])
-        self.base_attention.step_bwd(H.base, t, H.dctxb, dq_out, dq_residual)
-        wsg = W(self.sentinel_gate.weight, dt)  # [D, 2D]: query half and memory-state half both feed h_top
-        for half in (wsg[:, :D], wsg[:, D:]):
-            ops.gemm(H.dsgpre[t], True, half, False, B, D, D, dq_out, lda=D, ldb=2 * D, ldc=dq_out.stride(0),
-                     beta=1.0)
+        self.base_attention.step_bwd(H.base, t, H.dctxb, dq_out, dq_residual, dw=dw)
+        wsg = W(self.sentinel_gate.weight, dt)  # [D, 2D]: query half, memory-state half
+        for half, dst in ((wsg[:, :D], dq_out), (wsg[:, D:], dq_out if dh_mem_out is None else dh_mem_out)):
+            ops.gemm(H.dsgpre[t], True, half, False, B, D, D, dst, lda=D, ldb=2 * D, ldc=dst.stride(0), beta=1.0)
         return True
 
     def finish_bwd(self, H, Q):
@@ -376,10 +400,11 @@ class AdaptiveAttention(AttentionMechanism, CapkModule):
         return self.base_attention.finish_bwd(H.base, Q)
 
     def forward(self, query, key, value, key_padding_mask=None, memory_state=None, cell_state=None, **kwargs):
+        """attention.py:242-294; memory_state / cell_state [B, D] are shared by the Q queries."""
         assert memory_state is not None and cell_state is not None, \
             "AdaptiveAttention requires memory_state and cell_state"
-        raise NotImplementedError("capk AdaptiveAttention: standalone use outside the LSTM decoder is not supported; "
-                                  "the decoder path runs the step protocol")
+        return _standalone(self, query, key, value, key_padding_mask,
+                           dict(kwargs, memory_state=memory_state, cell_state=cell_state))
 
 
 class AttentionOnAttention(AttentionMechanism, CapkModule):
@@ -427,7 +452,7 @@ class AttentionOnAttention(AttentionMechanism, CapkModule):
         H.tmp = torch.empty(B, D, dtype=dt, device=dev)
         H.dcat = torch.empty(B, 2 * D, dtype=dt, device=dev)
 
-    def step_bwd(self, H, t, dctx, dq_out, dq_residual=None, dc_mem_out=None):
+    def step_bwd(self, H, t, dctx, dq_out, dq_residual=None, dc_mem_out=None, dw=None, dh_mem_out=None):
         dt = self.cdtype
         B, D = H.B, H.D
         iv, ig = self.info_vector_proj[0], self.info_gate_proj[0]
@@ -438,7 +463,7 @@ class AttentionOnAttention(AttentionMechanism, CapkModule):
         ops.linear_dx(H.dipre[t], W(iv.weight, dt), out=H.dcat)
         ops.linear_dx(H.dgpre[t], W(ig.weight, dt), out=H.dcat, beta=1.0)
         ops.copy_rows(H.dcat[:, D:], H.dqa[t])
-        self.base_attention.step_bwd(H.base, t, H.dcat[:, :D], dq_out, dq_residual)
+        self.base_attention.step_bwd(H.base, t, H.dcat[:, :D], dq_out, dq_residual, dw=dw)
         ops.gemm(H.dqa[t], True, W(self.query_proj.weight, dt), False, B, D, D, dq_out, lda=D, ldb=D,
                  ldc=dq_out.stride(0), beta=1.0)
         return False

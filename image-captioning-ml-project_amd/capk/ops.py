@@ -5,6 +5,8 @@ Every function here launches hand-written HIP kernels from libcapk.so on
 allocator), streams and autograd bookkeeping.  There is deliberately no CPU or
 eager-PyTorch fallback: a missing library or a non-GPU tensor raises.
 """
+import threading
+
 import torch
 
 from . import _lib
@@ -51,11 +53,20 @@ class KernelTimer:
 
     def __init__(self):
         self.enabled = False
+        self.thread = None
         self.records = []  # (start_event, end_event, flops, in_dtype, algorithmic HBM bytes)
 
     def start(self):
+        """Record the GEMMs launched by the calling thread only: the config-5 SCST update runs
+        its baseline search on a side stream from a second thread, whose overlapping (and
+        mutually stretched) launches would otherwise be summed into the main stream's."""
         self.records = []
+        self.thread = threading.get_ident()
         self.enabled = True
+
+    def active(self):
+        return (self.enabled and threading.get_ident() == self.thread
+                and not torch.cuda.is_current_stream_capturing())
 
     def stop(self):
         self.enabled = False
@@ -93,7 +104,7 @@ def gemm(A, a_kmajor, B, b_kmajor, M, N, K, C, *, lda, ldb, ldc, alpha=1.0, beta
     it, ot = dtype_code(A), dtype_code(C)
     wsb = L.capk_gemm_workspace(it, ot, M, N, K)
     ws = _ws(wsb, A.device)
-    timed = GEMM_TIMER.enabled and not torch.cuda.is_current_stream_capturing()
+    timed = GEMM_TIMER.active()
     if timed:
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
@@ -148,7 +159,7 @@ class Fp8State:
         captured graph holds the copies' addresses, never the quantisation itself)."""
         if not self.enabled:
             return
-        for key, ent in self.cache.items():  # ent = [epoch, q, scale, bf16 weight view]
+        for key, ent in list(self.cache.items()):  # snapshot: another thread may insert; ent = [epoch, q, scale, view]
             if ent[0] != self.epoch:
                 quant_fp8(ent[3], transpose=key[3], q=ent[1], scale=ent[2])
                 ent[0] = self.epoch
@@ -185,7 +196,7 @@ def gemm_f8(a, sa, b, sb, C, *, beta=0.0, bias=None, residual=None, act=0, preac
     N = b.shape[0]
     wsb = L.capk_gemm_f8_workspace(M, N, K)
     ws = _ws(wsb, a.device)
-    timed = GEMM_TIMER.enabled and not torch.cuda.is_current_stream_capturing()
+    timed = GEMM_TIMER.active()
     if timed:
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
@@ -262,7 +273,7 @@ def linear_dx(dy, w, *, out=None, act_bwd=0, aux=None, beta=0.0, drop=NO_DROP, d
             L = lib()
             wsb = L.capk_gemm_dx_act_colsum_workspace(M, K, N)
             ws = _ws(wsb, dy.device)
-            timed = GEMM_TIMER.enabled and not torch.cuda.is_current_stream_capturing()
+            timed = GEMM_TIMER.active()
             if timed:
                 ev0 = torch.cuda.Event(enable_timing=True)
                 ev1 = torch.cuda.Event(enable_timing=True)
@@ -681,6 +692,19 @@ def attention_probs_mean(q, k, lse, B, H, Nq, Nk, hd, scale, out, key_pad=None):
                                           k.ptr(), k.bs, k.rs, _p(key_pad), _p(lse), _p(out), _stream()),
           "capk_attention_probs_mean")
     return out
+
+
+def attention_probs_mean_bwd(q, k, lse, dw, dq, dk, B, H, Nq, Nk, hd, scale, key_pad=None):
+    """Gradient of attention_probs_mean: dw fp32 [B, Nq, Nk] contiguous; ACCUMULATES into dq
+    (HeadView, model dtype) and dk (HeadView over an fp32 buffer)."""
+    if dw.dtype != torch.float32 or not dw.is_contiguous() or dw.numel() != B * Nq * Nk:
+        raise ValueError("attention_probs_mean_bwd: dw must be contiguous fp32 [B, Nq, Nk]")
+    if dk.t.dtype != torch.float32:
+        raise ValueError("attention_probs_mean_bwd: dk accumulates in fp32")
+    check(lib().capk_attention_probs_mean_bwd(dtype_code(q.t), B, H, Nq, Nk, hd, float(scale), q.ptr(), q.bs, q.rs,
+                                              k.ptr(), k.bs, k.rs, _p(key_pad), _p(lse), _p(dw), dq.ptr(), dq.bs,
+                                              dq.rs, dk.ptr(), dk.bs, dk.rs, _stream()),
+          "capk_attention_probs_mean_bwd")
 
 
 # ------------------------------------------------- convolutional encoder (A3) ---

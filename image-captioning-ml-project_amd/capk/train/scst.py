@@ -28,6 +28,8 @@ import os
 import threading
 import time
 
+import weakref
+
 import numpy as np
 import torch
 
@@ -41,7 +43,7 @@ EOS_CHECK_EVERY = 4  # sampled steps between host checks of the all-EOS stop rul
 # idle (CAPK_SCST_CONCURRENT=0: one after the other)
 CONCURRENT = os.environ.get("CAPK_SCST_CONCURRENT", "1") != "0"
 _SIDE = {}
-_WARM = set()
+_WARM = weakref.WeakKeyDictionary()  # decoder -> set of (device, batch, max_length, baseline kwargs) already run
 
 
 def _side_stream(dev):
@@ -226,8 +228,11 @@ def scst_step(model, images, references, optimizer, lr, seed, max_length=20, bas
     # (the first update runs them one after the other: lazily created state is never shared
     # between the two threads); the stale fp8 copies are re-quantised here, before the fork.
     dev = next(v.device for v in enc_nograd.values() if torch.is_tensor(v))  # (images may be None: a stub encoder)
-    key = (id(dec), dev)
-    concurrent = CONCURRENT and dev.type == "cuda" and key in _WARM
+    # keyed on everything that selects a decode runner / graph / fp8 copy (a new batch size or
+    # max_length builds new ones), held weakly so a new decoder never inherits a dead one's entry
+    key = (dev, int(enc_nograd["features"].shape[0]) if torch.is_tensor(enc_nograd.get("features")) else None,
+           int(max_length), repr(sorted((baseline_kwargs or {}).items())))
+    concurrent = CONCURRENT and dev.type == "cuda" and key in _WARM.get(dec, ())
     side_out = {}
     if concurrent:
         ops.FP8.refresh()
@@ -305,5 +310,5 @@ def scst_step(model, images, references, optimizer, lr, seed, max_length=20, bas
     optimizer.step(lr=lr)
     ph.mark("optimizer")
     ph.close(host_ms)
-    _WARM.add(key)
+    _WARM.setdefault(dec, set()).add(key)
     return loss.detach(), float(np.mean(r_s)), float(np.mean(r_b))

@@ -36,6 +36,15 @@ _REF_CONFIG_CLASSES = ("EncoderType", "DecoderType", "AttentionType", "EncoderCo
                        "AttentionConfig", "TrainingConfig", "InferenceConfig", "ModelConfig", "Config")
 
 
+def _set_epoch(loader, tag):
+    """Tag the loader's sampler (capk.data.EpochSampler / DistributedSampler) with an explicit
+    pass number, so a pass's permutation and augmentations are a function of the training epoch
+    (and a resumed run repeats nothing) instead of the count of earlier iterations."""
+    sampler = getattr(loader, "sampler", None)
+    if sampler is not None and hasattr(sampler, "set_epoch"):
+        sampler.set_epoch(tag)
+
+
 def load_checkpoint_file(path, map_location="cpu"):
     """torch.load(weights_only=True) of a checkpoint written by this trainer or by the
     reference trainer (trainer.py:578-585, which pickles its ``src.config.Config`` dataclass
@@ -98,6 +107,7 @@ class CaptioningTrainer:
     def train_epoch(self, epoch, loader=None):
         """_train_epoch (trainer.py:200-317): mean CE over the loader, then SCST when enabled."""
         loader = loader or self.train_loader
+        _set_epoch(loader, 2 * epoch)  # crop / flip draws and the permutation follow the training epoch
         self.model.train()
         total, n = None, 0
         for i, batch in enumerate(loader):
@@ -134,6 +144,7 @@ class CaptioningTrainer:
         return loss, rs, rb
 
     def rl_epoch(self, epoch, loader):
+        _set_epoch(loader, 2 * epoch + 1)  # the SCST pass of an epoch draws its own permutation
         self.model.train()
         dec = self.model.decoder
         for batch in loader:

@@ -144,6 +144,65 @@ __global__ __launch_bounds__(256) void attn_probs_mean_kernel(int H, int Nq, int
   }
 }
 
+// Backward of attn_probs_mean_kernel (the head-averaged weights MultiHeadAttention returns,
+// attention.py:207-211, are differentiable in the reference): with P_h = softmax(scale
+// q_h.k_h) and dP_h = dW / H,
+//   dscore_h[s] = P_h[s] (dP_h[s] - sum_s' P_h[s'] dP_h[s']),
+//   dq_h += scale sum_s dscore_h[s] k_h[s],   dk_h[s] += scale dscore_h[s] q_h.
+// One block per (image, head) walks the queries in order (dk rows are shared by the
+// queries of an image): deterministic, no atomics.  dq (T) and dk (fp32) ACCUMULATE.
+static constexpr int PMB_MAXK = 2048;
+template <typename T>
+__global__ __launch_bounds__(256) void attn_probs_mean_bwd_kernel(int H, int Nq, int Nk, int hd, float scale,
+                                                                  const T* __restrict__ q, int64_t q_bs, int64_t q_rs,
+                                                                  const T* __restrict__ k, int64_t k_bs, int64_t k_rs,
+                                                                  const uint8_t* __restrict__ key_pad,
+                                                                  const float* __restrict__ lse,
+                                                                  const float* __restrict__ dw, T* __restrict__ dq,
+                                                                  int64_t dq_bs, int64_t dq_rs, float* __restrict__ dk,
+                                                                  int64_t dk_bs, int64_t dk_rs) {
+  const int b = blockIdx.x / H, h = blockIdx.x % H, tid = threadIdx.x;
+  __shared__ float ds[PMB_MAXK];
+  __shared__ float red[4];
+  const T* kb = k + (int64_t)b * k_bs + h * hd;
+  float* dkb = dk + (int64_t)b * dk_bs + h * hd;
+  const float invH = 1.f / H;
+  for (int qi = 0; qi < Nq; ++qi) {
+    const T* qr = q + (int64_t)b * q_bs + (int64_t)qi * q_rs + h * hd;
+    const float l = lse[((int64_t)b * H + h) * Nq + qi];
+    const float* g = dw + ((int64_t)b * Nq + qi) * Nk;
+    float part = 0.f;
+    for (int s = tid; s < Nk; s += blockDim.x) {
+      float p = 0.f;
+      if (!(key_pad && key_pad[(int64_t)b * Nk + s])) {
+        const T* kr = kb + (int64_t)s * k_rs;
+        float d = 0.f;
+        for (int i = 0; i < hd; ++i) d += to_f32(qr[i]) * to_f32(kr[i]);
+        p = __expf(d * scale - l);
+      }
+      ds[s] = p;
+      part += p * g[s] * invH;
+    }
+    part = wave_sum(part);
+    if ((tid & 63) == 0) red[tid >> 6] = part;
+    __syncthreads();
+    const float c = red[0] + red[1] + red[2] + red[3];
+    for (int s = tid; s < Nk; s += blockDim.x) ds[s] = ds[s] * (g[s] * invH - c) * scale;
+    __syncthreads();
+    for (int i = tid; i < hd; i += blockDim.x) {
+      float acc = 0.f;
+      for (int s = 0; s < Nk; ++s) acc += ds[s] * to_f32(kb[(int64_t)s * k_rs + i]);
+      T* dqr = dq + (int64_t)b * dq_bs + (int64_t)qi * dq_rs + h * hd;
+      dqr[i] = from_f32<T>(to_f32(dqr[i]) + acc);
+    }
+    for (int e = tid; e < Nk * hd; e += blockDim.x) {
+      const int s = e / hd, i = e % hd;
+      dkb[(int64_t)s * dk_rs + i] += ds[s] * to_f32(qr[i]);
+    }
+    __syncthreads();  // ds and red are rewritten by the next query
+  }
+}
+
 static int grid_e(int64_t n) {
   int64_t g = (n + 255) / 256;
   return (int)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
@@ -220,5 +279,19 @@ extern "C" int capk_attention_probs_mean(int dtype, int B, int H, int Nq, int Nk
   DT3(dtype, K);
 #undef K
   CAPK_LAUNCH_CHECK("attn_probs_mean_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_attention_probs_mean_bwd(int dtype, int B, int H, int Nq, int Nk, int hd, float scale,
+                                             const void* q, int64_t q_bs, int64_t q_rs, const void* k, int64_t k_bs,
+                                             int64_t k_rs, const uint8_t* key_pad, const float* lse, const float* dw,
+                                             void* dq, int64_t dq_bs, int64_t dq_rs, float* dk, int64_t dk_bs,
+                                             int64_t dk_rs, void* stream) {
+  CAPK_CHECK_ARG(B > 0 && H > 0 && Nq > 0 && Nk > 0 && hd > 0, "capk_attention_probs_mean_bwd: sizes");
+  CAPK_CHECK_ARG(Nk <= PMB_MAXK, "capk_attention_probs_mean_bwd: need Nk <= %d", PMB_MAXK);
+#define K(T) hipLaunchKernelGGL(attn_probs_mean_bwd_kernel<T>, dim3(B * H), dim3(256), 0, S(stream), H, Nq, Nk, hd, scale, (const T*)q, q_bs, q_rs, (const T*)k, k_bs, k_rs, key_pad, lse, dw, (T*)dq, dq_bs, dq_rs, dk, dk_bs, dk_rs)
+  DT3(dtype, K);
+#undef K
+  CAPK_LAUNCH_CHECK("attn_probs_mean_bwd_kernel");
   return CAPK_OK;
 }

@@ -370,7 +370,10 @@ int capk_soft_attn_bwd(int dtype, int B, int S, int D, const void* qp, int64_t l
  * out = beta ctx + (1 - beta) s (attention.py:279-285); bwd writes dctx, ds and
  * ACCUMULATES dwa [2D], dba [1] (fp32 atomics).
  * capk_attention_probs_mean: out[b,q,s] = mean_h softmax weights rebuilt from the lse
- * of capk_attention_fwd (MultiHeadAttention's returned weights, attention.py:207-210). */
+ * of capk_attention_fwd (MultiHeadAttention's returned weights, attention.py:207-210).
+ * capk_attention_probs_mean_bwd: gradient of those weights, dw fp32 [B, Nq, Nk]:
+ *   ACCUMULATES dq (dtype, [B, Nq, H*hd] view) and dk (fp32 [B, Nk, H*hd] view); one
+ *   block per (image, head), queries in order (deterministic).  Nk <= 2048. */
 int capk_ew_mul(int dtype, int rows, int cols, const void* a, int64_t lda, const void* b, int64_t ldb, void* out,
                 int64_t ldo, void* stream);
 int capk_tanh_gate_fwd(int dtype, int rows, int cols, const float* c, int64_t ldc, const void* g, int64_t ldg,
@@ -385,6 +388,10 @@ int capk_gate_mix_bwd(int dtype, int B, int D, const void* ctx, int64_t ldx, con
 int capk_attention_probs_mean(int dtype, int B, int H, int Nq, int Nk, int hd, float scale, const void* q,
                               int64_t q_bs, int64_t q_rs, const void* k, int64_t k_bs, int64_t k_rs,
                               const uint8_t* key_pad, const float* lse, float* out, void* stream);
+int capk_attention_probs_mean_bwd(int dtype, int B, int H, int Nq, int Nk, int hd, float scale, const void* q,
+                                  int64_t q_bs, int64_t q_rs, const void* k, int64_t k_bs, int64_t k_rs,
+                                  const uint8_t* key_pad, const float* lse, const float* dw, void* dq, int64_t dq_bs,
+                                  int64_t dq_rs, float* dk, int64_t dk_bs, int64_t dk_rs, void* stream);
 
 /* ------------------------------------------------ convolutional encoder (A3) ----
  * Channels-last activations [B, H, W, C] (row m = (b*H + h)*W + w, C contiguous).

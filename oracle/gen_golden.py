@@ -269,6 +269,69 @@ def case_lstm_attention(R):
     return arrs
 
 
+def case_attention_standalone(R):
+    """The AttentionMechanism drop-in contract (attention.py:12-35) of every module that
+    build_attention returns (attention.py:363-376), called standalone:
+    soft (T 0.7), multi_head (4 heads), aoa and adaptive over an MHA base (4 heads) and over
+    a soft base (1 head).  Three query forms per module:
+      q1  query [B, D] (2-D), key is value (one tensor), no mask;
+      q1m query [B, 1, D], distinct key / value, key_padding_mask;
+      qT  query [B, T=20, D], distinct key / value, key_padding_mask.
+    Loss = <context, gc> + <weights, gw> (the returned weights are differentiable in the
+    reference, MHA's head mean included); grads of query, key, value, memory_state,
+    cell_state (adaptive) and every parameter."""
+    D, B, S, T = 64, 3, 7, 20
+    arrs = {"meta/dims": np.array([D, B, S, T], dtype=np.int64)}
+    mask = torch.zeros(B, S, dtype=torch.bool)
+    mask[1, S - 2:] = True
+    mask[2, S - 4:] = True
+    arrs["in/mask"] = _np(mask)
+    variants = [("soft", R.config.AttentionType.SOFT, 1, 0.7), ("multi_head", R.config.AttentionType.MULTI_HEAD, 4, 1.0),
+                ("aoa", R.config.AttentionType.AOA, 4, 1.0), ("aoa_soft", R.config.AttentionType.AOA, 1, 1.0),
+                ("adaptive", R.config.AttentionType.ADAPTIVE, 4, 1.3),
+                ("adaptive_soft", R.config.AttentionType.ADAPTIVE, 1, 1.0)]
+    torch.manual_seed(4242)
+    inputs = {}
+    for form, Q in (("q1", 0), ("q1m", 1), ("qT", T)):
+        q = torch.randn(B, D) if Q == 0 else torch.randn(B, Q, D)
+        k = torch.randn(B, S, D)
+        v = k if form == "q1" else torch.randn(B, S, D)
+        h, c = torch.randn(B, D), torch.randn(B, D)
+        gc = torch.randn(B, D) if Q == 0 else torch.randn(B, Q, D)
+        gw = torch.randn(B, S) if Q == 0 else torch.randn(B, Q, S)
+        inputs[form] = (q, k, v, h, c, gc, gw, None if form == "q1" else mask)
+        for n, t in (("query", q), ("key", k), ("value", v), ("memory_state", h), ("cell_state", c), ("gc", gc),
+                     ("gw", gw)):
+            arrs[f"in/{form}/{n}"] = _np(t)
+    for name, at, heads, temp in variants:
+        torch.manual_seed(2000 + 7 * len(name) + heads)
+        acfg = R.config.AttentionConfig(attention_type=at, num_heads=heads, temperature=temp)
+        acfg.hidden_dim = D  # D3
+        mod = R.att.build_attention(acfg)
+        for n, p in mod.named_parameters():
+            arrs[f"{name}/p0/{n}"] = _np(p)
+        for form, (q, k, v, h, c, gc, gw, m) in inputs.items():
+            mod.zero_grad(set_to_none=True)
+            ql = q.clone().requires_grad_(True)
+            kl = k.clone().requires_grad_(True)
+            vl = kl if form == "q1" else v.clone().requires_grad_(True)
+            hl = h.clone().requires_grad_(True)
+            cl = c.clone().requires_grad_(True)
+            kw = {"memory_state": hl, "cell_state": cl} if name.startswith("adaptive") else {}
+            ctx, w = mod(ql, kl, vl, m, **kw)
+            ((ctx * gc).sum() + (w * gw).sum()).backward()
+            pre = f"{name}/{form}/"
+            arrs[pre + "context"], arrs[pre + "weights"] = _np(ctx), _np(w)
+            arrs[pre + "dquery"], arrs[pre + "dkey"] = _np(ql.grad), _np(kl.grad)
+            if form != "q1":
+                arrs[pre + "dvalue"] = _np(vl.grad)
+            if kw:
+                arrs[pre + "dmemory_state"], arrs[pre + "dcell_state"] = _np(hl.grad), _np(cl.grad)
+            for n, p in mod.named_parameters():
+                arrs[pre + "grad/" + n] = _np(p.grad) if p.grad is not None else np.zeros(tuple(p.shape), np.float32)
+    return arrs
+
+
 def case_resnet_lstm(R):
     """Config 2 path (ResNet + LSTMDecoder + soft attention), TRAIN mode (BatchNorm on batch
     statistics, running buffers updated) with decoder dropout 0 so the step is deterministic.
@@ -470,7 +533,8 @@ def case_swin_encoder(R):
 
 
 CASES = {"vit_transformer_step": case_vit_transformer, "qformer_step": case_qformer, "clip_gpt2_step": case_clip_gpt2,
-         "lstm_attention": case_lstm_attention, "resnet_lstm_step": case_resnet_lstm,
+         "lstm_attention": case_lstm_attention, "attention_standalone": case_attention_standalone,
+         "resnet_lstm_step": case_resnet_lstm,
          "legacy_decoder_step": case_legacy_decoder, "swin_encoder": case_swin_encoder}
 
 

@@ -8,35 +8,43 @@ import torch
 import torch.nn.functional as F
 
 
+def _q3(q):
+    """[B, D] -> ([B, 1, D], squeeze) as every module does first (attention.py:66-70)."""
+    return (q[:, None], True) if q.dim() == 2 else (q, False)
+
+
 def soft_attention(p, pre, q, k, v, temperature, key_pad=None):
-    """SoftAttention.forward (src/models/attention.py:57-118), q [B, D] (one query)."""
-    qp = F.linear(q, p[pre + "query_proj.weight"], p[pre + "query_proj.bias"])[:, None, None, :]
+    """SoftAttention.forward (src/models/attention.py:57-118), q [B, D] or [B, Q, D]."""
+    q, sq = _q3(q)
+    qp = F.linear(q, p[pre + "query_proj.weight"], p[pre + "query_proj.bias"])[:, :, None, :]
     kp = F.linear(k, p[pre + "key_proj.weight"], p[pre + "key_proj.bias"])[:, None, :, :]
     e = F.linear(torch.tanh(qp + kp), p[pre + "energy.weight"], p[pre + "energy.bias"]).squeeze(-1) / temperature
     if key_pad is not None:
         e = e.masked_fill(key_pad[:, None, :], -1e9)
     w = torch.softmax(e, -1)
     ctx = torch.matmul(w.unsqueeze(-2), v.unsqueeze(1)).squeeze(-2)
-    return ctx.squeeze(1), w.squeeze(1)
+    return (ctx.squeeze(1), w.squeeze(1)) if sq else (ctx, w)
 
 
 def mha_attention(p, pre, q, k, v, num_heads, temperature, key_pad=None):
     """MultiHeadAttention.forward (attention.py:142-218): scale 1/(T*sqrt(hd)),
     masked_fill(-1e9), output_proj, returned weights = mean over heads."""
-    B, D = q.shape
+    q, sq = _q3(q)
+    B, Q, D = q.shape
     hd = D // num_heads
 
     def proj(x, name):
         return F.linear(x, p[pre + name + ".weight"], p[pre + name + ".bias"]).view(B, -1, num_heads, hd).transpose(1, 2)
 
-    qh, kh, vh = proj(q[:, None], "query_proj"), proj(k, "key_proj"), proj(v, "value_proj")
+    qh, kh, vh = proj(q, "query_proj"), proj(k, "key_proj"), proj(v, "value_proj")
     s = torch.matmul(qh, kh.transpose(-1, -2)) / (temperature * hd ** 0.5)
     if key_pad is not None:
         s = s.masked_fill(key_pad[:, None, None, :], -1e9)
     a = torch.softmax(s, -1)
-    o = torch.matmul(a, vh).transpose(1, 2).reshape(B, 1, D)
+    o = torch.matmul(a, vh).transpose(1, 2).reshape(B, Q, D)
     ctx = F.linear(o, p[pre + "output_proj.weight"], p[pre + "output_proj.bias"])
-    return ctx.squeeze(1), a.mean(1).squeeze(1)
+    w = a.mean(1)
+    return (ctx.squeeze(1), w.squeeze(1)) if sq else (ctx, w)
 
 
 def base_attention(p, pre, q, k, v, num_heads, temperature, key_pad=None):
@@ -58,13 +66,29 @@ def aoa_attention(p, pre, q, k, v, num_heads, temperature, key_pad=None):
 
 def adaptive_attention(p, pre, q, k, v, num_heads, temperature, h, c, key_pad=None):
     """AdaptiveAttention.forward (attention.py:242-294): visual sentinel from the LSTM
-    memory/cell state, gate beta = sigmoid(W_a [ctx; s])."""
+    memory/cell state [B, D] (expanded over the Q queries), gate beta = sigmoid(W_a [ctx; s])."""
+    if q.dim() == 3:
+        h = h[:, None].expand(-1, q.shape[1], -1)
+        c = c[:, None].expand(-1, q.shape[1], -1)
     sg = torch.sigmoid(F.linear(torch.cat([q, h], -1), p[pre + "sentinel_gate.weight"], p[pre + "sentinel_gate.bias"]))
     sent = F.linear(sg * torch.tanh(c), p[pre + "sentinel_proj.weight"], p[pre + "sentinel_proj.bias"])
     ctx, w = base_attention(p, pre + "base_attention.", q, k, v, num_heads, temperature, key_pad)
     beta = torch.sigmoid(F.linear(torch.cat([ctx, sent], -1), p[pre + "adaptive_weight.weight"],
                                   p[pre + "adaptive_weight.bias"]))
     return beta * ctx + (1 - beta) * sent, w
+
+
+def standalone(kind, p, q, k, v, num_heads, temperature, key_pad=None, h=None, c=None, pre=""):
+    """build_attention(cfg)(q, k, v, key_padding_mask[, memory_state, cell_state]) (attention.py:363-376)."""
+    if kind == "soft":
+        return soft_attention(p, pre, q, k, v, temperature, key_pad)
+    if kind == "multi_head":
+        return mha_attention(p, pre, q, k, v, num_heads, temperature, key_pad)
+    if kind == "aoa":
+        return aoa_attention(p, pre, q, k, v, num_heads, temperature, key_pad)
+    if kind == "adaptive":
+        return adaptive_attention(p, pre, q, k, v, num_heads, temperature, h, c, key_pad)
+    raise ValueError(kind)
 
 
 def attend(kind, p, q, feats, num_heads, temperature, h_top, c_top):

@@ -119,6 +119,9 @@ def run(name, M, N, K, kind, iters=20):
 
 if __name__ == "__main__":
     only = os.environ.get("GEMM_ONLY")
+    extra = os.environ.get("GEMM_SHAPES")  # "name:M:N:K:kind,..." ad-hoc shapes (run instead of the table)
+    if extra:
+        SHAPES = [(f[0], int(f[1]), int(f[2]), int(f[3]), f[4]) for f in (x.split(":") for x in extra.split(","))]
     for s in SHAPES:
         if only and s[0] not in only.split(","):
             continue
