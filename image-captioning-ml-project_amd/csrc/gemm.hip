@@ -342,6 +342,11 @@ static int choose_cfg(int M, int N, int K, int a_kmajor, int b_kmajor, int act) 
       if (t5 * choose_splits(5, M, N, K) >= 192) return big;
     } else if (t5 > 256) {
       return big;
+    } else if (K >= 8192 && t5 * choose_splits(5, M, N, K) >= 192) {
+      // long-K products with a small tile grid (the LM-head dX: 5120 x 768 x 50 304, 60
+      // tiles): split-K on the 256x256 kernel -- the 128-row ring ran it as 240 one-WG-per-CU
+      // tiles at 0.17 of peak (938 us, profiles/round4)
+      return big;
     }
   }
   if (!a_kmajor && !b_kmajor && tiles_of(4, M, N) < slots_of(4)) return 1;  // split-K dW (cfg 4 measured slower)
