@@ -1026,39 +1026,47 @@ __global__ __launch_bounds__(256) void attn_decode_bf16(AttnArgs a) {
   }
 }
 
-// ------------------------------------------------- beam cross-attention step ---
-// The k beam queries of one image against its shared memory keys (config-3 beam-5: Nq = 5,
-// Nk = 196, hd 96; 114 launches per 256-image batch) on MFMA.  The VALU decode kernels
-// spend ~1000 VALU issues per wave on 5 x 196 x 96 dot products (88 us per step, 1.9 TB/s);
-// here the same products are 24 MFMAs per wave and the step is a K / V stream:
+// ------------------------------------------ cross-attention: short query block vs memory ---
+// The <= 32 queries of one (image, head) against its <= 256 memory keys on MFMA: the beam
+// cross-attention step (config-3 beam-5: Nq = 5, Nk = 196, hd 96; 114 launches per 256-image
+// batch) and, round 4, the training decoder's cross-attention forward (Nq = T = 20 caption
+// positions, attention dropout, nn.TransformerDecoderLayer.multihead_attn via
+// src/models/decoders.py:421-428).  The step is a K / V stream (K/V 154 MB at bs 256), so what
+// costs is round trips, not FLOPs; the VALU decode kernels spent ~1000 VALU issues per wave on
+// 5 x 196 x 96 dot products (88 us per step, 1.9 TB/s):
 //  * 4 waves per (batch, head), each owning 64 keys (Nk <= 256): S^T = K Q^T with K
 //    fragments loaded straight from global memory (16 keys x 32 dims per MFMA, 16-B lane
-//    loads of K rows) and the <= 16 queries as the B operand (one 16-query tile);
+//    loads of K rows) and the queries as the B operand (NQT 16-query tiles);
 //  * the wave's V rows staged in its own LDS image (row stride HDP + 16) and read as V^T
 //    fragments by ds_read_b64_tr_b16 for O^T = V^T P^T, P^T packed from the S^T registers
 //    (the attn_fwd_bf16 layout: no shuffles between the two products);
 //  * every K, V and Q load of the wave issued before the first wait (one round trip);
 //  * per-wave softmax (m, l, O^T) merged across the 4 waves in LDS with the flash-decoding
-//    rescale.  No dropout / causal; key padding honoured.
-template <int HDP, int MODE>
+//    rescale; the row sum l excludes dropout (dropout(softmax) V), the mask is the training
+//    kernels' pdrop index, so attn_bwd recomputes the same keep decisions.  No causal mask;
+//    key padding honoured.  lse (natural log) written for the backward.
+template <int HDP, int MODE, int NQT>
 __global__ __launch_bounds__(256) void attn_xdec_bf16(AttnArgs a) {
-  constexpr int NW = 4, KPW = 64, ST = HDP + 16, NCH = HDP / 8, NS = HDP / 32, ND = HDP / 16;
+  constexpr int NW = 4, KPW = 64, ST = HDP + 16, NCH = HDP / 8, NS = HDP / 32, ND = HDP / 16, NQ = 16 * NQT;
+  static_assert(NQ * HDP * 4 <= KPW * ST * 2, "the fp32 partial O of a wave fits its V image");
   __shared__ __attribute__((aligned(16))) bf16 vimg[NW][KPW * ST];
-  __shared__ float mm[NW][16], ll[NW][16];
+  __shared__ float mm[NW][NQ], ll[NW][NQ];
   const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
   const int hoff = h * a.hd;
   const int k0 = w * KPW;  // the wave's first key
   const bf16* kbase = (const bf16*)a.k + (int64_t)b * a.k_bs + hoff;
   const bf16* vbase = (const bf16*)a.v + (int64_t)b * a.v_bs + hoff;
-  // Q^T fragments (B operand): query c16, dims s*32 + 8g
-  bf16x8 qf[NS];
+  // Q^T fragments (B operand): query 16 qt + c16, dims s*32 + 8g
+  bf16x8 qf[NQT][NS];
 #pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int d = s * 32 + 8 * g;
-    qf[s] = (c16 < a.Nq && d < a.hd) ? ld8((const bf16*)a.q + (int64_t)b * a.q_bs + (int64_t)c16 * a.q_rs + hoff + d)
-                                     : zero8();
-  }
+  for (int qt = 0; qt < NQT; ++qt)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int d = s * 32 + 8 * g, q = 16 * qt + c16;
+      qf[qt][s] = (q < a.Nq && d < a.hd) ? ld8((const bf16*)a.q + (int64_t)b * a.q_bs + (int64_t)q * a.q_rs + hoff + d)
+                                         : zero8();
+    }
   // K fragments (A operand): key k0 + 16 kb + c16, dims s*32 + 8g
   bf16x8 kf[KPW / 16][NS];
 #pragma unroll
@@ -1083,57 +1091,74 @@ __global__ __launch_bounds__(256) void attn_xdec_bf16(AttnArgs a) {
     const int ch = lane + 64 * i, row = ch / NCH, col = (ch % NCH) * 8;
     *(bf16x8*)(Vs + row * ST + col) = vr[i];
   }
-  // S^T = K Q^T, scores in the log2 domain; keys past Nk / padded -> -inf
+  // S^T = K Q^T per query tile, scores in the log2 domain; keys past Nk / padded -> -inf
   const float sl2 = a.scale * kLog2e;
-  f32x4 sc[KPW / 16];
-  float m = -INFINITY;
+  f32x4 sc[NQT][KPW / 16];
+  float m[NQT], l[NQT];
 #pragma unroll
-  for (int kb = 0; kb < KPW / 16; ++kb) {
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int qt = 0; qt < NQT; ++qt) {
+    m[qt] = -INFINITY;
 #pragma unroll
-    for (int s = 0; s < NS; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kb][s], qf[s], acc, 0, 0, 0);
+    for (int kb = 0; kb < KPW / 16; ++kb) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int key = k0 + kb * 16 + 4 * g + r;
-      const bool ok = (MODE & AM_MASK) ? key_ok(a, b, key, c16) : key < a.Nk;
-      acc[r] = ok ? acc[r] * sl2 : -INFINITY;
-      m = fmaxf(m, acc[r]);
+      for (int s = 0; s < NS; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kb][s], qf[qt][s], acc, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + kb * 16 + 4 * g + r;
+        const bool ok = (MODE & AM_MASK) ? key_ok(a, b, key, 16 * qt + c16) : key < a.Nk;
+        acc[r] = ok ? acc[r] * sl2 : -INFINITY;
+        m[qt] = fmaxf(m[qt], acc[r]);
+      }
+      sc[qt][kb] = acc;
     }
-    sc[kb] = acc;
+    m[qt] = fmaxf(m[qt], __shfl_xor(m[qt], 16, 64));
+    m[qt] = fmaxf(m[qt], __shfl_xor(m[qt], 32, 64));
+    l[qt] = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < KPW / 16; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = m[qt] == -INFINITY ? 0.f : fexp2(sc[qt][kb][r] - m[qt]);
+        l[qt] += p;  // the normaliser excludes dropout
+        sc[qt][kb][r] = dropm<MODE>() && 16 * qt + c16 < a.Nq ? p * pdrop(a, b, h, 16 * qt + c16, k0 + kb * 16 + 4 * g + r)
+                                                              : p;
+      }
+    l[qt] += __shfl_xor(l[qt], 16, 64);
+    l[qt] += __shfl_xor(l[qt], 32, 64);
   }
-  m = fmaxf(m, __shfl_xor(m, 16, 64));
-  m = fmaxf(m, __shfl_xor(m, 32, 64));
-  float l = 0.f;
-#pragma unroll
-  for (int kb = 0; kb < KPW / 16; ++kb)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float p = m == -INFINITY ? 0.f : fexp2(sc[kb][r] - m);
-      sc[kb][r] = p;
-      l += p;
-    }
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own V image is written
   // O^T = V^T P^T over two 32-key chunks
-  f32x4 o[ND];
+  f32x4 o[NQT][ND];
 #pragma unroll
-  for (int db = 0; db < ND; ++db) o[db] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int qt = 0; qt < NQT; ++qt)
 #pragma unroll
-  for (int t = 0; t < KPW / 32; ++t) {
-    const bf16x8 pb = pack8(sc[2 * t], sc[2 * t + 1]);
+    for (int db = 0; db < ND; ++db) o[qt][db] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int db = 0; db < ND; ++db)
-      o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_read8(Vs, ST, 32 * t, db * 16, lane), pb, o[db], 0, 0, 0);
-  }
+  for (int t = 0; t < KPW / 32; ++t)
+#pragma unroll
+    for (int db = 0; db < ND; ++db) {
+      const bf16x8 vt = tr_read8(Vs, ST, 32 * t, db * 16, lane);
+#pragma unroll
+      for (int qt = 0; qt < NQT; ++qt)
+        o[qt][db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt, pack8(sc[qt][2 * t], sc[qt][2 * t + 1]), o[qt][db], 0, 0, 0);
+    }
   // merge the 4 waves: (m, l) per query, O^T partials into the (now free) V images as fp32
   __syncthreads();  // every wave is done reading its V image
-  float* op = (float*)vimg[w];  // [16 queries][HDP] fp32 (fits in the wave's image)
+  float* op = (float*)vimg[w];  // [NQ queries][HDP] fp32 (fits in the wave's image)
 #pragma unroll
-  for (int db = 0; db < ND; ++db)
+  for (int qt = 0; qt < NQT; ++qt)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) op[c16 * HDP + db * 16 + 4 * g + r] = o[db][r];
-  if (g == 0) { mm[w][c16] = m; ll[w][c16] = l; }
+    for (int db = 0; db < ND; ++db)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) op[(16 * qt + c16) * HDP + db * 16 + 4 * g + r] = o[qt][db][r];
+  if (g == 0) {
+#pragma unroll
+    for (int qt = 0; qt < NQT; ++qt) {
+      mm[w][16 * qt + c16] = m[qt];
+      ll[w][16 * qt + c16] = l[qt];
+    }
+  }
   __syncthreads();
   for (int e = threadIdx.x; e < a.Nq * a.hd; e += blockDim.x) {
     const int q = e / a.hd, d = e % a.hd;
@@ -1151,6 +1176,194 @@ __global__ __launch_bounds__(256) void attn_xdec_bf16(AttnArgs a) {
     }
     ((bf16*)a.out)[(int64_t)b * a.out_bs + (int64_t)q * a.out_rs + hoff + d] = (bf16)(den > 0.f ? num / den : 0.f);
     if (d == 0) a.lse[((int64_t)b * a.H + h) * a.Nq + q] = den > 0.f ? (mt + __log2f(den)) * kLn2 : -INFINITY;
+  }
+}
+
+// ------------------------------------ cross-attention backward: short query block ---
+// Backward of attn_xdec_bf16's training launch (the decoder's cross-attention: Nq = 20
+// caption positions against Nk = 196 memory keys, hd 96, dropout; <= 32 queries, <= 256 keys).
+// The data is K / V in and dK / dV out (2 x 154 MB at bs 256); Q, dO, O are 20 rows per
+// (image, head).  4 waves per (batch, head), each owning 64 keys in two 32-key chunks:
+//  * per 16-key block: S = Q K^T and dP = dO V^T with the KEY on the lane (Q / dO fragments
+//    from the staged images as the A operand, K / V fragments straight from global memory as
+//    the B operand), P = exp2(S - lse), dS = P (dP m - D) (m: the pdrop keep factor);
+//  * dV^T += dO^T (P m), dK^T += Q^T dS with the query as the MFMA k dimension: dO^T / Q^T by
+//    transposed reads of the zero-padded 32-row images, P / dS packed from the score registers
+//    (attn_fwd_bf16's k permutation on both sides); dK / dV rows written once (no reduction);
+//  * dQ = dS K needs the key on the k dimension: the chunk's dS (bf16) and K rows go to the
+//    wave's own LDS images and both are read transposed; the 4 waves' dQ partials are summed
+//    in LDS in a fixed order (deterministic).
+template <int HDP, int MODE, int NQT>
+__global__ __launch_bounds__(256) void attn_xbwd_bf16(AttnArgs a) {
+  constexpr int NW = 4, KPW = 64, ST = HDP + 16, NS = HDP / 32, ND = HDP / 16, NQ = 16 * NQT;
+  constexpr int DST = 32 + 8;  // dS image [32 keys][32 queries] row stride (bf16)
+  __shared__ __attribute__((aligned(16))) bf16 kimg[NW][32 * ST];  // the wave's 32-key chunk of K
+  __shared__ __attribute__((aligned(16))) bf16 qimg[32 * ST], doimg[32 * ST];  // rows >= Nq are zero
+  __shared__ __attribute__((aligned(16))) bf16 dsimg[NW][32 * DST];
+  __shared__ float lse_s[32], del_s[32];
+  static_assert(2 * NQ * HDP * 4 <= (int)sizeof(kimg), "two fp32 dQ partials fit the K images");
+  const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
+  const int hoff = h * a.hd;
+  const bf16* kbase = (const bf16*)a.k + (int64_t)b * a.k_bs + hoff;
+  const bf16* vbase = (const bf16*)a.v + (int64_t)b * a.v_bs + hoff;
+  // ---- prologue: Q / dO images (32 rows, zero past Nq), lse, D = rowsum(dO * O)
+  for (int e = threadIdx.x; e < 32 * (HDP / 8); e += blockDim.x) {
+    const int r = e / (HDP / 8), c = (e % (HDP / 8)) * 8;
+    const bool in = r < a.Nq && c < a.hd;
+    *(bf16x8*)(qimg + r * ST + c) = in ? ld8((const bf16*)a.q + (int64_t)b * a.q_bs + (int64_t)r * a.q_rs + hoff + c) : zero8();
+    *(bf16x8*)(doimg + r * ST + c) =
+        in ? ld8((const bf16*)a.dout + (int64_t)b * a.do_bs + (int64_t)r * a.do_rs + hoff + c) : zero8();
+  }
+  if (threadIdx.x < 32) {
+    const int q = threadIdx.x;
+    lse_s[q] = q < a.Nq ? a.lse_in[((int64_t)b * a.H + h) * a.Nq + q] * kLog2e : INFINITY;  // exp2(s - inf) = 0
+  }
+  __syncthreads();
+  // D[q]: 8 lanes per query row (the dO row from LDS, O from global)
+  for (int e = threadIdx.x; e < 32 * 8; e += blockDim.x) {
+    const int q = e >> 3, c8 = e & 7;
+    float d = 0.f;
+    if (q < a.Nq)
+      for (int c = c8 * 8; c < a.hd; c += 64) {
+        const bf16x8 ov = ld8((const bf16*)a.o + (int64_t)b * a.o_bs + (int64_t)q * a.o_rs + hoff + c);
+        const bf16x8 dv = *(const bf16x8*)(doimg + q * ST + c);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) d += (float)ov[i] * (float)dv[i];
+      }
+    d += __shfl_xor(d, 1, 64);
+    d += __shfl_xor(d, 2, 64);
+    d += __shfl_xor(d, 4, 64);
+    if (c8 == 0) del_s[q] = d;
+  }
+  // Q / dO fragments (A operand: query 16 qt + c16, dims s*32 + 8g)
+  bf16x8 qf[NQT][NS], dof[NQT][NS];
+#pragma unroll
+  for (int qt = 0; qt < NQT; ++qt)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      qf[qt][s] = *(const bf16x8*)(qimg + (16 * qt + c16) * ST + s * 32 + 8 * g);
+      dof[qt][s] = *(const bf16x8*)(doimg + (16 * qt + c16) * ST + s * 32 + 8 * g);
+    }
+  __syncthreads();  // del_s
+  float lq[NQT][4], dq_[NQT][4];
+#pragma unroll
+  for (int qt = 0; qt < NQT; ++qt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      lq[qt][r] = lse_s[16 * qt + 4 * g + r];
+      dq_[qt][r] = del_s[16 * qt + 4 * g + r];
+    }
+  const float sl2 = a.scale * kLog2e;
+  f32x4 dqa[NQT][ND];  // dQ[q][d] partial: lane = d (c16), rows q = 4g + r
+#pragma unroll
+  for (int qt = 0; qt < NQT; ++qt)
+#pragma unroll
+    for (int db = 0; db < ND; ++db) dqa[qt][db] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  bf16* Kc = kimg[w];
+  bf16* dSc = dsimg[w];
+  for (int ch = 0; ch < KPW / 32; ++ch) {
+    const int kc0 = w * KPW + ch * 32;  // the chunk's first key
+    if (kc0 >= a.Nk) break;             // (wave-uniform)
+    // K / V fragments of the chunk's two 16-key blocks (B operand: key c16, dims s*32 + 8g)
+    bf16x8 kf[2][NS], vf[2][NS];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const int key = kc0 + kb * 16 + c16, d = s * 32 + 8 * g;
+        const bool in = key < a.Nk && d < a.hd;
+        kf[kb][s] = in ? ld8(kbase + (int64_t)key * a.k_rs + d) : zero8();
+        vf[kb][s] = in ? ld8(vbase + (int64_t)key * a.v_rs + d) : zero8();
+      }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) *(bf16x8*)(Kc + (kb * 16 + c16) * ST + s * 32 + 8 * g) = kf[kb][s];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const int key = kc0 + kb * 16 + c16;
+      f32x4 p[NQT], ds[NQT];
+#pragma unroll
+      for (int qt = 0; qt < NQT; ++qt) {
+        f32x4 sa = {0.f, 0.f, 0.f, 0.f}, dpa = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          sa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[qt][s], kf[kb][s], sa, 0, 0, 0);
+          dpa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dof[qt][s], vf[kb][s], dpa, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = 16 * qt + 4 * g + r;
+          const bool ok = (MODE & AM_MASK) ? key_ok(a, b, key, q) : key < a.Nk;
+          const float pv = ok ? fexp2(sa[r] * sl2 - lq[qt][r]) : 0.f;
+          const float mk = dropm<MODE>() && q < a.Nq ? pdrop(a, b, h, q, key) : 1.f;
+          p[qt][r] = pv * mk;
+          ds[qt][r] = pv * (dpa[r] * mk - dq_[qt][r]);
+        }
+        // dS -> the chunk's image, row = key, columns = queries 16 qt + 4g .. + 3
+        bf16x4 d4;
+        d4[0] = (bf16)ds[qt][0]; d4[1] = (bf16)ds[qt][1]; d4[2] = (bf16)ds[qt][2]; d4[3] = (bf16)ds[qt][3];
+        *(bf16x4*)(dSc + (kb * 16 + c16) * DST + 16 * qt + 4 * g) = d4;
+      }
+      if constexpr (NQT == 1) {  // queries 16..31 of the images are zero rows; the dS columns too
+        const bf16x4 z = {(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+        *(bf16x4*)(dSc + (kb * 16 + c16) * DST + 16 + 4 * g) = z;
+      }
+      const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+      const bf16x8 pb = pack8(p[0], NQT > 1 ? p[NQT - 1] : zero4);
+      const bf16x8 dsb = pack8(ds[0], NQT > 1 ? ds[NQT - 1] : zero4);
+      // dV^T = dO^T (P m), dK^T = Q^T dS over the (permuted) 32 queries: lane = key, rows = dims
+      // (the transposed reads run with every lane active, as the ISA requires; only the stores
+      // are per lane)
+      bf16* dkrow = (bf16*)a.dk + (int64_t)b * a.dk_bs + (int64_t)key * a.dk_rs + hoff;
+      bf16* dvrow = (bf16*)a.dv + (int64_t)b * a.dv_bs + (int64_t)key * a.dv_rs + hoff;
+#pragma unroll
+      for (int db = 0; db < ND; ++db) {
+        f32x4 dv4 = {0.f, 0.f, 0.f, 0.f}, dk4 = {0.f, 0.f, 0.f, 0.f};
+        dv4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_read8(doimg, ST, 0, db * 16, lane), pb, dv4, 0, 0, 0);
+        dk4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_read8(qimg, ST, 0, db * 16, lane), dsb, dk4, 0, 0, 0);
+        const int d0 = db * 16 + 4 * g;
+        if (key < a.Nk && d0 < a.hd) {
+          store4(dkrow + d0, dk4, a.scale);
+          store4(dvrow + d0, dv4, 1.f);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the chunk's K and dS images are written (wave-private)
+    // dQ[q][d] += dS[q][keys] K[keys][d]: A = dS (lane = query), B = K (lane = dim), k = the
+    // chunk's 32 keys in tr_read8's order on both sides
+#pragma unroll
+    for (int qt = 0; qt < NQT; ++qt) {
+      const bf16x8 af = tr_read8(dSc, DST, 0, 16 * qt, lane);
+#pragma unroll
+      for (int db = 0; db < ND; ++db)
+        dqa[qt][db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, tr_read8(Kc, ST, 0, db * 16, lane), dqa[qt][db], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next chunk rewrites the images
+  }
+  // ---- dQ: the 4 waves' partials summed in a fixed order through two fp32 buffers over kimg
+  __syncthreads();
+  float* red = (float*)&kimg[0][0];  // [2][NQ][HDP]
+  auto put = [&](float* buf, bool add) {
+#pragma unroll
+    for (int qt = 0; qt < NQT; ++qt)
+#pragma unroll
+      for (int db = 0; db < ND; ++db)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float* x = buf + (16 * qt + 4 * g + r) * HDP + db * 16 + c16;
+          *x = add ? *x + dqa[qt][db][r] : dqa[qt][db][r];
+        }
+  };
+  if (w < 2) put(red + w * NQ * HDP, false);
+  __syncthreads();
+  if (w >= 2) put(red + (w - 2) * NQ * HDP, true);
+  __syncthreads();
+  for (int e = threadIdx.x; e < a.Nq * a.hd; e += blockDim.x) {
+    const int q = e / a.hd, d = e % a.hd;
+    ((bf16*)a.dq)[(int64_t)b * a.dq_bs + (int64_t)q * a.dq_rs + hoff + d] =
+        (bf16)((red[q * HDP + d] + red[NQ * HDP + q * HDP + d]) * a.scale);
   }
 }
 
@@ -1379,18 +1592,28 @@ extern "C" int capk_attention_fwd(int dtype, int B, int H, int Nq, int Nk, int h
                      k_bs % 8 == 0 && v_bs % 8 == 0,
                  "capk_attention_fwd(bf16): strides must allow 16-B vector access");
   static const bool decode_v1 = [] { const char* e = getenv("CAPK_DECODE_V1"); return e && e[0] == '1'; }();
-  // beam cross-attention steps (k beams of an image against its memory keys): the MFMA
-  // kernel (CAPK_XDEC=0 keeps them on the VALU decode kernel for A/B)
+  // short query blocks against memory keys (beam cross-attention steps: k beams of an image;
+  // the training decoder's cross-attention: T = 20 positions, with dropout): the MFMA xdec
+  // kernel (CAPK_XDEC=0 keeps the beam steps on the VALU decode kernel and the training
+  // launches on attn_fwd_bf16, for A/B)
   static const bool xdec_on = [] { const char* e = getenv("CAPK_XDEC"); return !(e && e[0] == '0'); }();
-  if (xdec_on && !decode_v1 && Nq >= 2 && Nq <= 16 && Nk > 64 && Nk <= 256 && !causal && !(drop_p > 0.f) &&
+  if (xdec_on && !decode_v1 && Nq >= 2 && Nq <= 32 && Nk > 64 && Nk <= 256 && !causal &&
       (hd == 64 || hd == 96 || hd == 128)) {
     const dim3 g(B * H), blk(256);
-    const int xm = key_pad ? AM_MASK : 0;
-#define XD(HD)                                                                                          \
-  if (xm) hipLaunchKernelGGL((attn_xdec_bf16<HD, AM_MASK>), g, blk, 0, st, a);                          \
-  else hipLaunchKernelGGL((attn_xdec_bf16<HD, 0>), g, blk, 0, st, a);
+    const int xm = (key_pad ? AM_MASK : 0) | (drop_p > 0.f ? AM_DROP : 0);
+#define XDQ(HD, M)                                                                  \
+  if (Nq <= 16) hipLaunchKernelGGL((attn_xdec_bf16<HD, M, 1>), g, blk, 0, st, a);   \
+  else hipLaunchKernelGGL((attn_xdec_bf16<HD, M, 2>), g, blk, 0, st, a);
+#define XD(HD)                                                                      \
+  switch (xm) {                                                                     \
+    case 0: XDQ(HD, 0) break;                                                       \
+    case AM_DROP: XDQ(HD, AM_DROP) break;                                           \
+    case AM_MASK: XDQ(HD, AM_MASK) break;                                           \
+    default: XDQ(HD, AM_MASK | AM_DROP) break;                                      \
+  }
     if (hd == 64) { XD(64) } else if (hd == 96) { XD(96) } else { XD(128) }
 #undef XD
+#undef XDQ
     CAPK_LAUNCH_CHECK("attn_xdec_bf16");
     return CAPK_OK;
   }
@@ -1528,6 +1751,28 @@ extern "C" int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int h
     default: CALL2(128, M); break; \
   }
   int rc2 = CAPK_OK;
+  // short query blocks against memory keys (the training decoder's cross-attention): the
+  // MFMA xbwd kernel, the backward of attn_xdec_bf16 (CAPK_XDEC=0: the fused kernel below)
+  static const bool xbwd_on = [] { const char* e = getenv("CAPK_XDEC"); return !(e && e[0] == '0'); }();
+  if (xbwd_on && Nq >= 2 && Nq <= 32 && Nk > 64 && Nk <= 256 && !causal && (hd == 64 || hd == 96 || hd == 128)) {
+    const dim3 g(B * H), blk(256);
+    const int xm = (key_pad ? AM_MASK : 0) | (drop_p > 0.f ? AM_DROP : 0);
+#define XBQ(HD, M)                                                                  \
+  if (Nq <= 16) hipLaunchKernelGGL((attn_xbwd_bf16<HD, M, 1>), g, blk, 0, st, a);   \
+  else hipLaunchKernelGGL((attn_xbwd_bf16<HD, M, 2>), g, blk, 0, st, a);
+#define XB(HD)                                                                      \
+  switch (xm) {                                                                     \
+    case 0: XBQ(HD, 0) break;                                                       \
+    case AM_DROP: XBQ(HD, AM_DROP) break;                                           \
+    case AM_MASK: XBQ(HD, AM_MASK) break;                                           \
+    default: XBQ(HD, AM_MASK | AM_DROP) break;                                      \
+  }
+    if (hd == 64) { XB(64) } else if (hd == 96) { XB(96) } else { XB(128) }
+#undef XB
+#undef XBQ
+    CAPK_LAUNCH_CHECK("attn_xbwd_bf16");
+    return CAPK_OK;
+  }
   {
     // split backward: dK/dV kernel, then dQ kernel (two head images in LDS each)
     const size_t s1 = bwd_kv_smem(Nq, hdp), s2 = fwd_kernel_smem(Nk, hdp);

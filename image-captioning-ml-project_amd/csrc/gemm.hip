@@ -394,7 +394,9 @@ extern "C" size_t capk_gemm_workspace(int in_dtype, int out_dtype, int M, int N,
   // upper bound over the configurations (the launch picks one of them)
   int s = 1;
   for (int c = 1; c <= 6; ++c) s = std::max(s, choose_splits(c, M, N, K));
-  return s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
+  const size_t slab = s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
+  // persistent grids: the split-tail hand-off area (gemm8q.hip)
+  return tiles_of(6, M, N) > 256 ? std::max(slab, gemm8q_spt_workspace()) : slab;
 }
 
 extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const void* A, int64_t lda,
@@ -472,8 +474,9 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
   else if (b_kmajor) LAUNCH(false, true, OT);           \
   else LAUNCH(false, false, OT);
   if (cfg == 6) {
+    void* spt = (!slab && ws && ws_bytes >= gemm8q_spt_workspace()) ? ws : nullptr;
     const int rc = launch_gemm8q(a_kmajor, b_kmajor, out_dtype == CAPK_F32, A, lda, B, ldb, M, N, K, splits, e, slab,
-                                 st);
+                                 st, nullptr, spt);
     if (rc != CAPK_OK) return rc;
   } else if (cfg == 5) {
     // Activation products on the 256x256 kernel: plain product (+ bias) into the kept

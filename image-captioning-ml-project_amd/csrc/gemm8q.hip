@@ -29,10 +29,26 @@
 //    where the phase issued a bias DMA).  Too small a count is safe (it only waits longer),
 //    so the run-time counts are rounded down to the encodings wait_le() has.
 //
+//  * Split tail round (round 4, SPT: grids whose last round is at most half full, e.g. the
+//    591 items = 2.31 rounds of a 50 432 x 768 product): after the R whole rounds, the rem
+//    leftover items are cut in two K halves run by a pair of WGs (virtual indices r and
+//    rem + r): WG r runs item r's upper K half FIRST (before its whole items) and hands its
+//    fp32 accumulators on (sc1 stores, drained, then a per-launch token in a flag word);
+//    WG rem + r runs the lower half LAST, starting from those accumulators (relaxed poll,
+//    agent acquire, loads straight into the zeroed accumulator registers), and writes the
+//    item.  The busiest WGs then run R + 1/2 items instead of R + 1.  The waiting side only
+//    waits for a WG whose first action is the hand-off, and WGs without a lower half never
+//    wait, so a launch cannot deadlock on WGs that are not yet resident; the split point is
+//    a function of K only (deterministic).  Contiguous-range stream-K over all items was
+//    measured slower (profiles/round4/streamk_contiguous_ab.txt: concurrent WGs no longer
+//    shared A row blocks in L2).
+//
 // Epilogue (compile-time forms, gemm8q_supports): bias, a forward GELU-family / ReLU
 // activation with act'(pre) (DV) or pre kept, OR one side operand -- the backward multiply by
 // aux = act'(pre), a residual, or beta*C -- and optionally (DSUM) the column sums of the
 // result.  alpha != 1, dropout and split-K run on gemm8p.
+#include <atomic>
+#include <ctime>
 #include <type_traits>
 
 #include "gemm_common.h"
@@ -42,6 +58,7 @@ namespace capk {
 namespace {
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) unsigned long long gu64;  // hand-off flag words: global, never flat
 
 // One segment of the side operand (8 elements of one row) loaded by an asm buffer load that
 // hipcc does not count; the epilogue waits for all of them with one vmcnt(0) statement that
@@ -103,7 +120,15 @@ struct Epi8q {
   int64_t ldc, lds, ldp;
   float beta;
   float* dsum;  // DSUM kernels: column-sum partials [2 * tile rows][N]
+  char* sk;     // split-tail hand-off workspace (SPT kernels)
+  unsigned long long token;  // this launch's hand-off token (nonzero, unique per host launch)
 };
+
+// split-tail workspace: 128 pair slots x 8 waves x 32 KiB of fp32 accumulators, then one flag
+// word per (slot, wave)
+constexpr size_t SPT_PART_BYTES = (size_t)128 * 8 * 32768;
+constexpr size_t SPT_WS_BYTES = SPT_PART_BYTES + (size_t)128 * 8 * 8;
+constexpr int SC1 = 16;  // buffer cache-policy bit (gfx950 sc1): write through / read past L1
 
 // s_waitcnt vmcnt(<= n) for a wave-uniform run-time n: the largest encoded count <= n
 __device__ __forceinline__ void wait_le(int n) {
@@ -122,7 +147,7 @@ __device__ __forceinline__ void wait_le(int n) {
 // DSUM: also the column sums of the final values (the bias gradient of the Linear whose
 // output gradient this dX is): per (tile row, wm) partial rows [2 ntm][N] into e.dsum,
 // summed in a fixed order by colsum_finish (capk_gemm_dx_act_colsum).
-template <bool AK, bool BK, typename OutT, int ACT, bool DV, int SK, bool DSUM = false>
+template <bool AK, bool BK, typename OutT, int ACT, bool DV, int SK, bool DSUM = false, bool SPT = false>
 __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A, int64_t lda,
                                                      const void* __restrict__ B, int64_t ldb, int M, int N, int K,
                                                      int splits, Epi8q e) {
@@ -135,9 +160,19 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
   const int ntn = (N + 255) / 256, ntiles = ((M + 255) / 256) * ntn, items = ntiles * splits;
   const int nk = ((K + 63) / 64 + splits - 1) / splits;  // K-tiles per item (>= 2: host)
   const int first = (blockIdx.x & 7) * 32 + (blockIdx.x >> 3);  // grid = 256
-  const int nmine = first < items ? (items - first + 255) >> 8 : 0;
-  if (nmine == 0) return;
-  const int total = nmine * nk;  // K-tile steps of this WG
+  // segments: [upper half of tail item] + whole items first + 256 j + [lower half of tail item]
+  // roles by contiguous virtual index (T: [0, rem), H: [rem, 2 rem)), so that the WGs running
+  // whole items side by side on an XCD -- which share A row blocks in its L2 -- start their
+  // whole items in the same phase (pairing 2r with 2r + 1 put every other WG half an item
+  // behind its neighbours and lost that sharing: profiles/round4/spt_ab.txt)
+  const int rem = SPT ? items & 255 : 0, rounds = SPT ? items >> 8 : 0, khalf = nk >> 1;
+  const bool hasT = SPT && first < rem;
+  const bool hasH = SPT && first >= rem && first < 2 * rem;
+  const int pair = hasT ? first : first - rem;
+  const int nwhole = SPT ? rounds : (first < items ? (items - first + 255) >> 8 : 0);
+  const int nseg = nwhole + hasT + hasH;
+  if (nseg == 0) return;
+  const int total = nwhole * nk + (hasT ? nk - khalf : 0) + (hasH ? khalf : 0);  // K-tile steps of this WG
 
   const __amdgpu_buffer_rsrc_t rsA = rsrc_of(A, (AK ? (int64_t)M * lda : (int64_t)K * lda) * 2);
   const __amdgpu_buffer_rsrc_t rsB = rsrc_of(B, (BK ? (int64_t)N * ldb : (int64_t)K * ldb) * 2);
@@ -147,11 +182,17 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
 
   struct Item {
     int m0, n0, kb;  // tile origin, first K-tile of the item's split
+    int k0, k1;      // K-tiles [k0, k1) of the item this segment runs
   };
   auto item_at = [&](int j) -> Item {
-    const int it = first + (j << 8);
+    int it = first + ((j - (hasT ? 1 : 0)) << 8), k0 = 0, k1 = nk;
+    if (SPT && ((hasT && j == 0) || (hasH && j == nseg - 1))) {  // a half of leftover item `pair`
+      it = (rounds << 8) + pair;
+      k0 = hasT ? khalf : 0;
+      k1 = hasT ? nk : khalf;
+    }
     const int sp = it / ntiles, tile = it - sp * ntiles, tm = tile / ntn;
-    return Item{tm * 256, (tile - tm * ntn) * 256, sp * nk};
+    return Item{tm * 256, (tile - tm * ntn) * 256, sp * nk, k0, k1};
   };
 
   // per-lane byte offsets of this wave's two 1-KiB pieces of each half (h: A0 A1 B0 B1) at
@@ -441,6 +482,61 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     return n0 + n1 + nd;
   };
 
+  // ---- SPT hand-off of the tail item `pair` (per wave: wave w pairs with wave w of the partner)
+  auto spt_rsrc = [&] { return rsrc_of(e.sk + (size_t)pair * (8 * 32768) + (size_t)wave * 32768, 32768); };
+  gu64* const spt_flag = (gu64*)(e.sk + SPT_PART_BYTES) + (size_t)pair * 8 + wave;
+  // publish the upper half's accumulators: written through (sc1), drained, then the flag;
+  // leaves nothing in flight
+  auto spt_publish = [&]() -> int {
+#if defined(CAPK_DIAG_SPTNOHO)  // diagnostic build: the split without the hand-off (wrong results)
+    return 0;
+#endif
+    const __amdgpu_buffer_rsrc_t rsP = spt_rsrc();
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            const int r = ((a * 2 + b) * 4 + i) * 2 + t;  // (register offset in the SGPR field: one VGPR)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, acc[a][b][i][t]), rsP,
+                                                   (uint32_t)(lane * 16), r * 1024, SC1);
+          }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(spt_flag, e.token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  };
+  // the lower half starts from them: bounded relaxed poll, agent acquire, loads straight into
+  // the (zeroed, dead) accumulators, flag back to 0 for the next launch on this memory
+  auto spt_consume = [&] {
+#if defined(CAPK_DIAG_SPTNOHO)
+    zero_acc();
+    return;
+#endif
+    for (int it = 0; it < (1 << 24); ++it) {
+      if (__hip_atomic_load(spt_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == e.token) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const __amdgpu_buffer_rsrc_t rsP = spt_rsrc();
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            const int r = ((a * 2 + b) * 4 + i) * 2 + t;
+            acc[a][b][i][t] = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsP, (uint32_t)(lane * 16), r * 1024, SC1));
+          }
+    if (lane == 0) __hip_atomic_store(spt_flag, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (also retires the in-flight prefetches and stores)
+  };
+
   // ---- main loop: gemm8p's two phases per K-tile over the continuous step sequence ----
   //   phase  quadrants          ds_read (L)           LDS-DMA issued (L)              wait (L)
   //   Q1     (0,0) (0,1)        A0(u) B0(u) B1(u)     A1(u+1)                         A1(u)
@@ -448,18 +544,19 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
   // Step u is K-tile k of item j (u = j nk + k); steps u+1, u+2 lie in item j or j+1 (nk >= 2).
   // Wait counts: Q1(u) leaves Q2(u-1)'s loads (6, +1 with a bias DMA) younger, Q2(u) leaves
   // Q1(u)'s 2; both + S when the epilogue of item j-1 ran since the awaited issue (k == 0).
-  int j = 0, k = 0;
-  Item cur = item_at(0), nxt = item_at(nmine > 1 ? 1 : 0);
+  // SPT: segments start at K-tile cur.k0 and end at cur.k1, each >= 2 K-tiles (host: nk >= 4)
+  Item cur = item_at(0), nxt = item_at(nseg > 1 ? 1 : 0);
+  int j = 0, k = SPT ? cur.k0 : 0;
   zero_acc();
   // prologue: A0 B0 B1 (+bias) of step 0, A1 of step 0, A0 B0 B1 of step 1
-  load(0, cur, 0, 0);
-  load(2, cur, 0, 0);
-  load(3, cur, 0, 0);
+  load(0, cur, k, 0);
+  load(2, cur, k, 0);
+  load(3, cur, k, 0);
   if (has_bias) bias_dma(cur, 0);
-  load(1, cur, 0, 0);
-  load(0, cur, 1, 1);
-  load(2, cur, 1, 1);
-  load(3, cur, 1, 1);
+  load(1, cur, k, 0);
+  load(0, cur, k + 1, 1);
+  load(2, cur, k + 1, 1);
+  load(3, cur, k + 1, 1);
   wait_vmc<8>();  // A0 B0 B1 (+bias) of step 0: A1(0) and step 1's three halves younger
   bar();
   if (lag) bar();  // waves 4-7 fall one barrier behind
@@ -473,7 +570,8 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     readA(fa, u, 0);
     readB(fb0, u, 2);
     readB(fb1, u, 3);
-    const int e1 = k == 0 ? S : 0;
+    const int kend = SPT ? cur.k1 : nk, kbn = SPT ? nxt.k0 : 0;  // this segment's end, the next's start
+    const int e1 = k == (SPT ? cur.k0 : 0) ? S : 0;
     {
       const int n1 = q2prev + e1;  // steady state: 6, +1 with a bias DMA in that phase
       if (n1 == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
@@ -481,8 +579,8 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
       else wait_le(n1);
     }
     if (has1) {
-      if (k + 1 < nk) load(1, cur, k + 1, u + 1);
-      else load(1, nxt, 0, u + 1);
+      if (k + 1 < kend) load(1, cur, k + 1, u + 1);
+      else load(1, nxt, kbn, u + 1);
     }
     lds_done();
     bar();
@@ -498,14 +596,14 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     else wait_le(q1n + e1);
     q2prev = 0;
     if (has2) {
-      const bool same = k + 2 < nk;
-      const int k2 = same ? k + 2 : k + 2 - nk;
+      const bool same = k + 2 < kend;
+      const int k2 = same ? k + 2 : kbn + (k + 2 - kend);
       const Item& t2 = same ? cur : nxt;
       load(0, t2, k2, u + 2);
       load(2, t2, k2, u + 2);
       load(3, t2, k2, u + 2);
       q2prev = 6;
-      if (k2 == 0 && has_bias) {
+      if ((SPT ? !same && k + 2 == kend : k2 == 0) && has_bias) {  // the next segment's first K-tile
         bias_dma(t2, j + 1);
         q2prev = 7;
       }
@@ -517,15 +615,27 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     mma(fa, fb0, acc[1][0]);
     __builtin_amdgcn_s_setprio(0);
     bar();
-    if (++k == nk) {  // the item's last K-tile: epilogue, stores left in flight
+    if (++k == kend) {  // the segment's last K-tile: epilogue, stores left in flight
       fence();
-      S = epilogue(cur, j);
-      zero_acc();
-      fence();
-      if (++j == nmine) break;
-      k = 0;
+      if constexpr (SPT) {
+        S = (hasT && j == 0) ? spt_publish() : epilogue(cur, j);  // upper half of the tail item: hand it on
+        if (++j == nseg) break;
+        if (hasH && j == nseg - 1) {  // lower half of the tail item: start from the partner's accumulators
+          spt_consume();
+          S = 0;
+        } else {
+          zero_acc();
+        }
+        fence();
+      } else {
+        S = epilogue(cur, j);
+        zero_acc();
+        fence();
+        if (++j == nseg) break;
+      }
       cur = nxt;
-      nxt = item_at(j + 1 < nmine ? j + 1 : j);
+      k = SPT ? cur.k0 : 0;
+      nxt = item_at(j + 1 < nseg ? j + 1 : j);
     }
   }
   if (!lag) bar();  // realign the two groups (every barrier is matched)
@@ -546,8 +656,33 @@ bool gemm8q_supports(const Epi& e, bool out_f32) {
   return sides <= (out_f32 ? 0 : 1) && (!(e.act & CAPK_ACT_BWD) || (e.act & CAPK_ACT_DERIV));
 }
 
+size_t gemm8q_spt_workspace() { return SPT_WS_BYTES; }
+
+// The split tail round pays when the last round is at most half full (its leftover items are
+// cut in halves over 2 * rem <= 256 WGs) and the halves are >= 2 K-tiles.  capk_gemm_set_spt /
+// CAPK_GEMM_SPT=0 turn it off (A/B).
+static int g_spt_mode = -1;
+static bool use_spt(int items, int nk) {
+  static const int env_mode = [] {
+    const char* v = getenv("CAPK_GEMM_SPT");
+    return v ? atoi(v) : 0;  // default off until it measures faster (profiles/round4/spt_ab.txt)
+  }();
+  const int mode = g_spt_mode >= 0 ? g_spt_mode : env_mode;
+  const int rem = items & 255;
+  return mode != 0 && rem != 0 && rem <= 128 && nk >= 4;
+}
+
+static unsigned long long next_token() {
+  static std::atomic<unsigned long long> ctr{0x2545F4914F6CDD1Dull ^ (unsigned long long)time(nullptr)};
+  unsigned long long t;
+  do t = ctr.fetch_add(0x9E3779B97F4A7C15ull) + 0x9E3779B97F4A7C15ull;
+  while (t == 0);
+  return t;
+}
+
 int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int64_t lda, const void* B, int64_t ldb,
-                  int M, int N, int K, int splits, const Epi& e, float* slab, hipStream_t st, float* dsum) {
+                  int M, int N, int K, int splits, const Epi& e, float* slab, hipStream_t st, float* dsum,
+                  void* spt_ws) {
   CAPK_CHECK_ARG((a_kmajor ? (int64_t)M * lda : (int64_t)K * lda) * 2 < (1ll << 31) &&
                      (b_kmajor ? (int64_t)N * ldb : (int64_t)K * ldb) * 2 < (1ll << 31),
                  "capk_gemm(bf16, 256x256): operand larger than 2 GiB");
@@ -584,10 +719,23 @@ int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int
                  "capk_gemm(bf16, 256x256): output or side operand larger than 2 GiB");
   const int items = cdiv(M, 256) * cdiv(N, 256);
   CAPK_CHECK_ARG(items > 256, "capk_gemm(gemm8q): persistent kernel for grids of more than 256 items");
+  // (not the DSUM form, whose register budget has no room for the hand-off; bf16 outputs only)
+  if (spt_ws && !dsum && !out_f32 && use_spt(items, cdiv(K, 64))) {
+    p.sk = (char*)spt_ws;
+    p.token = next_token();
+  }
   CAPK_CHECK_ARG(!fwd_act || (a_kmajor && b_kmajor), "capk_gemm(gemm8q): forward activations need K-major operands");
   const dim3 grid(256), block(512);
-#define L8(AK, BKM, OT, ACTK, DVK, SKK, DS) \
-  hipLaunchKernelGGL((gemm8q_kernel<AK, BKM, OT, ACTK, DVK, SKK, DS>), grid, block, 0, st, A, lda, B, ldb, M, N, K, 1, p)
+#define L8(AK, BKM, OT, ACTK, DVK, SKK, DS)                                                                        \
+  do {                                                                                                          \
+    constexpr bool SPTV = std::is_same<OT, bf16>::value && !DS;                                                 \
+    if (SPTV && p.sk)                                                                                           \
+      hipLaunchKernelGGL((gemm8q_kernel<AK, BKM, OT, ACTK, DVK, SKK, DS, SPTV>), grid, block, 0, st, A, lda, B,  \
+                         ldb, M, N, K, 1, p);                                                                   \
+    else                                                                                                        \
+      hipLaunchKernelGGL((gemm8q_kernel<AK, BKM, OT, ACTK, DVK, SKK, DS, false>), grid, block, 0, st, A, lda, B, \
+                         ldb, M, N, K, 1, p);                                                                   \
+  } while (0)
 #define L8SK(AK, BKM)                                      \
   switch (sk) {                                            \
     case SIDE_AUX: L8(AK, BKM, bf16, 0, false, SIDE_AUX, false); break; \
@@ -632,3 +780,9 @@ int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int
 }
 
 }  // namespace capk
+
+extern "C" int capk_gemm_set_spt(int mode) {
+  CAPK_CHECK_ARG(mode >= -1 && mode <= 1, "capk_gemm_set_spt: mode must be -1 (environment), 0 or 1");
+  capk::g_spt_mode = mode;
+  return CAPK_OK;
+}

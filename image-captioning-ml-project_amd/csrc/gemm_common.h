@@ -340,7 +340,11 @@ bool gemm8q_supports(const Epi& e, bool out_f32);
 int launch_colsum_finish(int parts, int N, const float* part, float* out, int accumulate, hipStream_t st);
 // dsum != nullptr: the dX x act' product also writes per-(tile row, wave row) column-sum
 // partials [2 * cdiv(M, 256)][N] fp32 there (capk_gemm_dx_act_colsum)
+// spt_ws != nullptr (gemm8q_spt_workspace() bytes, any contents): the split tail round for
+// grids whose last round is at most half full
 int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int64_t lda, const void* B, int64_t ldb,
-                  int M, int N, int K, int splits, const Epi& e, float* slab, hipStream_t st, float* dsum = nullptr);
+                  int M, int N, int K, int splits, const Epi& e, float* slab, hipStream_t st, float* dsum = nullptr,
+                  void* spt_ws = nullptr);
+size_t gemm8q_spt_workspace();
 
 }  // namespace capk

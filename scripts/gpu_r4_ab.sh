@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round-4 A/B session: GEMM split-tail on/off per shape, config-3 bench with the MFMA
+# cross-attention kernels on/off, then a kernel-trace profile of the default build.
+set -u
+OUT=gpurun_out/r4
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "== $name" | tee -a $OUT/status
+  timeout -k 10 $secs "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a $OUT/status
+  grep -v amdgpu.ids $OUT/$name.log | tail -${TAILN:-12} | cut -c1-400
+  [ $rc -eq 0 ] || [ $rc -eq 1 ] || { echo "stopping after $name (rc=$rc)"; exit $rc; }
+}
+export GEMM_SHAPES="dx768_197:50432:768:768:dx,dx3072_197:50432:768:3072:dx,dx2304_197:50432:768:2304:dx,res768_197:50432:768:768:fwd_res,res3072_197:50432:768:3072:fwd_res,fc1g_197:50432:3072:768:fwd_gelu_deriv,lmfwd:5120:50304:768:fwd"
+[[ ${SKIP_SPT:-0} == 0 ]] && CAPK_GEMM_SPT=1 run spt_on 200 python tools/gemm_bench.py
+[[ ${SKIP_SPT:-0} == 0 ]] && CAPK_GEMM_SPT=0 run spt_off 200 python tools/gemm_bench.py
+[[ ${SKIP_SPT:-0} == 0 ]] && CAPK_GEMM_SPT=1 CAPK_LIB_PATH=image-captioning-ml-project_amd/capk/libcapk_diag_sptnoho.so run spt_noho 200 python tools/gemm_bench.py
+TAILN=1 run bench_xdec 400 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --beam-batch 0
+TAILN=1 CAPK_XDEC=0 run bench_noxdec 400 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --beam-batch 0
+[[ ${PROF:-1} == 1 ]] && TAILN=2 run prof3 420 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof3 -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --beam-batch 0
+exit 0

@@ -181,3 +181,64 @@ def test_dx_act_colsum_fused(M):
     refb = out.float().sum(0)  # the sums of the values actually stored (bf16-rounded) ...
     assert _rel(db, ref.sum(0)) < 2e-3  # ... and of the exact product
     assert _rel(db, refb) < 2e-3
+
+
+@cuda
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
+def test_split_tail_exact(mode, ak, bk):
+    """The persistent kernel's split tail round (capk_gemm_set_spt(1): the leftover items of a
+    last round at most half full run as two K halves on a pair of workgroups, the upper half
+    handed to the lower through the workspace) vs whole items (0): a 273-item grid (21 x 13
+    tiles, 17 leftover items, each split) with K = 640 (10 K-tiles, halves of 5), exact
+    small-integer operands (every partial sum exact in fp32, so the hand-off must reproduce the
+    product bit for bit), plain / bias + residual / beta * C / GELU + act' / backward * aux
+    epilogues, element by element; then two launches on one workspace (the flag words cleared)."""
+    from capk import _lib, ops
+    from capk._lib import ACT_DERIV, ACT_GELU_ERF
+    L = _lib.load()
+    L.capk_gemm_force_config(6)
+    L.capk_gemm_set_spt(mode)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(21 + 2 * ak + bk)
+        M, N, K = 20 * 256 + 72, 13 * 256, 640
+        a = torch.randint(-2, 3, (M, K), device="cuda", generator=g).bfloat16()
+        w = torch.randint(-2, 3, (N, K), device="cuda", generator=g).bfloat16()
+        A = a if ak else a.t().contiguous()
+        B = w if bk else w.t().contiguous()
+        ref = a.float() @ w.float().t()  # |x| <= 2560: exact in fp32; C = its bf16 rounding
+        C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        kw = dict(lda=A.stride(0), ldb=B.stride(0), ldc=N)
+        ops.gemm(A, ak, B, bk, M, N, K, C, **kw)
+        assert L.capk_gemm_last_config() == 6
+        assert torch.equal(C.float(), ref.bfloat16().float())
+        bias = torch.randint(-3, 4, (N,), device="cuda", generator=g).float()
+        res = torch.randint(-8, 9, (M, N), device="cuda", generator=g).bfloat16()
+        ops.gemm(A, ak, B, bk, M, N, K, C, bias=bias, residual=res, ldr=N, **kw)
+        assert torch.equal(C.float(), (ref + bias + res.float()).bfloat16().float())
+        C0 = torch.randint(-8, 9, (M, N), device="cuda", generator=g).bfloat16()
+        C.copy_(C0)
+        ops.gemm(A, ak, B, bk, M, N, K, C, beta=1.0, **kw)
+        assert torch.equal(C.float(), (ref + C0.float()).bfloat16().float())
+        if ak and bk:  # forward activation (K-major only) and the backward multiply
+            x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+            pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            y = ops.linear(x, w / 64, bias, act=ACT_GELU_ERF | ACT_DERIV, preact=pre)
+            z = (x.float() @ (w.float() / 64).t() + bias).requires_grad_(True)
+            F.gelu(z).sum().backward()
+            assert _rel(y, F.gelu(z.detach())) < 1e-2 and _rel(pre, z.grad) < 1e-2
+            aux = torch.randint(0, 3, (M, N), device="cuda", generator=g).bfloat16()
+            out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            ops.gemm(a, True, w, True, M, N, K, out, lda=K, ldb=K, ldc=N, act=16 | ACT_GELU_ERF | ACT_DERIV, aux=aux,
+                     ldx=N)
+            assert torch.equal(out.float(), (ref * aux.float()).bfloat16().float())
+        ws = torch.empty(L.capk_gemm_workspace(1, 1, M, N, K), dtype=torch.uint8, device="cuda")
+        C1 = torch.empty_like(C)
+        for _ in range(2):
+            _lib.check(L.capk_gemm(1, 1, M, N, K, A.data_ptr(), A.stride(0), int(ak), B.data_ptr(), B.stride(0),
+                                   int(bk), C1.data_ptr(), N, 1.0, 0.0, None, None, 0, 0, None, None, 0, 0.0, 0,
+                                   ws.data_ptr(), ws.numel(), ops._stream()), "capk_gemm")
+            assert torch.equal(C1.float(), ref.bfloat16().float())
+    finally:
+        L.capk_gemm_set_spt(-1)
+        L.capk_gemm_force_config(-1)

@@ -437,3 +437,62 @@ def test_act_bwd_colsum(ops, dtype, deriv):
     db2 = db.clone()
     ops.act_bwd_colsum(c.clone(), aux, ACT_GELU_ERF | (ACT_DERIV if deriv else 0), db2, accumulate=True)
     assert db2.shape == db.shape and bool(torch.isfinite(db2).all())
+
+
+@cuda
+@pytest.mark.parametrize("case", ["dec_cross_drop", "qformer_cross", "cross_q16_pad"])
+def test_cross_attention_xdec_train(ops, case):
+    """Short query blocks against memory keys on the MFMA xdec kernel (chosen for 2 <= Nq <= 32,
+    64 < Nk <= 256, hd 64 / 96 / 128): the training decoder's cross-attention (Nq = 20 caption
+    positions, Nk = 196 memory keys, hd 96) with probability dropout p = 0.1 -- the mask is
+    materialised by capk_dropout_mask at index ((b*H + h)*Nq + q)*Nk + key, as attn_bwd
+    recomputes it -- the QFormer's 32 queries (two query tiles, hd 64), and 16 queries with a
+    key-padding mask; forward (O, and the lse through the backward) and the backward that
+    consumes it, bf16 vs an fp32 reference on the bf16 inputs."""
+    from capk.ops import HeadView
+    g = torch.Generator(device="cuda").manual_seed(17)
+    p, seed = 0.0, 0
+    key_pad = None
+    if case == "dec_cross_drop":
+        B, H, Nq, Nk, hd = 24, 8, 20, 196, 96
+        p, seed = 0.1, 4242
+    elif case == "qformer_cross":
+        B, H, Nq, Nk, hd = 10, 12, 32, 196, 64
+    else:
+        B, H, Nq, Nk, hd = 6, 4, 16, 150, 128
+        key_pad = torch.zeros(B, Nk, dtype=torch.bool, device="cuda")
+        key_pad[1, 100:] = True
+        key_pad[4, 7] = True
+    D = H * hd
+    dt = torch.bfloat16
+    q = torch.randn(B * Nq, D, device="cuda", generator=g).to(dt)
+    kv = torch.randn(B * Nk, 2 * D, device="cuda", generator=g).to(dt)
+    do = torch.randn(B * Nq, D, device="cuda", generator=g).to(dt)
+    o = torch.empty(B * Nq, D, device="cuda", dtype=dt)
+    qv, ov = HeadView(q, 0, Nq * D, D), HeadView(o, 0, Nq * D, D)
+    kview, vview = HeadView(kv, 0, Nk * 2 * D, 2 * D), HeadView(kv, D, Nk * 2 * D, 2 * D)
+    scale = 1.0 / math.sqrt(hd)
+    lse, kp = ops.attention_fwd(qv, kview, vview, ov, B, H, Nq, Nk, hd, scale, key_pad=key_pad, drop=(p, seed))
+    qr = q.float().view(B, Nq, H, hd).transpose(1, 2).contiguous().requires_grad_(True)
+    kr = kv[:, :D].float().reshape(B, Nk, H, hd).transpose(1, 2).contiguous().requires_grad_(True)
+    vr = kv[:, D:].float().reshape(B, Nk, H, hd).transpose(1, 2).contiguous().requires_grad_(True)
+    s = torch.einsum("bhqd,bhkd->bhqk", qr, kr) * scale
+    if key_pad is not None:
+        s = s.masked_fill(key_pad[:, None, None, :], float("-inf"))
+    a = torch.softmax(s, -1)
+    if p > 0:
+        a = a * (ops.dropout_mask(B * H * Nq * Nk, p, seed).view(B, H, Nq, Nk).float() / (1 - p))
+    ref = torch.einsum("bhqk,bhkd->bhqd", a, vr)
+    got = o.float().view(B, Nq, H, hd).transpose(1, 2)
+    assert _rel(got, ref) < 1.5e-2
+    ref_lse = torch.logsumexp(s, -1)
+    assert _rel(lse, ref_lse) < 1e-3
+    ref.backward(do.float().view(B, Nq, H, hd).transpose(1, 2))
+    dq = torch.empty_like(q)
+    dkv = torch.zeros_like(kv)
+    ops.attention_bwd(qv, kview, vview, ov, HeadView(do, 0, Nq * D, D), lse, HeadView(dq, 0, Nq * D, D),
+                      HeadView(dkv, 0, Nk * 2 * D, 2 * D), HeadView(dkv, D, Nk * 2 * D, 2 * D),
+                      B, H, Nq, Nk, hd, scale, key_pad_u8=kp, drop=(p, seed))
+    assert _rel(dq.float().view(B, Nq, H, hd).transpose(1, 2), qr.grad) < 3e-2
+    assert _rel(dkv[:, :D].float().reshape(B, Nk, H, hd).transpose(1, 2), kr.grad) < 3e-2
+    assert _rel(dkv[:, D:].float().reshape(B, Nk, H, hd).transpose(1, 2), vr.grad) < 3e-2
