@@ -1367,6 +1367,226 @@ __global__ __launch_bounds__(256) void attn_xbwd_bf16(AttnArgs a) {
   }
 }
 
+// --------------------------------------------- short sequences: one wave per (batch, head) ---
+// The decoder's causal self-attention (T = 20 caption positions, hd 96, key-padding mask of the
+// caption pads, probability dropout; nn.TransformerDecoderLayer.self_attn via
+// src/models/decoders.py:421-428): <= 32 queries x <= 32 keys per (batch, head) is a handful of
+// MFMAs, so the 8-wave per-(batch, head) kernels spent their time on set-up and barriers.  Here
+// one wave owns a (batch, head): S^T = K Q^T from global fragments (the xdec layout, query on
+// the lane), softmax over the 32 keys in registers (two xor-shuffles), O^T = V^T P^T with V^T
+// by transposed reads of the wave's own LDS image; no barriers.  WG = SW_WAVES waves.
+constexpr int SW_WAVES = 4;
+template <int HDP, int MODE>
+__global__ __launch_bounds__(64 * SW_WAVES) void attn_short_fwd_bf16(AttnArgs a) {
+  constexpr int ST = HDP + 16, NCH = HDP / 8, NS = HDP / 32, ND = HDP / 16;
+  __shared__ __attribute__((aligned(16))) bf16 vimg[SW_WAVES][32 * ST];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
+  const int bh = blockIdx.x * SW_WAVES + w;
+  if (bh >= a.B * a.H) return;  // (wave-uniform; no barriers below)
+  const int b = bh / a.H, h = bh % a.H, hoff = h * a.hd;
+  const bf16* kbase = (const bf16*)a.k + (int64_t)b * a.k_bs + hoff;
+  const bf16* vbase = (const bf16*)a.v + (int64_t)b * a.v_bs + hoff;
+  bf16x8 qf[2][NS], kf[2][NS];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int r = 16 * t + c16, d = s * 32 + 8 * g;
+      qf[t][s] = (r < a.Nq && d < a.hd) ? ld8((const bf16*)a.q + (int64_t)b * a.q_bs + (int64_t)r * a.q_rs + hoff + d)
+                                        : zero8();
+      kf[t][s] = (r < a.Nk && d < a.hd) ? ld8(kbase + (int64_t)r * a.k_rs + d) : zero8();
+    }
+  bf16* Vs = vimg[w];
+  constexpr int VIT = 32 * NCH / 64;
+#pragma unroll
+  for (int i = 0; i < VIT; ++i) {
+    const int ch = lane + 64 * i, row = ch / NCH, col = (ch % NCH) * 8;
+    *(bf16x8*)(Vs + row * ST + col) = (row < a.Nk && col < a.hd) ? ld8(vbase + (int64_t)row * a.v_rs + col) : zero8();
+  }
+  const float sl2 = a.scale * kLog2e;
+  f32x4 sc[2][2];  // [query tile][key block]: lane = query 16 qt + c16, keys 16 kb + 4g + r
+  f32x4 o[2][ND];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int q = 16 * qt + c16;
+    float m = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < NS; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kb][s], qf[qt][s], acc, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = 16 * kb + 4 * g + r;
+        const bool ok = (MODE & AM_MASK) ? key_ok(a, b, key, q) : key < a.Nk;
+        acc[r] = ok ? acc[r] * sl2 : -INFINITY;
+        m = fmaxf(m, acc[r]);
+      }
+      sc[qt][kb] = acc;
+    }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float l = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = m == -INFINITY ? 0.f : fexp2(sc[qt][kb][r] - m);
+        l += p;  // the normaliser excludes dropout
+        sc[qt][kb][r] = dropm<MODE>() && q < a.Nq ? p * pdrop(a, b, h, q, 16 * kb + 4 * g + r) : p;
+      }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    if (q < a.Nq && g == 0) a.lse[((int64_t)b * a.H + h) * a.Nq + q] = l > 0.f ? (m + __log2f(l)) * kLn2 : -INFINITY;
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) sc[qt][kb] *= inv;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's V image is written
+#pragma unroll
+  for (int db = 0; db < ND; ++db) {
+    const bf16x8 vt = tr_read8(Vs, ST, 0, db * 16, lane);
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      o[qt][db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt, pack8(sc[qt][0], sc[qt][1]), z, 0, 0, 0);
+    }
+  }
+  // O^T fragments: lane = query, rows = dims 16 db + 4g + r -> 8-B row stores
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int q = 16 * qt + c16;
+    if (q < a.Nq) {
+      bf16* orow = (bf16*)a.out + (int64_t)b * a.out_bs + (int64_t)q * a.out_rs + hoff;
+#pragma unroll
+      for (int db = 0; db < ND; ++db) {
+        const int d0 = db * 16 + 4 * g;
+        if (d0 < a.hd) store4(orow + d0, o[qt][db], 1.f);
+      }
+    }
+  }
+}
+
+// Backward of attn_short_fwd_bf16: one wave per (batch, head), attn_xbwd_bf16's products for
+// one 32-key chunk (dV^T = dO^T (P m), dK^T = Q^T dS with the key on the lane; dQ^T = K^T dS^T
+// through the wave's transposed K and dS images, so dQ rows are stored directly).
+constexpr int SB_WAVES = 2;
+template <int HDP, int MODE>
+__global__ __launch_bounds__(64 * SB_WAVES) void attn_short_bwd_bf16(AttnArgs a) {
+  constexpr int ST = HDP + 16, NS = HDP / 32, ND = HDP / 16, NCH = HDP / 8, DST = 32 + 8;
+  __shared__ __attribute__((aligned(16))) bf16 qimg[SB_WAVES][32 * ST], doimg[SB_WAVES][32 * ST];
+  __shared__ __attribute__((aligned(16))) bf16 kimg[SB_WAVES][32 * ST], dsimg[SB_WAVES][32 * DST];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
+  const int bh = blockIdx.x * SB_WAVES + w;
+  if (bh >= a.B * a.H) return;  // (wave-uniform; no barriers below)
+  const int b = bh / a.H, h = bh % a.H, hoff = h * a.hd;
+  bf16 *Qi = qimg[w], *dOi = doimg[w], *Ki = kimg[w], *dSi = dsimg[w];
+  // images: rows 0..31 (zero past Nq / Nk), 16-B chunks round-robin over the wave
+  constexpr int IT = 32 * NCH / 64;
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int ch = lane + 64 * i, r = ch / NCH, c = (ch % NCH) * 8;
+    const bool iq = r < a.Nq && c < a.hd, ik = r < a.Nk && c < a.hd;
+    *(bf16x8*)(Qi + r * ST + c) = iq ? ld8((const bf16*)a.q + (int64_t)b * a.q_bs + (int64_t)r * a.q_rs + hoff + c) : zero8();
+    *(bf16x8*)(dOi + r * ST + c) =
+        iq ? ld8((const bf16*)a.dout + (int64_t)b * a.do_bs + (int64_t)r * a.do_rs + hoff + c) : zero8();
+    *(bf16x8*)(Ki + r * ST + c) = ik ? ld8((const bf16*)a.k + (int64_t)b * a.k_bs + (int64_t)r * a.k_rs + hoff + c) : zero8();
+  }
+  // D[q] = rowsum(dO * O) for the lane's 4 queries 4g + r of each tile (O from global, dO
+  // from the image once it is written), lse
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  float lq[2][4], dd[2][4];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = 16 * qt + 4 * g + r;
+      lq[qt][r] = q < a.Nq ? a.lse_in[((int64_t)b * a.H + h) * a.Nq + q] * kLog2e : INFINITY;
+      // 16 lanes (c16) share the row: each sums hd / 16 columns, then xor-reduce over c16
+      float d = 0.f;
+      if (q < a.Nq)
+        for (int c = c16 * 8; c < a.hd; c += 128) {
+          const bf16x8 ov = ld8((const bf16*)a.o + (int64_t)b * a.o_bs + (int64_t)q * a.o_rs + hoff + c);
+          const bf16x8 dv = *(const bf16x8*)(dOi + q * ST + c);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) d += (float)ov[i] * (float)dv[i];
+        }
+      d += __shfl_xor(d, 1, 64);
+      d += __shfl_xor(d, 2, 64);
+      d += __shfl_xor(d, 4, 64);
+      d += __shfl_xor(d, 8, 64);
+      dd[qt][r] = d;
+    }
+  bf16x8 qf[2][NS], dof[2][NS], kf[2][NS], vf[2][NS];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int r = 16 * t + c16, d = s * 32 + 8 * g;
+      qf[t][s] = *(const bf16x8*)(Qi + r * ST + d);
+      dof[t][s] = *(const bf16x8*)(dOi + r * ST + d);
+      kf[t][s] = *(const bf16x8*)(Ki + r * ST + d);
+      vf[t][s] = (r < a.Nk && d < a.hd) ? ld8((const bf16*)a.v + (int64_t)b * a.v_bs + (int64_t)r * a.v_rs + hoff + d)
+                                        : zero8();
+    }
+  const float sl2 = a.scale * kLog2e;
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+    const int key = 16 * kb + c16;
+    f32x4 p[2], ds[2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      f32x4 sa = {0.f, 0.f, 0.f, 0.f}, dpa = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        sa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[qt][s], kf[kb][s], sa, 0, 0, 0);
+        dpa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dof[qt][s], vf[kb][s], dpa, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int q = 16 * qt + 4 * g + r;
+        const bool ok = (MODE & AM_MASK) ? key_ok(a, b, key, q) : key < a.Nk;
+        const float pv = ok ? fexp2(sa[r] * sl2 - lq[qt][r]) : 0.f;
+        const float mk = dropm<MODE>() && q < a.Nq ? pdrop(a, b, h, q, key) : 1.f;
+        p[qt][r] = pv * mk;
+        ds[qt][r] = pv * (dpa[r] * mk - dd[qt][r]);
+      }
+      bf16x4 d4;
+      d4[0] = (bf16)ds[qt][0]; d4[1] = (bf16)ds[qt][1]; d4[2] = (bf16)ds[qt][2]; d4[3] = (bf16)ds[qt][3];
+      *(bf16x4*)(dSi + key * DST + 16 * qt + 4 * g) = d4;
+    }
+    const bf16x8 pb = pack8(p[0], p[1]), dsb = pack8(ds[0], ds[1]);
+    bf16* dkrow = (bf16*)a.dk + (int64_t)b * a.dk_bs + (int64_t)key * a.dk_rs + hoff;
+    bf16* dvrow = (bf16*)a.dv + (int64_t)b * a.dv_bs + (int64_t)key * a.dv_rs + hoff;
+#pragma unroll
+    for (int db = 0; db < ND; ++db) {
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      const f32x4 dv4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_read8(dOi, ST, 0, db * 16, lane), pb, z, 0, 0, 0);
+      const f32x4 dk4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_read8(Qi, ST, 0, db * 16, lane), dsb, z, 0, 0, 0);
+      const int d0 = db * 16 + 4 * g;
+      if (key < a.Nk && d0 < a.hd) {
+        store4(dkrow + d0, dk4, a.scale);
+        store4(dvrow + d0, dv4, 1.f);
+      }
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the dS image is written
+  // dQ^T[d][q] = K^T dS^T over the 32 keys (tr_read8's k order on both sides): lane = query
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const bf16x8 dst = tr_read8(dSi, DST, 0, 16 * qt, lane);
+    const int q = 16 * qt + c16;
+    bf16* dqrow = (bf16*)a.dq + (int64_t)b * a.dq_bs + (int64_t)q * a.dq_rs + hoff;
+#pragma unroll
+    for (int db = 0; db < ND; ++db) {
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      const f32x4 dq4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_read8(Ki, ST, 0, db * 16, lane), dst, z, 0, 0, 0);
+      const int d0 = db * 16 + 4 * g;
+      if (q < a.Nq && d0 < a.hd) store4(dqrow + d0, dq4, a.scale);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- decode v2 ---
 // KV-cached decode attention (Nq <= 8 queries per (batch, head): one beam row's query, or the
 // k beams of one image against its shared memory K/V).  The step is HBM-bound on the K/V
@@ -1592,6 +1812,24 @@ extern "C" int capk_attention_fwd(int dtype, int B, int H, int Nq, int Nk, int h
                      k_bs % 8 == 0 && v_bs % 8 == 0,
                  "capk_attention_fwd(bf16): strides must allow 16-B vector access");
   static const bool decode_v1 = [] { const char* e = getenv("CAPK_DECODE_V1"); return e && e[0] == '1'; }();
+  // short sequences (the decoder / GPT-2 / QFormer self-attention: 8 < Nq <= 32, Nk <= 32): one
+  // wave per (batch, head) (CAPK_SHORT_ATTN=0: the per-(batch, head) 8-wave kernel, for A/B)
+  static const bool short_on = [] { const char* e = getenv("CAPK_SHORT_ATTN"); return !(e && e[0] == '0'); }();
+  if (short_on && Nq > 8 && Nq <= 32 && Nk <= 32 && (hd == 64 || hd == 96 || hd == 128)) {
+    const dim3 g(cdiv(B * H, SW_WAVES)), blk(64 * SW_WAVES);
+    const int sm = (causal || key_pad ? AM_MASK : 0) | (drop_p > 0.f ? AM_DROP : 0);
+#define SFM(HD)                                                                                    \
+  switch (sm) {                                                                                    \
+    case 0: hipLaunchKernelGGL((attn_short_fwd_bf16<HD, 0>), g, blk, 0, st, a); break;               \
+    case AM_DROP: hipLaunchKernelGGL((attn_short_fwd_bf16<HD, AM_DROP>), g, blk, 0, st, a); break;   \
+    case AM_MASK: hipLaunchKernelGGL((attn_short_fwd_bf16<HD, AM_MASK>), g, blk, 0, st, a); break;   \
+    default: hipLaunchKernelGGL((attn_short_fwd_bf16<HD, AM_MASK | AM_DROP>), g, blk, 0, st, a); break; \
+  }
+    if (hd == 64) { SFM(64) } else if (hd == 96) { SFM(96) } else { SFM(128) }
+#undef SFM
+    CAPK_LAUNCH_CHECK("attn_short_fwd_bf16");
+    return CAPK_OK;
+  }
   // short query blocks against memory keys (beam cross-attention steps: k beams of an image;
   // the training decoder's cross-attention: T = 20 positions, with dropout): the MFMA xdec
   // kernel (CAPK_XDEC=0 keeps the beam steps on the VALU decode kernel and the training
@@ -1751,6 +1989,22 @@ extern "C" int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int h
     default: CALL2(128, M); break; \
   }
   int rc2 = CAPK_OK;
+  static const bool short_on = [] { const char* e = getenv("CAPK_SHORT_ATTN"); return !(e && e[0] == '0'); }();
+  if (short_on && Nq > 8 && Nq <= 32 && Nk <= 32 && (hd == 64 || hd == 96 || hd == 128)) {
+    const dim3 g(cdiv(B * H, SB_WAVES)), blk(64 * SB_WAVES);
+    const int sm = (causal || key_pad ? AM_MASK : 0) | (drop_p > 0.f ? AM_DROP : 0);
+#define SBM(HD)                                                                                    \
+  switch (sm) {                                                                                    \
+    case 0: hipLaunchKernelGGL((attn_short_bwd_bf16<HD, 0>), g, blk, 0, st, a); break;               \
+    case AM_DROP: hipLaunchKernelGGL((attn_short_bwd_bf16<HD, AM_DROP>), g, blk, 0, st, a); break;   \
+    case AM_MASK: hipLaunchKernelGGL((attn_short_bwd_bf16<HD, AM_MASK>), g, blk, 0, st, a); break;   \
+    default: hipLaunchKernelGGL((attn_short_bwd_bf16<HD, AM_MASK | AM_DROP>), g, blk, 0, st, a); break; \
+  }
+    if (hd == 64) { SBM(64) } else if (hd == 96) { SBM(96) } else { SBM(128) }
+#undef SBM
+    CAPK_LAUNCH_CHECK("attn_short_bwd_bf16");
+    return CAPK_OK;
+  }
   // short query blocks against memory keys (the training decoder's cross-attention): the
   // MFMA xbwd kernel, the backward of attn_xdec_bf16 (CAPK_XDEC=0: the fused kernel below)
   static const bool xbwd_on = [] { const char* e = getenv("CAPK_XDEC"); return !(e && e[0] == '0'); }();

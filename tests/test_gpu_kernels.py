@@ -496,3 +496,63 @@ def test_cross_attention_xdec_train(ops, case):
     assert _rel(dq.float().view(B, Nq, H, hd).transpose(1, 2), qr.grad) < 3e-2
     assert _rel(dkv[:, :D].float().reshape(B, Nk, H, hd).transpose(1, 2), kr.grad) < 3e-2
     assert _rel(dkv[:, D:].float().reshape(B, Nk, H, hd).transpose(1, 2), vr.grad) < 3e-2
+
+
+@cuda
+@pytest.mark.parametrize("case", ["dec_self_drop", "qformer_self", "gpt2_prefix"])
+def test_short_attention_train(ops, case):
+    """Short sequences on the one-wave-per-(batch, head) kernels (chosen for 8 < Nq <= 32,
+    Nk <= 32): the training decoder's causal self-attention (T = 20, hd 96) with the caption
+    key-padding mask and probability dropout p = 0.1 (mask materialised by capk_dropout_mask
+    at ((b*H + h)*Nq + q)*Nk + key, as the backward recomputes it), the QFormer's 32 queries
+    (hd 64, no mask), and a causal 20-query block over 30 keys (a 10-slot prefix, bottom-right
+    aligned); forward, lse and backward, bf16 vs an fp32 reference on the bf16 inputs."""
+    from capk.ops import HeadView
+    g = torch.Generator(device="cuda").manual_seed(23)
+    p, seed, causal, key_pad = 0.0, 0, False, None
+    if case == "dec_self_drop":
+        B, H, Nq, Nk, hd = 40, 8, 20, 20, 96
+        p, seed, causal = 0.1, 777, True
+        key_pad = torch.zeros(B, Nk, dtype=torch.bool, device="cuda")
+        key_pad[1, 12:] = True
+        key_pad[5, 19] = True
+    elif case == "qformer_self":
+        B, H, Nq, Nk, hd = 12, 12, 32, 32, 64
+    else:
+        B, H, Nq, Nk, hd = 9, 12, 20, 30, 64
+        causal = True
+    D = H * hd
+    dt = torch.bfloat16
+    q = torch.randn(B * Nq, D, device="cuda", generator=g).to(dt)
+    kv = torch.randn(B * Nk, 2 * D, device="cuda", generator=g).to(dt)
+    do = torch.randn(B * Nq, D, device="cuda", generator=g).to(dt)
+    o = torch.empty(B * Nq, D, device="cuda", dtype=dt)
+    qv, ov = HeadView(q, 0, Nq * D, D), HeadView(o, 0, Nq * D, D)
+    kview, vview = HeadView(kv, 0, Nk * 2 * D, 2 * D), HeadView(kv, D, Nk * 2 * D, 2 * D)
+    scale = 1.0 / math.sqrt(hd)
+    lse, kp = ops.attention_fwd(qv, kview, vview, ov, B, H, Nq, Nk, hd, scale, causal=causal, key_pad=key_pad,
+                                drop=(p, seed))
+    qr = q.float().view(B, Nq, H, hd).transpose(1, 2).contiguous().requires_grad_(True)
+    kr = kv[:, :D].float().reshape(B, Nk, H, hd).transpose(1, 2).contiguous().requires_grad_(True)
+    vr = kv[:, D:].float().reshape(B, Nk, H, hd).transpose(1, 2).contiguous().requires_grad_(True)
+    s = torch.einsum("bhqd,bhkd->bhqk", qr, kr) * scale
+    if causal:  # bottom-right aligned: key j visible to query i when j <= i + Nk - Nq
+        s = s.masked_fill(torch.ones(Nq, Nk, dtype=torch.bool, device="cuda").triu(1 + Nk - Nq), float("-inf"))
+    if key_pad is not None:
+        s = s.masked_fill(key_pad[:, None, None, :], float("-inf"))
+    a = torch.softmax(s, -1)
+    if p > 0:
+        a = a * (ops.dropout_mask(B * H * Nq * Nk, p, seed).view(B, H, Nq, Nk).float() / (1 - p))
+    ref = torch.einsum("bhqk,bhkd->bhqd", a, vr)
+    got = o.float().view(B, Nq, H, hd).transpose(1, 2)
+    assert _rel(got, ref) < 1.5e-2
+    assert _rel(lse, torch.logsumexp(s, -1)) < 1e-3
+    ref.backward(do.float().view(B, Nq, H, hd).transpose(1, 2))
+    dq = torch.empty_like(q)
+    dkv = torch.zeros_like(kv)
+    ops.attention_bwd(qv, kview, vview, ov, HeadView(do, 0, Nq * D, D), lse, HeadView(dq, 0, Nq * D, D),
+                      HeadView(dkv, 0, Nk * 2 * D, 2 * D), HeadView(dkv, D, Nk * 2 * D, 2 * D),
+                      B, H, Nq, Nk, hd, scale, causal=causal, key_pad_u8=kp, drop=(p, seed))
+    assert _rel(dq.float().view(B, Nq, H, hd).transpose(1, 2), qr.grad) < 3e-2
+    assert _rel(dkv[:, :D].float().reshape(B, Nk, H, hd).transpose(1, 2), kr.grad) < 3e-2
+    assert _rel(dkv[:, D:].float().reshape(B, Nk, H, hd).transpose(1, 2), vr.grad) < 3e-2
