@@ -59,6 +59,13 @@ SIGNATURES = {
                                 _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p,      # o, dout, lse
                                 _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _i64, _i64,  # dq dk dv
                                 _f, _u32, _c_p]),
+    "capk_attention_bwd_bias_workspace": (_sz, [_i, _i, _i, _i, _i]),
+    "capk_attention_bwd_bias": (_i, [_i, _i, _i, _i, _i, _i, _f, _i,
+                                     _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _i64, _i64,
+                                     _c_p,
+                                     _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p,
+                                     _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _i64, _i64,
+                                     _f, _u32, _c_p, _i, _c_p, _sz, _c_p]),   # ... drop, dbias, accumulate, ws
     "capk_patchify": (_i, [_i, _i, _i, _i, _i, _i, _c_p, _c_p, _c_p]),
     "capk_vit_assemble": (_i, [_i, _i, _i, _i, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "capk_vit_assemble_bwd_workspace": (_sz, [_i, _i, _i]),

@@ -16,6 +16,7 @@ Activations live as [B*(N+1), D] row-major buffers; heads are addressed by
 stride, so there are no transposes anywhere.
 """
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -24,6 +25,12 @@ from .. import ops
 from .._lib import ACT_DERIV, ACT_GELU_ERF, ACT_TANH
 from ..params import Fused, notify_final, store_of
 from .common import G, CapkModule, W, heads, join_dw, linear_bwd, mark
+
+# CAPK_ATTN_BIAS=1: the QKV bias gradient fused into the attention backward
+# (capk_attention_bwd_bias).  Default off: the separate column-sum pass runs on the
+# weight-gradient stream under the dX chain, and the fused kernels' extra registers cost more
+# (config-3 train 5240 -> 5122 img/s same box, profiles/round4/README.md)
+_ATTN_BIAS = os.environ.get("CAPK_ATTN_BIAS", "0") == "1"
 
 VIT_ARCHS = {
     # pretrained_model_name -> architecture (weights are random-init offline or loaded from a checkpoint)
@@ -263,10 +270,16 @@ class _ViTLayerFn(torch.autograd.Function):
                                 dsum=G(at.o_proj.bias))
         do = linear_bwd(dx1, o, at.o_proj.weight, None, dt, side_dw=True)
         dqkv = torch.empty_like(qkv)
-        ops.attention_bwd(heads(qkv, 0, B, N), heads(qkv, D, B, N), heads(qkv, 2 * D, B, N), heads(o, 0, B, N),
-                          heads(do, 0, B, N), lse, heads(dqkv, 0, B, N), heads(dqkv, D, B, N),
-                          heads(dqkv, 2 * D, B, N), B, H, N, N, hd, 1.0 / math.sqrt(hd))
-        dh1 = linear_bwd(dqkv, h1, None, None, dt, fused=(at.qkv_w, at.qkv_b), side_dw=True)
+        hv = (heads(qkv, 0, B, N), heads(qkv, D, B, N), heads(qkv, 2 * D, B, N), heads(o, 0, B, N),
+              heads(do, 0, B, N), lse, heads(dqkv, 0, B, N), heads(dqkv, D, B, N), heads(dqkv, 2 * D, B, N),
+              B, H, N, N, hd, 1.0 / math.sqrt(hd))
+        if _ATTN_BIAS:
+            # the QKV bias gradient (column sums of dQ | dK | dV) comes out of the attention backward kernels
+            ops.attention_bwd_bias(*hv, at.qkv_b.grad)
+            dh1 = linear_bwd(dqkv, h1, None, None, dt, fused=(at.qkv_w, None), side_dw=True)
+        else:
+            ops.attention_bwd(*hv)
+            dh1 = linear_bwd(dqkv, h1, None, None, dt, fused=(at.qkv_w, at.qkv_b), side_dw=True)
         prev = getattr(L, "_capk_prev", None)
         dx = ops.layernorm_bwd(dh1, x, ln1.weight.detach(), mu1, rs1, G(ln1.weight), G(ln1.bias), dres=dx1,
                                dsum=G(prev.fc2.bias) if prev is not None else None)

@@ -404,6 +404,22 @@ def attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Nq, Nk, hd, scale, caus
                                    float(drop[0]), int(drop[1]) & 0xFFFFFFFF, _stream()), "capk_attention_bwd")
 
 
+def attention_bwd_bias(q, k, v, o, do, lse, dq, dk, dv, B, H, Nq, Nk, hd, scale, dbias, *, causal=False,
+                       key_pad_u8=None, drop=NO_DROP, accumulate=False):
+    """attention_bwd + the fused QKV bias gradient: dbias [3*H*hd] fp32 (+)= column sums of dQ | dK | dV
+    (capk_attention_bwd_bias)."""
+    _need_gpu(dbias)
+    L = lib()
+    wsb = L.capk_attention_bwd_bias_workspace(B, H, Nq, Nk, hd)
+    ws = _ws(wsb, q.t.device)
+    check(L.capk_attention_bwd_bias(dtype_code(q.t), B, H, Nq, Nk, hd, float(scale), int(causal),
+                                    q.ptr(), q.bs, q.rs, k.ptr(), k.bs, k.rs, v.ptr(), v.bs, v.rs,
+                                    _p(key_pad_u8), o.ptr(), o.bs, o.rs, do.ptr(), do.bs, do.rs, _p(lse),
+                                    dq.ptr(), dq.bs, dq.rs, dk.ptr(), dk.bs, dk.rs, dv.ptr(), dv.bs, dv.rs,
+                                    float(drop[0]), int(drop[1]) & 0xFFFFFFFF, _p(dbias), int(accumulate), _p(ws), wsb,
+                                    _stream()), "capk_attention_bwd_bias")
+
+
 # ------------------------------------------------------ embeddings / misc ---
 def patchify(images, P, out_dtype):
     B, C, H, W = images.shape

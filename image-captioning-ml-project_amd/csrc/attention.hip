@@ -39,7 +39,15 @@ struct AttnArgs {
   // lives in K/V row kv_rows[b * kv_rows_ld + j], the last key (the step's own token) in row b
   const int* kv_rows;
   int64_t kv_rows_ld;
+  // backward, optional (split kernels): per-image column sums of dQ / dK / dV -- the fused QKV
+  // bias gradient of capk_attention_bwd_bias.  Row b of [B][ld]: dQ sums at h*hd + d, dK at
+  // H*hd + h*hd + d, dV at 2*H*hd + h*hd + d (one colsum_finish launch sums the images).
+  // rsum: [B*H][2][Nq] scratch of the dQ kernel (per-query sums over the keys of dS and P).
+  float* dbias_part;
+  int64_t dbias_ld;
+  float* rsum;
 };
+
 // the K / V batch row holding key j of batch row b
 __device__ __forceinline__ int64_t kv_row(const AttnArgs& a, int b, int j) {
   return (a.kv_rows && j < a.Nk - 1) ? (int64_t)a.kv_rows[(int64_t)b * a.kv_rows_ld + j] : (int64_t)b;
@@ -517,7 +525,10 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16(AttnArgs a) {
 // in registers; dQ with K, V staged and the wave's own Q/dO rows in registers.  Same
 // arithmetic as attn_bwd_bf16 phases A and B (which remains for reference shapes that
 // do not fit this split's launch checks).
-template <int HDP, int WPE, int MODE>
+// BIAS: also the per-image column sums of dQ (AttnArgs::dbias_part), as
+// sum_k dQ[k, :] = scale * sum_k (sum_q dS[q, k]) K[k, :]: the per-key sums of the dS this
+// kernel forms anyway go to LDS, then one pass over the head's K rows (L2-resident).
+template <int HDP, int WPE, int MODE, bool BIAS = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void attn_bwd_kv_bf16(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
@@ -569,6 +580,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
     stage_images<HDP, 2, 512, SW>(S, a.hd);
   }
   if (threadIdx.x < NQP) lse_s[threadIdx.x] = lse_r;  // log2 domain
+  float* ksum_s = del_s + NQP;  // BIAS: [NKP] sum_q dS[q, key]
   __syncthreads();
 #pragma unroll
   for (int it = 0; it < DIT; ++it) {
@@ -598,6 +610,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
     f32x4 dvt[HDP / 16], dkt[HDP / 16];
 #pragma unroll
     for (int db = 0; db < HDP / 16; ++db) dvt[db] = dkt[db] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    float dsum = 0.f;  // BIAS: this lane's share of sum_q dS[q, key]
     for (int t = 0; t < NQP / 32; ++t) {
       f32x4 p[2], ds[2];
 #pragma unroll
@@ -619,6 +632,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
           const float mk = dropm<MODE>() && q < a.Nq ? pdrop(a, b, h, q, keyl) : 1.f;
           p[c][r] = pv * mk;
           ds[c][r] = pv * (dp_acc[r] * mk - del_s[q]);
+          if constexpr (BIAS) dsum += ds[c][r];
         }
       }
       const bf16x8 pb = pack8(p[0], p[1]), dsb = pack8(ds[0], ds[1]);
@@ -642,17 +656,45 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
       }
     }
+    if constexpr (BIAS) {  // (keys past Nk: zeros)
+      dsum += __shfl_xor(dsum, 16, 64);
+      dsum += __shfl_xor(dsum, 32, 64);
+      if (lane < 16) ksum_s[keyl] = dsum;
+    }
 #pragma unroll
     for (int s = 0; s < HDP / 32; ++s) {
       kf[s] = kn[s];
       vf[s] = vn[s];
     }
   }
+  if constexpr (BIAS) {  // dQ column sums: G key-strided partials per column, then summed in order
+    __syncthreads();  // ksum_s complete; the Q image is free for the partials
+    constexpr int G = 512 / HDP;
+    float* part = (float*)smem;  // [G][HDP]
+    const int g = threadIdx.x / HDP, d = threadIdx.x % HDP;
+    if (g < G) {
+      float t = 0.f;
+      if (d < a.hd)
+        for (int k = g; k < a.Nk; k += G) t += ksum_s[k] * (float)kbase[(int64_t)k * a.k_rs + d];
+      part[g * HDP + d] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < a.hd) {
+      float t = 0.f;
+#pragma unroll
+      for (int g2 = 0; g2 < G; ++g2) t += part[g2 * HDP + threadIdx.x];
+      a.dbias_part[(int64_t)b * a.dbias_ld + hoff + threadIdx.x] = t * a.scale;
+    }
+  }
 }
 
 // dQ kernel; HDP 64: swizzled 16-row K/V images and <= 80 VGPRs (three workgroups per CU),
 // as the forward kernel.
-template <int HDP, int MODE>
+// BIAS: also the per-image column sums of dK and dV (AttnArgs::dbias_part), as
+// sum_k dK[k, :] = scale * sum_q (sum_k dS[q, k]) Q[q, :] and sum_k dV[k, :] =
+// sum_q (sum_k P~[q, k]) dO[q, :]: per-query sums of the dS / dropped-P rows this kernel forms
+// go to the rsum scratch, then one pass over the head's Q and dO rows (L2-resident).
+template <int HDP, int MODE, bool BIAS = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HDP == 64 ? 6 : 1))) void attn_bwd_q_bf16(
     AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -713,6 +755,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HDP == 64 ?
     f32x4 dqt[HDP / 16];
 #pragma unroll
     for (int db = 0; db < HDP / 16; ++db) dqt[db] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    float dsr = 0.f, pr = 0.f;  // BIAS: this lane's share of sum_k dS[ql, k], sum_k P~[ql, k]
     for (int t = 0; t * 32 < NKP; ++t) {
       f32x4 ds[2];
       const bool hi = (2 * t + 1) * 16 < NKP;  // the chunk's upper 16 keys are staged
@@ -736,6 +779,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HDP == 64 ?
           const float pv = ok ? fexp2(s_acc[r] * sl2 - lq) : 0.f;
           const float mk = dropm<MODE>() && ok ? pdrop(a, b, h, ql, key) : 1.f;
           ds[c][r] = pv * (dp_acc[r] * mk - dd);
+          if constexpr (BIAS) {
+            dsr += ds[c][r];
+            pr += pv * mk;
+          }
         }
       }
       const bf16x8 dsb = pack8(ds[0], ds[1]);
@@ -750,6 +797,43 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HDP == 64 ?
       for (int db = 0; db < HDP / 16; ++db) {
         const int d0 = db * 16 + (lane >> 4) * 4;
         if (d0 < a.hd) store4(dqrow + d0, dqt[db], a.scale);
+      }
+    }
+    if constexpr (BIAS) {
+      dsr += __shfl_xor(dsr, 16, 64);
+      dsr += __shfl_xor(dsr, 32, 64);
+      pr += __shfl_xor(pr, 16, 64);
+      pr += __shfl_xor(pr, 32, 64);
+      float* rs = a.rsum + (int64_t)blockIdx.x * 2 * a.Nq;
+      if (lane < 16 && ql < a.Nq) {
+        rs[ql] = dsr;
+        rs[a.Nq + ql] = pr;
+      }
+    }
+  }
+  if constexpr (BIAS) {  // dK | dV column sums: G query-strided partials per column, then summed in order
+    __syncthreads();  // rsum rows visible to the workgroup; the K / V images are free for the partials
+    constexpr int NC = 2 * HDP, G = 512 / NC;
+    const float* rs = a.rsum + (int64_t)blockIdx.x * 2 * a.Nq;
+    float* part = (float*)smem;  // [G][NC]
+    const int g = threadIdx.x / NC, col = threadIdx.x % NC, kind = col / HDP, d = col % HDP;
+    if (g < G) {
+      float t = 0.f;
+      if (d < a.hd) {
+        const bf16* x = kind ? dobase : qbase;
+        const int64_t xrs = kind ? a.do_rs : a.q_rs;
+        for (int q = g; q < a.Nq; q += G) t += rs[kind * a.Nq + q] * (float)x[(int64_t)q * xrs + d];
+      }
+      part[g * NC + col] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < NC) {
+      const int kd = threadIdx.x / HDP, dd2 = threadIdx.x % HDP;
+      if (dd2 < a.hd) {
+        float t = 0.f;
+#pragma unroll
+        for (int g2 = 0; g2 < G; ++g2) t += part[g2 * NC + threadIdx.x];
+        a.dbias_part[(int64_t)b * a.dbias_ld + (int64_t)(1 + kd) * a.H * a.hd + hoff + dd2] = kd ? t : t * a.scale;
       }
     }
   }
@@ -1785,6 +1869,8 @@ static int check_common(int dtype, int B, int H, int Nq, int Nk, int hd) {
     default: set_error("capk_attention(f32): hd=%d unsupported", a.hd); return CAPK_EUNSUPPORTED;   \
   }
 
+int launch_colsum_finish(int parts, int N, const float* part, float* out, int accumulate, hipStream_t st);  // misc.hip
+
 }  // namespace capk
 
 using namespace capk;
@@ -1938,13 +2024,16 @@ extern "C" int capk_attention_decode_rows(int dtype, int B, int H, int Nq, int N
   }
 }
 
-extern "C" int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int hd, float scale, int causal,
-                                  const void* q, int64_t q_bs, int64_t q_rs, const void* k, int64_t k_bs,
-                                  int64_t k_rs, const void* v, int64_t v_bs, int64_t v_rs, const uint8_t* key_pad,
-                                  const void* o, int64_t o_bs, int64_t o_rs, const void* dout, int64_t do_bs,
-                                  int64_t do_rs, const float* lse, void* dq, int64_t dq_bs, int64_t dq_rs, void* dk,
-                                  int64_t dk_bs, int64_t dk_rs, void* dv, int64_t dv_bs, int64_t dv_rs,
-                                  float drop_p, uint32_t drop_seed, void* stream) {
+// bias_part != nullptr: the split kernels also write per-image dQ / dK / dV column sums
+// ([B][3*H*hd], AttnArgs::dbias_part) and *bias_fused is set; other routes leave it false.
+static int attention_bwd_impl(int dtype, int B, int H, int Nq, int Nk, int hd, float scale, int causal,
+                              const void* q, int64_t q_bs, int64_t q_rs, const void* k, int64_t k_bs,
+                              int64_t k_rs, const void* v, int64_t v_bs, int64_t v_rs, const uint8_t* key_pad,
+                              const void* o, int64_t o_bs, int64_t o_rs, const void* dout, int64_t do_bs,
+                              int64_t do_rs, const float* lse, void* dq, int64_t dq_bs, int64_t dq_rs, void* dk,
+                              int64_t dk_bs, int64_t dk_rs, void* dv, int64_t dv_bs, int64_t dv_rs,
+                              float drop_p, uint32_t drop_seed, void* stream, float* bias_part, bool* bias_fused) {
+  if (bias_fused) *bias_fused = false;
   int rc = check_common(dtype, B, H, Nq, Nk, hd);
   if (rc) return rc;
   AttnArgs a{};
@@ -2029,23 +2118,42 @@ extern "C" int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int h
   }
   {
     // split backward: dK/dV kernel, then dQ kernel (two head images in LDS each)
-    const size_t s1 = bwd_kv_smem(Nq, hdp), s2 = fwd_kernel_smem(Nk, hdp);
+    static const int wpe = [] { const char* e = getenv("CAPK_ATTN_WPE"); return e ? atoi(e) : 4; }();
+    // the bias sums ride on the dK/dV kernel (<= 128-VGPR build only): per-wave rows after the images
+    const bool bias = bias_part && wpe == 4 && hdp <= 128;
+    const size_t s1 = bwd_kv_smem(Nq, hdp) + (bias ? (size_t)((Nk + 31) & ~31) * sizeof(float) : 0);
+    const size_t s2 = fwd_kernel_smem(Nk, hdp);
     // (measured: ViT N=197 bwd 554 -> 460 us; for Nq <= 32 the second launch costs more than it saves)
     if (Nq > 32 && s1 <= 80 * 1024 && s2 <= 80 * 1024) {
-      static const int wpe = [] { const char* e = getenv("CAPK_ATTN_WPE"); return e ? atoi(e) : 4; }();
+      if (bias) {
+        a.dbias_part = bias_part;
+        a.dbias_ld = (int64_t)3 * H * hd;
+        a.rsum = bias_part + (size_t)B * 3 * H * hd;
+        *bias_fused = true;
+      }
 #define KV4(HD, M) rc2 = launch_dyn(attn_bwd_kv_bf16<HD, 4, M>, grid, block, s1, st, a, "attn_bwd_kv_bf16")
+#define KV4B(HD, M) rc2 = launch_dyn(attn_bwd_kv_bf16<HD, 4, M, true>, grid, block, s1, st, a, "attn_bwd_kv_bf16")
 #define KV2(HD, M) rc2 = launch_dyn(attn_bwd_kv_bf16<HD, 2, M>, grid, block, s1, st, a, "attn_bwd_kv_bf16")
 #define QK(HD, M) rc2 = launch_dyn(attn_bwd_q_bf16<HD, M>, grid, block, s2, st, a, "attn_bwd_q_bf16")
+#define QKB(HD, M) rc2 = launch_dyn(attn_bwd_q_bf16<HD, M, true>, grid, block, s2, st, a, "attn_bwd_q_bf16")
 #define KV4M(M) BY_HDP(KV4, M)
+#define KV4BM(M) BY_HDP(KV4B, M)
 #define KV2M(M) BY_HDP(KV2, M)
 #define QKM(M) BY_HDP(QK, M)
-      if (wpe == 4) {  // <= 128 VGPRs: two workgroups per CU
+#define QKBM(M) BY_HDP(QKB, M)
+      if (bias) {
+        BY_MODE(KV4BM)
+      } else if (wpe == 4) {  // <= 128 VGPRs: two workgroups per CU
         BY_MODE(KV4M)
       } else {
         BY_MODE(KV2M)
       }
       if (rc2) return rc2;
-      BY_MODE(QKM)
+      if (bias) {
+        BY_MODE(QKBM)
+      } else {
+        BY_MODE(QKM)
+      }
       return rc2;
     }
   }
@@ -2058,11 +2166,62 @@ extern "C" int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int h
 #undef FB
 #undef FBM
 #undef KV4
+#undef KV4B
 #undef KV2
 #undef QK
+#undef QKB
+#undef QKBM
 #undef KV4M
+#undef KV4BM
 #undef KV2M
 #undef QKM
 #undef BY_HDP
 #undef BY_MODE
+}
+
+
+extern "C" int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int hd, float scale, int causal,
+                                  const void* q, int64_t q_bs, int64_t q_rs, const void* k, int64_t k_bs,
+                                  int64_t k_rs, const void* v, int64_t v_bs, int64_t v_rs, const uint8_t* key_pad,
+                                  const void* o, int64_t o_bs, int64_t o_rs, const void* dout, int64_t do_bs,
+                                  int64_t do_rs, const float* lse, void* dq, int64_t dq_bs, int64_t dq_rs, void* dk,
+                                  int64_t dk_bs, int64_t dk_rs, void* dv, int64_t dv_bs, int64_t dv_rs,
+                                  float drop_p, uint32_t drop_seed, void* stream) {
+  return attention_bwd_impl(dtype, B, H, Nq, Nk, hd, scale, causal, q, q_bs, q_rs, k, k_bs, k_rs, v, v_bs, v_rs,
+                            key_pad, o, o_bs, o_rs, dout, do_bs, do_rs, lse, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv,
+                            dv_bs, dv_rs, drop_p, drop_seed, stream, nullptr, nullptr);
+}
+
+extern "C" size_t capk_attention_bwd_bias_workspace(int B, int H, int Nq, int Nk, int hd) {
+  const int D = H * hd;
+  const size_t fused = ((size_t)B * 3 * D + (size_t)B * H * 2 * Nq) * sizeof(float);
+  const size_t sep = capk_colsum_workspace(B * std::max(Nq, Nk), D);
+  return std::max(fused, sep);
+}
+
+extern "C" int capk_attention_bwd_bias(int dtype, int B, int H, int Nq, int Nk, int hd, float scale, int causal,
+                                       const void* q, int64_t q_bs, int64_t q_rs, const void* k, int64_t k_bs,
+                                       int64_t k_rs, const void* v, int64_t v_bs, int64_t v_rs, const uint8_t* key_pad,
+                                       const void* o, int64_t o_bs, int64_t o_rs, const void* dout, int64_t do_bs,
+                                       int64_t do_rs, const float* lse, void* dq, int64_t dq_bs, int64_t dq_rs,
+                                       void* dk, int64_t dk_bs, int64_t dk_rs, void* dv, int64_t dv_bs,
+                                       int64_t dv_rs, float drop_p, uint32_t drop_seed, float* dbias, int accumulate,
+                                       void* ws, size_t ws_bytes, void* stream) {
+  CAPK_CHECK_ARG(dbias != nullptr, "capk_attention_bwd_bias: dbias is NULL");
+  const int D = H * hd;
+  CAPK_CHECK_ARG(ws && ws_bytes >= capk_attention_bwd_bias_workspace(B, H, Nq, Nk, hd),
+                 "capk_attention_bwd_bias: workspace too small");
+  bool fused = false;
+  int rc = attention_bwd_impl(dtype, B, H, Nq, Nk, hd, scale, causal, q, q_bs, q_rs, k, k_bs, k_rs, v, v_bs, v_rs,
+                              key_pad, o, o_bs, o_rs, dout, do_bs, do_rs, lse, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv,
+                              dv_bs, dv_rs, drop_p, drop_seed, stream, (float*)ws, &fused);
+  if (rc) return rc;
+  if (fused) return launch_colsum_finish(B, 3 * D, (const float*)ws, dbias, accumulate, S(stream));
+  // other routes: column sums of the three gradient views (row-uniform: batch stride = rows * row stride)
+  CAPK_CHECK_ARG(dq_bs == (int64_t)Nq * dq_rs && dk_bs == (int64_t)Nk * dk_rs && dv_bs == (int64_t)Nk * dv_rs,
+                 "capk_attention_bwd_bias: gradient views must be row-uniform ([B*N, ld])");
+  rc = capk_colsum(dtype, B * Nq, D, dq, dq_rs, dbias, accumulate, ws, ws_bytes, stream);
+  if (!rc) rc = capk_colsum(dtype, B * Nk, D, dk, dk_rs, dbias + D, accumulate, ws, ws_bytes, stream);
+  if (!rc) rc = capk_colsum(dtype, B * Nk, D, dv, dv_rs, dbias + 2 * D, accumulate, ws, ws_bytes, stream);
+  return rc;
 }

@@ -153,7 +153,12 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
                                                      int splits, Epi8q e) {
   constexpr int HALF = 128 * 64 * 2, STAGE = 4 * HALF, BIAS0 = 2 * STAGE;
   // two stages + bias slots [item parity][wave] of 64 fp32 (the wave's columns)
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 2 * 8 * 256 + 16];
+#if defined(CAPK_DIAG_TRACE)  // diagnostic build: per-item timestamps of waves 0 and 4 (LDS, then e.sk)
+  constexpr int TR_ITEMS = 64, TR_BYTES = 2 * TR_ITEMS * 4 * 8;
+#else
+  constexpr int TR_BYTES = 0;
+#endif
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 2 * 8 * 256 + 16 + TR_BYTES];
   unsigned* const spt_cnt = (unsigned*)(smem + 2 * STAGE + 2 * 8 * 256);  // SPT: [0] publish, [1] consume
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
@@ -277,6 +282,17 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     fence();
   };
+#if defined(CAPK_DIAG_TRACE)
+  // stamp s (0: item's MFMAs done, 1: epilogue done, 2: next item's first data wait done,
+  // 3: next item's first MFMA phase entered) of item jx, waves 0 and 4 only
+  unsigned long long* const trs = (unsigned long long*)(smem + 2 * STAGE + 2 * 8 * 256 + 16);
+  auto stamp = [&](int jx, int st) {
+    if ((wave & 3) == 0 && lane == 0 && jx < TR_ITEMS)
+      trs[((wave >> 2) * TR_ITEMS + jx) * 4 + st] = __builtin_amdgcn_s_memrealtime();
+  };
+#else
+  auto stamp = [](int, int) {};
+#endif
 
   // ---- epilogue (register-direct); returns the memory instructions it leaves in flight ----
   const int g4 = lane >> 4, qq = ((g4 & 1) << 1) | (g4 >> 1);  // lane's 8-column group after the swap
@@ -592,19 +608,22 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     readB(fb0, u, 2);
     readB(fb1, u, 3);
     const int kend = SPT ? cur.k1 : nk, kbn = SPT ? nxt.k0 : 0;  // this segment's end, the next's start
-    const int e1 = k == (SPT ? cur.k0 : 0) ? S : 0;
+    const int k0c = SPT ? cur.k0 : 0;
+    const int e1 = k == k0c ? S : 0;
     {
       const int n1 = q2prev + e1;  // steady state: 6, +1 with a bias DMA in that phase
       if (n1 == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
       else if (n1 == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       else wait_le(n1);
     }
+    if (k == k0c) stamp(j, 2);
     if (has1) {
       if (k + 1 < kend) load(1, cur, k + 1, u + 1);
       else load(1, nxt, kbn, u + 1);
     }
     lds_done();
     bar();
+    if (k == k0c) stamp(j, 3);
     __builtin_amdgcn_s_setprio(1);
     mma(fa, fb0, acc[0][0]);
     mma(fa, fb1, acc[0][1]);
@@ -637,6 +656,7 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     __builtin_amdgcn_s_setprio(0);
     bar();
     if (++k == kend) {  // the segment's last K-tile: epilogue, stores left in flight
+      stamp(j, 0);
       fence();
       if constexpr (SPT) {
         S = (hasT && j == 0) ? spt_publish() : epilogue(cur, j);  // upper half of the tail item: hand it on
@@ -652,6 +672,7 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
         S = epilogue(cur, j);
         zero_acc();
         fence();
+        stamp(j, 1);
         if (++j == nseg) break;
       }
       cur = nxt;
@@ -660,6 +681,13 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     }
   }
   if (!lag) bar();  // realign the two groups (every barrier is matched)
+#if defined(CAPK_DIAG_TRACE)
+  if ((wave & 3) == 0) {  // this wave's stamps -> e.sk [blockIdx][group][item][4]
+    unsigned long long* dst = (unsigned long long*)e.sk + ((size_t)blockIdx.x * 2 + (wave >> 2)) * TR_ITEMS * 4;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int x = lane; x < TR_ITEMS * 4; x += 64) dst[x] = trs[(wave >> 2) * TR_ITEMS * 4 + x];
+  }
+#endif
 }
 
 }  // namespace
@@ -678,6 +706,15 @@ bool gemm8q_supports(const Epi& e, bool out_f32) {
 }
 
 size_t gemm8q_spt_workspace() { return SPT_WS_BYTES; }
+
+#if defined(CAPK_DIAG_TRACE)
+static size_t diag_trace_bytes() { return (size_t)256 * 2 * 64 * 4 * 8; }
+static void* diag_trace_buf() {
+  static void* buf = nullptr;
+  if (!buf && hipMalloc(&buf, diag_trace_bytes()) != hipSuccess) buf = nullptr;
+  return buf;
+}
+#endif
 
 // The split tail round pays when the last round is at most half full (its leftover items are
 // cut in halves over 2 * rem <= 256 WGs) and the halves are >= 2 K-tiles.  capk_gemm_set_spt /
@@ -746,6 +783,10 @@ int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int
     p.token = next_token();
   }
   CAPK_CHECK_ARG(!fwd_act || (a_kmajor && b_kmajor), "capk_gemm(gemm8q): forward activations need K-major operands");
+#if defined(CAPK_DIAG_TRACE)
+  p.sk = (char*)diag_trace_buf();
+  hipMemsetAsync(p.sk, 0, diag_trace_bytes(), st);
+#endif
   const dim3 grid(256), block(512);
 #define L8(AK, BKM, OT, ACTK, DVK, SKK, DS)                                                                        \
   do {                                                                                                          \
@@ -801,6 +842,16 @@ int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int
 }
 
 }  // namespace capk
+
+#if defined(CAPK_DIAG_TRACE)
+// diagnostic build only: the last gemm8q launch's timestamps (s_memrealtime, 100 MHz) as
+// uint64 [256 WGs][2 wave groups][64 items][4 stamps] (see stamp() in the kernel)
+extern "C" int capk_gemm_diag_trace(void* host_dst, size_t bytes) {
+  void* b = capk::diag_trace_buf();
+  if (!b || bytes < capk::diag_trace_bytes()) return CAPK_EINVAL;
+  return hipMemcpy(host_dst, b, capk::diag_trace_bytes(), hipMemcpyDeviceToHost) == hipSuccess ? CAPK_OK : CAPK_EINVAL;
+}
+#endif
 
 extern "C" int capk_gemm_set_spt(int mode) {
   CAPK_CHECK_ARG(mode >= -1 && mode <= 1, "capk_gemm_set_spt: mode must be -1 (environment), 0 or 1");

@@ -375,6 +375,53 @@ __global__ __launch_bounds__(256) void add_rows_kernel(int G, int rows, int cols
 }
 
 // ------------------------------------------------------------ AdamW --------
+// One pass, ADAM_U float4 groups per thread (all loads issued before the arithmetic), each
+// byte touched once: nontemporal loads / stores keep the 30 B/param stream out of the way
+// of L2 / MALL.  Same per-element arithmetic as adamw_kernel (the grid-stride reference
+// form kept for the tail).
+constexpr int ADAM_U = 4;
+__global__ __launch_bounds__(256) void adamw_u_kernel(int64_t n4, f32x4* __restrict__ p, const f32x4* __restrict__ g,
+                                                      f32x4* __restrict__ m, f32x4* __restrict__ v,
+                                                      bf16x4* __restrict__ pb, float lr, float wd, float b1, float b2,
+                                                      float eps, float bc1, float bc2) {
+  const float step_size = lr / bc1;
+  const float bc2s = sqrtf(bc2);
+  const float decay = 1.f - lr * wd;
+  const int64_t base = (int64_t)blockIdx.x * 256 * ADAM_U + threadIdx.x;
+  f32x4 pv[ADAM_U], gv[ADAM_U], mv[ADAM_U], vv[ADAM_U];
+#pragma unroll
+  for (int u = 0; u < ADAM_U; ++u) {
+    const int64_t i = base + u * 256;
+    if (i < n4) {
+      gv[u] = __builtin_nontemporal_load(g + i);
+      pv[u] = __builtin_nontemporal_load(p + i);
+      mv[u] = __builtin_nontemporal_load(m + i);
+      vv[u] = __builtin_nontemporal_load(v + i);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < ADAM_U; ++u) {
+    const int64_t i = base + u * 256;
+    if (i >= n4) break;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      pv[u][k] *= decay;
+      mv[u][k] = mv[u][k] + (gv[u][k] - mv[u][k]) * (1.f - b1);
+      vv[u][k] = vv[u][k] * b2 + (1.f - b2) * gv[u][k] * gv[u][k];
+      const float denom = sqrtf(vv[u][k]) / bc2s + eps;
+      pv[u][k] = pv[u][k] - step_size * (mv[u][k] / denom);
+    }
+    __builtin_nontemporal_store(pv[u], p + i);
+    __builtin_nontemporal_store(mv[u], m + i);
+    __builtin_nontemporal_store(vv[u], v + i);
+    if (pb) {
+      bf16x4 o;
+      o[0] = (bf16)pv[u][0]; o[1] = (bf16)pv[u][1]; o[2] = (bf16)pv[u][2]; o[3] = (bf16)pv[u][3];
+      __builtin_nontemporal_store(o, pb + i);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void adamw_kernel(int64_t n, float* __restrict__ p, const float* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v,
                                                     bf16* __restrict__ pb, float lr, float wd, float b1, float b2,
@@ -643,6 +690,23 @@ extern "C" int capk_adamw(int64_t n, float* param, const float* grad, float* m, 
                      (uintptr_t)v % 16 == 0 && (uintptr_t)param_bf16 % 8 == 0,
                  "capk_adamw: buffers must be 16-B aligned");
   if (n == 0) return CAPK_OK;
+  static const bool one_pass = [] { const char* e = getenv("CAPK_ADAMW_GRIDSTRIDE"); return !(e && e[0] == '1'); }();
+  const int64_t n4 = n / 4;
+  if (one_pass && n4 > 0) {
+    const int64_t blocks = (n4 + 256 * ADAM_U - 1) / (256 * ADAM_U);
+    CAPK_CHECK_ARG(blocks < (1ll << 31), "capk_adamw: n too large");
+    hipLaunchKernelGGL(adamw_u_kernel, dim3((unsigned)blocks), dim3(256), 0, S(stream), n4, (f32x4*)param,
+                       (const f32x4*)grad, (f32x4*)m, (f32x4*)v, (bf16x4*)param_bf16, lr, weight_decay, beta1, beta2,
+                       eps, bc1, bc2);
+    CAPK_LAUNCH_CHECK("adamw_u_kernel");
+    if (n4 * 4 == n) return CAPK_OK;
+    // the < 4 trailing elements: the reference kernel on the tail
+    const int64_t off = n4 * 4;
+    hipLaunchKernelGGL(adamw_kernel, dim3(1), dim3(64), 0, S(stream), n - off, param + off, grad + off, m + off, v + off,
+                       param_bf16 ? (bf16*)param_bf16 + off : nullptr, lr, weight_decay, beta1, beta2, eps, bc1, bc2);
+    CAPK_LAUNCH_CHECK("adamw_kernel");
+    return CAPK_OK;
+  }
   hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, S(stream), n, param, grad, m, v,
                      (bf16*)param_bf16, lr, weight_decay, beta1, beta2, eps, bc1, bc2);
   CAPK_LAUNCH_CHECK("adamw_kernel");

@@ -183,6 +183,26 @@ int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int hd, float sc
                        void* dk, int64_t dk_bs, int64_t dk_rs,
                        void* dv, int64_t dv_bs, int64_t dv_rs,
                        float drop_p, uint32_t drop_seed, void* stream);
+/* capk_attention_bwd plus the bias gradient of the fused QKV projection that produced q, k, v
+ * (in_proj / c_attn / ViT query,key,value biases: autograd's sum of dQ, dK, dV over the tokens,
+ * modeling_vit.py:205-216 through F.linear): dbias[3*H*hd] fp32 (+)= [colsum dQ | colsum dK |
+ * colsum dV].  The split backward kernels (self-attention, Nq > 32) emit per-image column sums
+ * and one finish pass sums the images in a fixed order; other routes run capk_colsum on the
+ * three gradient views, which must then be row-uniform (batch stride = rows * row stride).
+ * ws: capk_attention_bwd_bias_workspace(B, H, Nq, Nk, hd) bytes. */
+size_t capk_attention_bwd_bias_workspace(int B, int H, int Nq, int Nk, int hd);
+int capk_attention_bwd_bias(int dtype, int B, int H, int Nq, int Nk, int hd, float scale, int causal,
+                            const void* q, int64_t q_bs, int64_t q_rs,
+                            const void* k, int64_t k_bs, int64_t k_rs,
+                            const void* v, int64_t v_bs, int64_t v_rs,
+                            const uint8_t* key_pad,
+                            const void* o, int64_t o_bs, int64_t o_rs,
+                            const void* dout, int64_t do_bs, int64_t do_rs, const float* lse,
+                            void* dq, int64_t dq_bs, int64_t dq_rs,
+                            void* dk, int64_t dk_bs, int64_t dk_rs,
+                            void* dv, int64_t dv_bs, int64_t dv_rs,
+                            float drop_p, uint32_t drop_seed, float* dbias, int accumulate,
+                            void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------- Embedding / patches ----
  * ViT patchify (im2col of Conv2d k=s=P, modeling_vit.py:60-69): images fp32

@@ -243,3 +243,87 @@ def test_transformer_beam5_config3_fp32_vs_oracle():
     assert torch.equal(ids.cpu(), ref["sequences"])
     assert torch.equal(info["beam_indices"].cpu(), ref["beam_indices"])
     torch.testing.assert_close(info["sequences_scores"].cpu(), ref["sequences_scores"], rtol=1e-4, atol=1e-4)
+
+
+@cuda
+def test_transformer_beam5_config3_bf16_vs_fp32():
+    """The benchmarked path end to end: config-3 model (ViT-B/16 + 6L/8H decoder, V = 50257),
+    256 images, bf16 beam-5 through ``generate`` (graph-replayed KV-cached decode), against the
+    fp32 capk search on the same weights (fp32 beam-5 is pinned bit-exactly to the CPU
+    reference by test_transformer_beam5_config3_fp32_vs_oracle).
+
+    The fp32 search is re-run with a step wrapper that feeds the bf16 decoder the same
+    hypotheses, so along the fp32 path every candidate score is known in both precisions
+    (running score + log-prob; the bf16 running scores are summed from the bf16 log-probs of
+    the chosen tokens).  Per image:
+      * stable: at every step the fp32 gap between the k-th and (k+1)-th candidate (every
+        consecutive gap of the top 2k+1 when an EOS or the length limit is in play) exceeds
+        twice the largest bf16-vs-fp32 difference among those candidates, and the final best
+        finished score leads the second by twice the largest difference seen;
+      * exact: at every step the bf16 candidate scores select the same top 2k+1 in the same
+        order as fp32 (the bf16 search then makes the fp32 search's decisions), and the final
+        best-vs-second finished gap exceeds twice the largest difference.
+    Every stable or exact image must give the identical best sequence in bf16; coverage and
+    agreement are printed (random-init weights: nearly flat next-token distributions, the
+    hard case for agreement)."""
+    from capk.beam import beam_search
+    from capk.models.transformer import KVDecodeRunner
+    from test_gpu_model import _full_model
+    m32, _, cfg, _ = _full_model("fp32")
+    m16, _, _, _ = _full_model("bf16")
+    B, k, L = 256, 5, 20
+    V, eos = cfg.model.vocab_size, cfg.model.eos_token_id
+    images = torch.randn(B, 3, 224, 224, generator=torch.Generator().manual_seed(3)).cuda()
+    with torch.no_grad():
+        f32 = m32.encoder(images)["features"]
+        f16 = m16.encoder(images)["features"]
+        ids16, _ = m16.generate(images=images, max_length=L, num_beams=k)
+        r32 = KVDecodeRunner(m32.decoder, f32, k, L)
+        r16 = KVDecodeRunner(m16.decoder, f16, k, L)
+        init = torch.full((B, k), -1e9, device="cuda")
+        init[:, 0] = 0.0
+        st = {"S32": init.clone(), "S16": init.clone(), "err": torch.zeros(B, device="cuda"),
+              "stable": torch.ones(B, dtype=torch.bool, device="cuda"),
+              "exact": torch.ones(B, dtype=torch.bool, device="cuda"), "lp32": None, "lp16": None}
+
+        def step(cur_len, ids, reorder):
+            if reorder is not None:  # running scores of the new rows: parent's score + chosen token's log-prob
+                par = reorder.long()
+                for p in ("32", "16"):
+                    st["S" + p] = (st["S" + p].view(-1)[par] + st["lp" + p][par, ids]).view(B, k)
+            lg32 = r32.step(cur_len, ids, reorder)
+            lg16 = r16.step(cur_len, ids, reorder)
+            st["lp32"] = torch.log_softmax(lg32[:, :V].float(), -1)
+            st["lp16"] = torch.log_softmax(lg16[:, :V].float(), -1)
+            c32 = (st["S32"][:, :, None] + st["lp32"].view(B, k, V)).view(B, k * V)
+            c16 = (st["S16"][:, :, None] + st["lp16"].view(B, k, V)).view(B, k * V)
+            val, idx = c32.topk(2 * k + 1, -1)
+            err = (c16.gather(1, idx) - val).abs().amax(1)
+            st["err"] = torch.maximum(st["err"], err)
+            gaps = val[:, :-1] - val[:, 1:]
+            hit = ((idx % V) == eos).any(1) | (cur_len + 1 >= L)
+            need = torch.where(hit, gaps.amin(1), gaps[:, k - 1])
+            st["stable"] &= need > 2 * err
+            st["exact"] &= (c16.topk(2 * k + 1, -1).indices == idx).all(1)
+            return lg32
+
+        prompt = torch.full((B,), cfg.model.bos_token_id, dtype=torch.long, device="cuda")
+        out = beam_search(step, B, k, L, prompt, eos, pad_token_id=cfg.model.pad_token_id, vocab_size=V)
+    sc = out["all_scores"]
+    final = (sc[:, 0] - sc[:, 1]) > 2 * st["err"]  # the best finished hypothesis keeps its place
+    stable, exact = st["stable"] & final, st["exact"] & final
+    pad = cfg.model.pad_token_id
+
+    def padded(x):
+        y = torch.full((B, L), pad, dtype=torch.long, device="cuda")
+        y[:, :x.shape[1]] = x
+        return y
+
+    same = (padded(out["sequences"]) == padded(ids16)).all(1)
+    print(f"bf16 beam-5 vs fp32 at config-3 size: identical best sequence {float(same.float().mean()):.3f}; "
+          f"stable {int(stable.sum())}/{B} (identical {int((same & stable).sum())}); "
+          f"exact {int(exact.sum())}/{B} (identical {int((same & exact).sum())}); "
+          f"median max candidate error {float(st['err'].median()):.2e}")
+    assert int(exact.sum()) > 0
+    assert bool(same[stable].all()), torch.nonzero(stable & ~same).flatten().tolist()
+    assert bool(same[exact].all()), torch.nonzero(exact & ~same).flatten().tolist()

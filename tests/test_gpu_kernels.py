@@ -556,3 +556,65 @@ def test_short_attention_train(ops, case):
     assert _rel(dq.float().view(B, Nq, H, hd).transpose(1, 2), qr.grad) < 3e-2
     assert _rel(dkv[:, :D].float().reshape(B, Nk, H, hd).transpose(1, 2), kr.grad) < 3e-2
     assert _rel(dkv[:, D:].float().reshape(B, Nk, H, hd).transpose(1, 2), vr.grad) < 3e-2
+
+
+@cuda
+@pytest.mark.parametrize("case", ["vit", "mask_drop", "hd128", "short", "fp32"])
+def test_attention_bwd_qkv_bias(ops, case):
+    """capk_attention_bwd_bias: the backward plus the fused QKV bias gradient dbias = [colsum dQ |
+    colsum dK | colsum dV] over the B*N tokens (the ViT query / key / value bias gradients,
+    modeling_vit.py:205-216).  ViT self-attention (N = 197, hd 64) rides on the split kernels
+    (dQ sums from sum_q dS x K in the dK/dV kernel, dK / dV sums from per-query dS / P~ sums x Q /
+    dO in the dQ kernel); key padding + dropout, hd 128, and the short / fp32 routes (separate
+    column sums) are checked against the fp32 autograd reference and against the column sums of
+    the kernel's own gradients; accumulate adds."""
+    from capk.ops import HeadView
+    g = torch.Generator(device="cuda").manual_seed(31)
+    p, seed, key_pad, dt = 0.0, 0, None, torch.bfloat16
+    if case == "vit":
+        B, H, N, hd = 8, 12, 197, 64
+    elif case == "mask_drop":
+        B, H, N, hd = 5, 6, 150, 64
+        p, seed = 0.1, 99
+        key_pad = torch.zeros(B, N, dtype=torch.bool, device="cuda")
+        key_pad[2, 120:] = True
+        key_pad[4, 3] = True
+    elif case == "hd128":
+        B, H, N, hd = 4, 4, 100, 128
+    elif case == "short":
+        B, H, N, hd = 16, 8, 20, 96
+    else:
+        B, H, N, hd, dt = 3, 4, 77, 32, torch.float32
+    D = H * hd
+    qkv = torch.randn(B * N, 3 * D, device="cuda", generator=g).to(dt)
+    do = torch.randn(B * N, D, device="cuda", generator=g).to(dt)
+    o = torch.empty(B * N, D, device="cuda", dtype=dt)
+    hv = lambda t, off, ld: HeadView(t, off, N * ld, ld)
+    Q, K_, V_, O = hv(qkv, 0, 3 * D), hv(qkv, D, 3 * D), hv(qkv, 2 * D, 3 * D), hv(o, 0, D)
+    sc = 1.0 / math.sqrt(hd)
+    lse, kp = ops.attention_fwd(Q, K_, V_, O, B, H, N, N, hd, sc, key_pad=key_pad, drop=(p, seed))
+    x = qkv.float().view(B, N, 3, H, hd)
+    qr, kr, vr = (x[:, :, i].transpose(1, 2).contiguous().requires_grad_(True) for i in range(3))
+    s = torch.einsum("bhqd,bhkd->bhqk", qr, kr) * sc
+    if key_pad is not None:
+        s = s.masked_fill(key_pad[:, None, None, :], float("-inf"))
+    a = torch.softmax(s, -1)
+    if p > 0:
+        a = a * (ops.dropout_mask(B * H * N * N, p, seed).view(B, H, N, N).float() / (1 - p))
+    torch.einsum("bhqk,bhkd->bhqd", a, vr).backward(do.float().view(B, N, H, hd).transpose(1, 2))
+    ref = torch.cat([t.grad.sum((0, 2)).reshape(-1) for t in (qr, kr, vr)])  # [h, d] order = column h*hd + d
+    dqkv = torch.empty_like(qkv)
+    dbias = torch.full((3 * D,), 5.0, device="cuda")
+    ops.attention_bwd_bias(Q, K_, V_, O, hv(do, 0, D), lse, hv(dqkv, 0, 3 * D), hv(dqkv, D, 3 * D),
+                           hv(dqkv, 2 * D, 3 * D), B, H, N, N, hd, sc, dbias, key_pad_u8=kp, drop=(p, seed))
+    tol = 1e-4 if dt == torch.float32 else 2e-2
+    scale_ref = ref.abs().max()
+    assert _rel(dbias, ref) < tol, _rel(dbias, ref)
+    assert float((dbias[D:2 * D] - ref[D:2 * D]).abs().max()) < tol * float(scale_ref)  # analytically ~0
+    own = dqkv.float().sum(0)  # column sums of the kernel's own (rounded) gradients
+    assert _rel(dbias, own) < (1e-5 if dt == torch.float32 else 1e-2), _rel(dbias, own)
+    acc = torch.full((3 * D,), 5.0, device="cuda")
+    ops.attention_bwd_bias(Q, K_, V_, O, hv(do, 0, D), lse, hv(dqkv, 0, 3 * D), hv(dqkv, D, 3 * D),
+                           hv(dqkv, 2 * D, 3 * D), B, H, N, N, hd, sc, acc, key_pad_u8=kp, drop=(p, seed),
+                           accumulate=True)
+    torch.testing.assert_close(acc, dbias + 5.0, rtol=0, atol=1e-4 * float(scale_ref) + 1e-5)
