@@ -46,6 +46,7 @@ struct AttnArgs {
   float* dbias_part;
   int64_t dbias_ld;
   float* rsum;
+  int b_base;  // batch index of this launch's first image (a batch slice): dropout mask index
 };
 
 // the K / V batch row holding key j of batch row b
@@ -53,7 +54,7 @@ __device__ __forceinline__ int64_t kv_row(const AttnArgs& a, int b, int j) {
   return (a.kv_rows && j < a.Nk - 1) ? (int64_t)a.kv_rows[(int64_t)b * a.kv_rows_ld + j] : (int64_t)b;
 }
 __device__ __forceinline__ float pdrop(const AttnArgs& a, int b, int h, int q, int key) {
-  return a.drop.mul((((uint64_t)b * a.H + h) * a.Nq + q) * a.Nk + key);
+  return a.drop.mul((((uint64_t)(b + a.b_base) * a.H + h) * a.Nq + q) * a.Nk + key);
 }
 
 __device__ __forceinline__ bool key_ok(const AttnArgs& a, int b, int key, int q) {
@@ -602,6 +603,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
     if ((idx & 7) == 0 && q < NQP) del_s[q] = s;
   }
   __syncthreads();
+  // delta for the dQ kernel, which then needs no O: stashed as fp32 in the first 4 bytes of
+  // each (image, query, head) slot of dQ, which that kernel reads before overwriting it
+  for (int q = threadIdx.x; q < a.Nq; q += blockDim.x)
+    *(float*)((bf16*)a.dq + (int64_t)b * a.dq_bs + (int64_t)q * a.dq_rs + hoff) = del_s[q];
   const float sl2 = a.scale * kLog2e;
   for (int kb = wave; kb < NKP / 16; kb += nwaves) {
     const int keyl = kb * 16 + (lane & 15);
@@ -708,10 +713,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HDP == 64 ?
   const int hoff = h * a.hd;
   const bf16* qbase = (const bf16*)a.q + (int64_t)b * a.q_bs + hoff;
   const bf16* dobase = (const bf16*)a.dout + (int64_t)b * a.do_bs + hoff;
-  const bf16* obase = (const bf16*)a.o + (int64_t)b * a.o_bs + hoff;
-  // the wave's query block operands: Q, dO, O rows (fragment layout) and lse
-  bf16x8 qf[HDP / 32], dof[HDP / 32], of[HDP / 32];
-  float lq = 0.f;
+  const bf16* dqbase = (const bf16*)a.dq + (int64_t)b * a.dq_bs + hoff;
+  // the wave's query block operands: Q, dO rows (fragment layout), lse and delta_q =
+  // sum_d dO * O (from the dK/dV kernel, stashed in this query's dQ slot)
+  bf16x8 qf[HDP / 32], dof[HDP / 32];
+  float lq = 0.f, dd = 0.f;
   auto load_q = [&](int qb) {
     const int ql = qb * 16 + (lane & 15);
 #pragma unroll
@@ -722,17 +728,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HDP == 64 ?
       dof[s] = in ? ld8(dobase + (int64_t)ql * a.do_rs + d) : zero8();
     }
     lq = ql < a.Nq ? a.lse_in[((int64_t)b * a.H + h) * a.Nq + ql] * kLog2e : 0.f;
+    dd = ql < a.Nq ? *(const float*)(dqbase + (int64_t)ql * a.dq_rs) : 0.f;
   };
-  auto load_o = [&](int qb) {
-    const int ql = qb * 16 + (lane & 15);
-#pragma unroll
-    for (int s = 0; s < HDP / 32; ++s) {
-      const int d = s * 32 + 8 * (lane >> 4);
-      of[s] = ql < a.Nq && d < a.hd ? ld8(obase + (int64_t)ql * a.o_rs + d) : zero8();
-    }
-  };
-  // the first block's Q / dO / lse are requested before the K / V staging (O after it:
-  // holding O across the staging loads spills at the 80-VGPR budget of three WGs per CU)
+  // the first block's Q / dO / lse / delta are requested before the K / V staging
   if (wave < NQP / 16) load_q(wave);
   {
     const StageSrc S[2] = {{Ks, (const bf16*)a.k + (int64_t)b * a.k_bs + hoff, a.k_rs, a.Nk, NKP},
@@ -744,14 +742,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HDP == 64 ?
   for (int qb = wave; qb < NQP / 16; qb += nwaves) {
     const int ql = qb * 16 + (lane & 15);
     if (qb != wave) load_q(qb);
-    load_o(qb);
-    float dd = 0.f;  // delta_q = sum_d dO * O, this lane's 8-dim chunks, then over the lane group
-#pragma unroll
-    for (int s = 0; s < HDP / 32; ++s)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) dd += (float)of[s][i] * (float)dof[s][i];
-    dd += __shfl_xor(dd, 16, 64);
-    dd += __shfl_xor(dd, 32, 64);
     f32x4 dqt[HDP / 16];
 #pragma unroll
     for (int db = 0; db < HDP / 16; ++db) dqt[db] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -2024,6 +2014,8 @@ extern "C" int capk_attention_decode_rows(int dtype, int B, int H, int Nq, int N
   }
 }
 
+static int g_bwd_slice = -1;  // capk_attention_set_bwd_slice (-1: CAPK_ATTN_BWD_SLICE)
+
 // bias_part != nullptr: the split kernels also write per-image dQ / dK / dV column sums
 // ([B][3*H*hd], AttnArgs::dbias_part) and *bias_fused is set; other routes leave it false.
 static int attention_bwd_impl(int dtype, int B, int H, int Nq, int Nk, int hd, float scale, int causal,
@@ -2141,18 +2133,47 @@ static int attention_bwd_impl(int dtype, int B, int H, int Nq, int Nk, int hd, f
 #define KV2M(M) BY_HDP(KV2, M)
 #define QKM(M) BY_HDP(QK, M)
 #define QKBM(M) BY_HDP(QKB, M)
-      if (bias) {
-        BY_MODE(KV4BM)
-      } else if (wpe == 4) {  // <= 128 VGPRs: two workgroups per CU
-        BY_MODE(KV4M)
-      } else {
-        BY_MODE(KV2M)
-      }
-      if (rc2) return rc2;
-      if (bias) {
-        BY_MODE(QKBM)
-      } else {
-        BY_MODE(QKM)
+      // CAPK_ATTN_BWD_SLICE=n: the two kernels alternate over slices of n images, so the dQ
+      // kernel re-reads a slice's Q / K / V / O / dO while the Infinity Cache still holds them
+      static const int env_slice = [] { const char* e = getenv("CAPK_ATTN_BWD_SLICE"); return e ? atoi(e) : 0; }();
+      const int slice = g_bwd_slice >= 0 ? g_bwd_slice : env_slice;
+      const int sl = slice > 0 && slice < B ? slice : B;
+      const size_t es = 2;  // bf16
+      const AttnArgs base = a;
+      for (int b0 = 0; b0 < B; b0 += sl) {
+        const int nb = std::min(sl, B - b0);
+        AttnArgs a = base;
+        const dim3 grid(nb * H);
+        a.B = nb;
+        a.b_base = b0;
+        a.q = (const char*)base.q + (size_t)b0 * q_bs * es;
+        a.k = (const char*)base.k + (size_t)b0 * k_bs * es;
+        a.v = (const char*)base.v + (size_t)b0 * v_bs * es;
+        a.o = (const char*)base.o + (size_t)b0 * o_bs * es;
+        a.dout = (const char*)base.dout + (size_t)b0 * do_bs * es;
+        a.dq = (char*)base.dq + (size_t)b0 * dq_bs * es;
+        a.dk = (char*)base.dk + (size_t)b0 * dk_bs * es;
+        a.dv = (char*)base.dv + (size_t)b0 * dv_bs * es;
+        a.lse_in = base.lse_in + (size_t)b0 * H * Nq;
+        if (base.key_pad) a.key_pad = base.key_pad + (size_t)b0 * Nk;
+        if (bias) {
+          a.dbias_part = base.dbias_part + (size_t)b0 * base.dbias_ld;
+          a.rsum = base.rsum + (size_t)b0 * H * 2 * Nq;
+        }
+        if (bias) {
+          BY_MODE(KV4BM)
+        } else if (wpe == 4) {  // <= 128 VGPRs: two workgroups per CU
+          BY_MODE(KV4M)
+        } else {
+          BY_MODE(KV2M)
+        }
+        if (rc2) return rc2;
+        if (bias) {
+          BY_MODE(QKBM)
+        } else {
+          BY_MODE(QKM)
+        }
+        if (rc2) return rc2;
       }
       return rc2;
     }
@@ -2190,6 +2211,12 @@ extern "C" int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int h
   return attention_bwd_impl(dtype, B, H, Nq, Nk, hd, scale, causal, q, q_bs, q_rs, k, k_bs, k_rs, v, v_bs, v_rs,
                             key_pad, o, o_bs, o_rs, dout, do_bs, do_rs, lse, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv,
                             dv_bs, dv_rs, drop_p, drop_seed, stream, nullptr, nullptr);
+}
+
+extern "C" int capk_attention_set_bwd_slice(int images) {
+  CAPK_CHECK_ARG(images >= -1, "capk_attention_set_bwd_slice: images must be >= -1");
+  g_bwd_slice = images;
+  return CAPK_OK;
 }
 
 extern "C" size_t capk_attention_bwd_bias_workspace(int B, int H, int Nq, int Nk, int hd) {

@@ -122,6 +122,7 @@ struct Epi8q {
   float* dsum;  // DSUM kernels: column-sum partials [2 * tile rows][N]
   char* sk;     // split-tail hand-off workspace (SPT kernels)
   unsigned long long token;  // this launch's hand-off token (nonzero, unique per host launch)
+  unsigned long long* trace;  // CAPK_DIAG_TRACE builds only: per-item timestamps (never the SPT workspace)
 };
 
 // split-tail workspace: 128 pair slots x 8 waves x 32 KiB of fp32 accumulators, then flag words
@@ -153,7 +154,7 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
                                                      int splits, Epi8q e) {
   constexpr int HALF = 128 * 64 * 2, STAGE = 4 * HALF, BIAS0 = 2 * STAGE;
   // two stages + bias slots [item parity][wave] of 64 fp32 (the wave's columns)
-#if defined(CAPK_DIAG_TRACE)  // diagnostic build: per-item timestamps of waves 0 and 4 (LDS, then e.sk)
+#if defined(CAPK_DIAG_TRACE)  // diagnostic build: per-item timestamps of waves 0 and 4 (LDS, then e.trace)
   constexpr int TR_ITEMS = 64, TR_BYTES = 2 * TR_ITEMS * 4 * 8;
 #else
   constexpr int TR_BYTES = 0;
@@ -682,8 +683,8 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
   }
   if (!lag) bar();  // realign the two groups (every barrier is matched)
 #if defined(CAPK_DIAG_TRACE)
-  if ((wave & 3) == 0) {  // this wave's stamps -> e.sk [blockIdx][group][item][4]
-    unsigned long long* dst = (unsigned long long*)e.sk + ((size_t)blockIdx.x * 2 + (wave >> 2)) * TR_ITEMS * 4;
+  if ((wave & 3) == 0 && e.trace) {  // this wave's stamps -> e.trace [blockIdx][group][item][4]
+    unsigned long long* dst = e.trace + ((size_t)blockIdx.x * 2 + (wave >> 2)) * TR_ITEMS * 4;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     for (int x = lane; x < TR_ITEMS * 4; x += 64) dst[x] = trs[(wave >> 2) * TR_ITEMS * 4 + x];
   }
@@ -784,8 +785,9 @@ int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int
   }
   CAPK_CHECK_ARG(!fwd_act || (a_kmajor && b_kmajor), "capk_gemm(gemm8q): forward activations need K-major operands");
 #if defined(CAPK_DIAG_TRACE)
-  p.sk = (char*)diag_trace_buf();
-  hipMemsetAsync(p.sk, 0, diag_trace_bytes(), st);
+  p.trace = (unsigned long long*)diag_trace_buf();
+  CAPK_CHECK_ARG(p.trace != nullptr, "capk_gemm(gemm8q, trace build): no trace buffer");
+  hipMemsetAsync(p.trace, 0, diag_trace_bytes(), st);
 #endif
   const dim3 grid(256), block(512);
 #define L8(AK, BKM, OT, ACTK, DVK, SKK, DS)                                                                        \

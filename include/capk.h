@@ -183,6 +183,11 @@ int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int hd, float sc
                        void* dk, int64_t dk_bs, int64_t dk_rs,
                        void* dv, int64_t dv_bs, int64_t dv_rs,
                        float drop_p, uint32_t drop_seed, void* stream);
+/* The self-attention split backward (Nq > 32) alternates its dK/dV and dQ kernels over
+ * slices of `images` batch entries (0 = one launch each over the whole batch; -1 = the
+ * CAPK_ATTN_BWD_SLICE environment value), so the dQ kernel re-reads a slice's operands while
+ * they are still in the Infinity Cache.  Results are identical for every slice size. */
+int capk_attention_set_bwd_slice(int images);
 /* capk_attention_bwd plus the bias gradient of the fused QKV projection that produced q, k, v
  * (in_proj / c_attn / ViT query,key,value biases: autograd's sum of dQ, dK, dV over the tokens,
  * modeling_vit.py:205-216 through F.linear): dbias[3*H*hd] fp32 (+)= [colsum dQ | colsum dK |

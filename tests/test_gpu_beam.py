@@ -260,9 +260,10 @@ def test_transformer_beam5_config3_bf16_vs_fp32():
         consecutive gap of the top 2k+1 when an EOS or the length limit is in play) exceeds
         twice the largest bf16-vs-fp32 difference among those candidates, and the final best
         finished score leads the second by twice the largest difference seen;
-      * exact: at every step the bf16 candidate scores select the same top 2k+1 in the same
-        order as fp32 (the bf16 search then makes the fp32 search's decisions), and the final
-        best-vs-second finished gap exceeds twice the largest difference.
+      * exact: at every step the bf16 candidate scores select the same k best candidates (as a
+        set) with no EOS among the 2k+1 best of either precision before the last step, so the
+        bf16 search keeps the fp32 search's hypotheses, and the final best-vs-second finished
+        gap exceeds twice the largest difference.
     Every stable or exact image must give the identical best sequence in bf16; coverage and
     agreement are printed (random-init weights: nearly flat next-token distributions, the
     hard case for agreement)."""
@@ -304,7 +305,14 @@ def test_transformer_beam5_config3_bf16_vs_fp32():
             hit = ((idx % V) == eos).any(1) | (cur_len + 1 >= L)
             need = torch.where(hit, gaps.amin(1), gaps[:, k - 1])
             st["stable"] &= need > 2 * err
-            st["exact"] &= (c16.topk(2 * k + 1, -1).indices == idx).all(1)
+            # the bf16 scores keep the running set: the same k best candidates (as a set; their
+            # slot order only permutes the beams), and no EOS / length hit among the 2k + 1 best
+            # of either precision, except at the last step, where every candidate finishes
+            i16 = c16.topk(2 * k + 1, -1).indices
+            same_k = (i16[:, :k].sort(1).values == idx[:, :k].sort(1).values).all(1)
+            last = cur_len + 1 >= L
+            no_hit = ~((idx % V) == eos).any(1) & ~((i16 % V) == eos).any(1)
+            st["exact"] &= same_k & (no_hit | last)
             return lg32
 
         prompt = torch.full((B,), cfg.model.bos_token_id, dtype=torch.long, device="cuda")

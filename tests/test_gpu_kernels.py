@@ -618,3 +618,39 @@ def test_attention_bwd_qkv_bias(ops, case):
                            hv(dqkv, 2 * D, 3 * D), B, H, N, N, hd, sc, acc, key_pad_u8=kp, drop=(p, seed),
                            accumulate=True)
     torch.testing.assert_close(acc, dbias + 5.0, rtol=0, atol=1e-4 * float(scale_ref) + 1e-5)
+
+
+@cuda
+def test_attention_bwd_batch_slices_identical(ops):
+    """capk_attention_set_bwd_slice: the split backward alternating its dK/dV and dQ kernels over
+    batch slices (the dropout mask index carries the slice's first image) gives bit-identical
+    dQ / dK / dV to one launch pair over the whole batch -- ViT shape with a key-padding mask
+    and probability dropout, slices that do and do not divide the batch."""
+    from capk.ops import HeadView
+    L = ops.lib()
+    g = torch.Generator(device="cuda").manual_seed(41)
+    B, H, N, hd, p, seed = 7, 4, 197, 64, 0.1, 1234
+    D = H * hd
+    qkv = torch.randn(B * N, 3 * D, device="cuda", generator=g).bfloat16()
+    do = torch.randn(B * N, D, device="cuda", generator=g).bfloat16()
+    o = torch.empty(B * N, D, device="cuda", dtype=torch.bfloat16)
+    key_pad = torch.zeros(B, N, dtype=torch.bool, device="cuda")
+    key_pad[3, 150:] = True
+    hv = lambda t, off, ld: HeadView(t, off, N * ld, ld)
+    sc = 1.0 / math.sqrt(hd)
+    lse, kp = ops.attention_fwd(hv(qkv, 0, 3 * D), hv(qkv, D, 3 * D), hv(qkv, 2 * D, 3 * D), hv(o, 0, D), B, H, N, N,
+                                hd, sc, key_pad=key_pad, drop=(p, seed))
+    outs = []
+    try:
+        for sl in (0, 2, 3, 7):
+            ops.check(L.capk_attention_set_bwd_slice(sl), "set_bwd_slice")
+            d = torch.full_like(qkv, float("nan"))
+            ops.attention_bwd(hv(qkv, 0, 3 * D), hv(qkv, D, 3 * D), hv(qkv, 2 * D, 3 * D), hv(o, 0, D), hv(do, 0, D),
+                              lse, hv(d, 0, 3 * D), hv(d, D, 3 * D), hv(d, 2 * D, 3 * D), B, H, N, N, hd, sc,
+                              key_pad_u8=kp, drop=(p, seed))
+            outs.append(d)
+    finally:
+        L.capk_attention_set_bwd_slice(-1)
+    assert bool(torch.isfinite(outs[0].float()).all())
+    for d in outs[1:]:
+        assert torch.equal(d, outs[0])
