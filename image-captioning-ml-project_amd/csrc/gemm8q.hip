@@ -291,6 +291,8 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     if ((wave & 3) == 0 && lane == 0 && jx < TR_ITEMS)
       trs[((wave >> 2) * TR_ITEMS + jx) * 4 + st] = __builtin_amdgcn_s_memrealtime();
   };
+  if ((wave & 3) == 0)  // unstamped entries read as 0 (the same wave copies them out at the end)
+    for (int x = lane; x < TR_ITEMS * 4; x += 64) trs[(wave >> 2) * TR_ITEMS * 4 + x] = 0ull;
 #else
   auto stamp = [](int, int) {};
 #endif
