@@ -396,7 +396,7 @@ extern "C" size_t capk_gemm_workspace(int in_dtype, int out_dtype, int M, int N,
   for (int c = 1; c <= 6; ++c) s = std::max(s, choose_splits(c, M, N, K));
   const size_t slab = s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
   // persistent grids: the split-tail hand-off area (gemm8q.hip)
-  return tiles_of(6, M, N) > 256 ? std::max(slab, gemm8q_spt_workspace()) : slab;
+  return tiles_of(6, M, N) > 256 ? std::max(slab, gemm8q_tail_workspace(M, N, K)) : slab;
 }
 
 extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const void* A, int64_t lda,
@@ -474,10 +474,23 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
   else if (b_kmajor) LAUNCH(false, true, OT);           \
   else LAUNCH(false, false, OT);
   if (cfg == 6) {
-    void* spt = (!slab && ws && ws_bytes >= gemm8q_spt_workspace()) ? ws : nullptr;
+    int tail_r0 = -1, tail_splits = 1;
     const int rc = launch_gemm8q(a_kmajor, b_kmajor, out_dtype == CAPK_F32, A, lda, B, ldb, M, N, K, splits, e, slab,
-                                 st, nullptr, spt);
+                                 st, nullptr, slab ? nullptr : ws, slab ? 0 : ws_bytes, &tail_r0, &tail_splits);
     if (rc != CAPK_OK) return rc;
+    if (tail_r0 >= 0) {  // the split-K tail round's slabs -> rows [256 r0, M) with the epilogue
+      const int64_t r = (int64_t)tail_r0 * 256;
+      Epi et = e;
+      et.M = M - (int)r;
+      et.C = (char*)e.C + r * e.ldc * 2;  // (bf16 outputs only)
+      if (e.res) et.res = (const char*)e.res + r * e.ldr * 2;
+      if (e.aux) et.aux = (const char*)e.aux + r * e.ldx * 2;
+      if (e.pre) et.pre = (char*)e.pre + r * e.ldx * 2;
+      const int64_t n8 = (int64_t)et.M * N / 8;
+      const int g = (int)std::min<int64_t>(2048, (n8 + 255) / 256);
+      hipLaunchKernelGGL(splitk_reduce_kernel<bf16>, dim3(g), dim3(256), 0, st, (const float*)ws, tail_splits, et);
+      CAPK_LAUNCH_CHECK("splitk_reduce_kernel");
+    }
   } else if (cfg == 5) {
     // Activation products on the 256x256 kernel: plain product (+ bias) into the kept
     // pre-activation / C, then one elementwise pass (act_pass_kernel) -- measured faster than
@@ -559,7 +572,8 @@ extern "C" int capk_gemm_dx_act_colsum(int M, int N, int K, const void* dY, int6
                      tiles_of(6, M, N) > 256 && gemm8q_supports(e, false) && K >= 128;
   if (fused) {
     g_last_cfg = 6;
-    const int rc = launch_gemm8q(true, false, false, dY, ldy, W, ldw, M, N, K, 1, e, nullptr, S(stream), (float*)ws);
+    const int rc = launch_gemm8q(true, false, false, dY, ldy, W, ldw, M, N, K, 1, e, nullptr, S(stream), (float*)ws,
+                                 nullptr, 0, nullptr, nullptr);
     if (rc != CAPK_OK) return rc;
     return launch_colsum_finish(cdiv(M, 256) * 2, N, (const float*)ws, db, accumulate, S(stream));
   }

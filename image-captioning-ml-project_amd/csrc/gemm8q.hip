@@ -29,19 +29,17 @@
 //    where the phase issued a bias DMA).  Too small a count is safe (it only waits longer),
 //    so the run-time counts are rounded down to the encodings wait_le() has.
 //
-//  * Split tail round (round 4, SPT: grids whose last round is at most half full, e.g. the
-//    591 items = 2.31 rounds of a 50 432 x 768 product): after the R whole rounds, the rem
-//    leftover items are cut in two K halves run by a pair of WGs (virtual indices r and
-//    rem + r): WG r runs item r's upper K half FIRST (before its whole items) and hands its
-//    fp32 accumulators on (sc1 stores, each wave drained, then the last wave stores a
-//    per-launch token in the pair's flag word); WG rem + r runs the lower half LAST,
-//    starting from those accumulators (every wave polls the flag and loads its part with sc1
-//    loads straight into the zeroed accumulator registers), and writes the item.  The busiest WGs then run R + 1/2 items instead of R + 1.  The waiting side only
-//    waits for a WG whose first action is the hand-off, and WGs without a lower half never
-//    wait, so a launch cannot deadlock on WGs that are not yet resident; the split point is
-//    a function of K only (deterministic).  Contiguous-range stream-K over all items was
-//    measured slower (profiles/round4/streamk_contiguous_ab.txt: concurrent WGs no longer
-//    shared A row blocks in L2).
+//  * Split-K tail round (round 4, TAIL: grids whose last round is partly empty, e.g. the
+//    591 items = 2.31 rounds of a 50 432 x 768 product, when K is long enough): only the
+//    row blocks [0, r0) run as whole items (r0 * ntn <= 256 * rounds), and the remaining
+//    row blocks run as S K-splits per tile in one extra round (T * S <= 256 parts), each
+//    part writing its fp32 accumulators to its own slab; the host then launches the split-K
+//    reduce + epilogue over those rows (gemm.hip: splitk_reduce_kernel).  No cross-WG
+//    hand-off: the kernel boundary orders the slabs (the round-4 alternative that handed
+//    accumulators between WGs through an sc1 workspace paid more for the payload round trip
+//    than it saved, profiles/round4/ab_round4.md).  Contiguous-range stream-K was measured
+//    slower (profiles/round4/streamk_contiguous_ab.txt: concurrent WGs no longer shared A
+//    row blocks in L2).
 //
 // Epilogue (compile-time forms, gemm8q_supports): bias, a forward GELU-family / ReLU
 // activation with act'(pre) (DV) or pre kept, OR one side operand -- the backward multiply by
@@ -120,16 +118,11 @@ struct Epi8q {
   int64_t ldc, lds, ldp;
   float beta;
   float* dsum;  // DSUM kernels: column-sum partials [2 * tile rows][N]
-  char* sk;     // split-tail hand-off workspace (SPT kernels)
-  unsigned long long token;  // this launch's hand-off token (nonzero, unique per host launch)
-  unsigned long long* trace;  // CAPK_DIAG_TRACE builds only: per-item timestamps (never the SPT workspace)
+  float* tail_ws;  // TAIL kernels: fp32 slabs [splits][M - 256 tail_r0][N] of the tail row blocks
+  int tail_r0, tail_splits;
+  unsigned long long* trace;  // CAPK_DIAG_TRACE builds only: per-item timestamps
 };
 
-// split-tail workspace: 128 pair slots x 8 waves x 32 KiB of fp32 accumulators, then flag words
-// (one per slot used; 8 per slot reserved)
-constexpr size_t SPT_PART_BYTES = (size_t)128 * 8 * 32768;
-constexpr size_t SPT_WS_BYTES = SPT_PART_BYTES + (size_t)128 * 8 * 8;
-constexpr int SC1 = 16;  // buffer cache-policy bit (gfx950 sc1): write through / read past L1
 
 // s_waitcnt vmcnt(<= n) for a wave-uniform run-time n: the largest encoded count <= n
 __device__ __forceinline__ void wait_le(int n) {
@@ -148,7 +141,7 @@ __device__ __forceinline__ void wait_le(int n) {
 // DSUM: also the column sums of the final values (the bias gradient of the Linear whose
 // output gradient this dX is): per (tile row, wm) partial rows [2 ntm][N] into e.dsum,
 // summed in a fixed order by colsum_finish (capk_gemm_dx_act_colsum).
-template <bool AK, bool BK, typename OutT, int ACT, bool DV, int SK, bool DSUM = false, bool SPT = false>
+template <bool AK, bool BK, typename OutT, int ACT, bool DV, int SK, bool DSUM = false, bool TAIL = false>
 __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A, int64_t lda,
                                                      const void* __restrict__ B, int64_t ldb, int M, int N, int K,
                                                      int splits, Epi8q e) {
@@ -160,26 +153,23 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
   constexpr int TR_BYTES = 0;
 #endif
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 2 * 8 * 256 + 16 + TR_BYTES];
-  unsigned* const spt_cnt = (unsigned*)(smem + 2 * STAGE + 2 * 8 * 256);  // SPT: [0] publish, [1] consume
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   const bool lag = wave >= 4;  // waves 4-7 run one barrier behind
   const int ntn = (N + 255) / 256, ntiles = ((M + 255) / 256) * ntn, items = ntiles * splits;
   const int nk = ((K + 63) / 64 + splits - 1) / splits;  // K-tiles per item (>= 2: host)
   const int first = (blockIdx.x & 7) * 32 + (blockIdx.x >> 3);  // grid = 256
-  // segments: [upper half of tail item] + whole items first + 256 j + [lower half of tail item]
-  // roles by contiguous virtual index (T: [0, rem), H: [rem, 2 rem)), so that the WGs running
-  // whole items side by side on an XCD -- which share A row blocks in its L2 -- start their
-  // whole items in the same phase (pairing 2r with 2r + 1 put every other WG half an item
-  // behind its neighbours and lost that sharing: profiles/round4/spt_ab.txt)
-  const int rem = SPT ? items & 255 : 0, rounds = SPT ? items >> 8 : 0, khalf = nk >> 1;
-  const bool hasT = SPT && first < rem;
-  const bool hasH = SPT && first >= rem && first < 2 * rem;
-  const int pair = hasT ? first : first - rem;
-  const int nwhole = SPT ? rounds : (first < items ? (items - first + 255) >> 8 : 0);
-  const int nseg = nwhole + hasT + hasH;
+  // segments: whole items first + 256 j (< W), then (TAIL) one K-split part of a tail tile:
+  // part p = first (< T * S) is split p / T of tail tile p % T, so the WGs of an XCD run one
+  // split of neighbouring tiles (shared A row-block slices in its L2)
+  const int W = TAIL ? e.tail_r0 * ntn : items, T = items - W, TS = TAIL ? e.tail_splits : 1;
+  const bool hasTail = TAIL && first < T * TS;
+  const int tsplit = hasTail ? first / T : 0, ttile = hasTail ? first % T : 0;
+  const int tk0 = tsplit * nk / TS, tk1 = (tsplit + 1) * nk / TS;
+  const int nwhole = first < W ? (W - first + 255) >> 8 : 0;
+  const int nseg = nwhole + hasTail;
   if (nseg == 0) return;
-  const int total = nwhole * nk + (hasT ? nk - khalf : 0) + (hasH ? khalf : 0);  // K-tile steps of this WG
+  const int total = nwhole * nk + (hasTail ? tk1 - tk0 : 0);  // K-tile steps of this WG
 
   const __amdgpu_buffer_rsrc_t rsA = rsrc_of(A, (AK ? (int64_t)M * lda : (int64_t)K * lda) * 2);
   const __amdgpu_buffer_rsrc_t rsB = rsrc_of(B, (BK ? (int64_t)N * ldb : (int64_t)K * ldb) * 2);
@@ -192,11 +182,11 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     int k0, k1;      // K-tiles [k0, k1) of the item this segment runs
   };
   auto item_at = [&](int j) -> Item {
-    int it = first + ((j - (hasT ? 1 : 0)) << 8), k0 = 0, k1 = nk;
-    if (SPT && ((hasT && j == 0) || (hasH && j == nseg - 1))) {  // a half of leftover item `pair`
-      it = (rounds << 8) + pair;
-      k0 = hasT ? khalf : 0;
-      k1 = hasT ? nk : khalf;
+    int it = first + (j << 8), k0 = 0, k1 = nk;
+    if (TAIL && hasTail && j == nseg - 1) {  // this WG's K-split part of a tail tile
+      it = W + ttile;
+      k0 = tk0;
+      k1 = tk1;
     }
     const int sp = it / ntiles, tile = it - sp * ntiles, tm = tile / ntn;
     return Item{tm * 256, (tile - tm * ntn) * 256, sp * nk, k0, k1};
@@ -502,78 +492,35 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     return n0 + n1 + nd;
   };
 
-  // ---- SPT hand-off of the tail item `pair`: the payload is written and read with sc1
-  // buffer operations (write-through / read past this CU's L1) and signalled by ONE flag per
-  // pair, stored by the last wave of the producing WG to drain its stores (an LDS counter),
-  // polled by every consuming wave before its own sc1 loads; no cache-wide release / acquire
-  // (MI355X_MICROARCH visibility table, first row: 16-B sc1 payload both ways, one sc1 flag
-  // store after every storing wave's vmcnt(0), sc1 poll, one WG per CU, hipMalloc memory).
-  auto spt_rsrc = [&] { return rsrc_of(e.sk + (size_t)pair * (8 * 32768) + (size_t)wave * 32768, 32768); };
-  gu64* const spt_flag = (gu64*)(e.sk + SPT_PART_BYTES) + (size_t)pair * 8;
-  // publish the upper half's accumulators; leaves nothing in flight
-  auto spt_publish = [&]() -> int {
-#if defined(CAPK_DIAG_SPTNOHO)  // diagnostic build: the split without the hand-off (wrong results)
-    return 0;
-#endif
-    const __amdgpu_buffer_rsrc_t rsP = spt_rsrc();
-#if !defined(CAPK_DIAG_SPTNOSTORE)  // diagnostic build: no payload stores (timing only)
+  // ---- TAIL: this WG's K-split part of a tail tile -> fp32 slab tsplit (no bias / epilogue:
+  // the reduce applies them once); rows past M and columns past N are not written (a row past
+  // the slab's rows would land in the next split's slab).  Returns the stores left in flight.
+  auto tail_store = [&](const Item& c) -> int {
+    const int64_t Mt = (int64_t)M - (int64_t)e.tail_r0 * 256;
+    const __amdgpu_buffer_rsrc_t rsW = rsrc_of(e.tail_ws + (size_t)tsplit * Mt * N, Mt * N * 4);
+    auto seg = [&](auto qmc, auto qnc, auto ic) {
+      constexpr int qm = decltype(qmc)::value, qn = decltype(qnc)::value, i = decltype(ic)::value;
+      float v[8];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int t = 0; t < 2; ++t) {
-            const int r = ((a * 2 + b) * 4 + i) * 2 + t;  // (register offset in the SGPR field: one VGPR)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, acc[a][b][i][t]), rsP,
-                                                   (uint32_t)(lane * 16), r * 1024, SC1);
-          }
-#endif
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's payload has left the CU
-    if (lane == 0) {
-      const unsigned done = __hip_atomic_fetch_add(&spt_cnt[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (done == 7u) __hip_atomic_store(spt_flag, e.token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    return 0;
-  };
-  // the lower half starts from them: bounded sc1 poll, sc1 loads straight into the (zeroed,
-  // dead) accumulators; the last wave to finish its loads clears the flag for the next launch
-  // on this memory
-  auto spt_consume = [&] {
-#if defined(CAPK_DIAG_SPTNOHO)
-    zero_acc();
-    return;
-#endif
-#if !defined(CAPK_DIAG_SPTNOPOLL)
-    for (int it = 0; it < (1 << 24); ++it) {
-      if (__hip_atomic_load(spt_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == e.token) break;
-      __builtin_amdgcn_s_sleep(2);
-    }
-#endif
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the poll)
-    const __amdgpu_buffer_rsrc_t rsP = spt_rsrc();
-#if defined(CAPK_DIAG_SPTNOLOAD)  // diagnostic build: no payload loads (timing only)
-    zero_acc();
-#else
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int t = 0; t < 2; ++t) {
-            const int r = ((a * 2 + b) * 4 + i) * 2 + t;
-            acc[a][b][i][t] = __builtin_bit_cast(
-                f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsP, (uint32_t)(lane * 16), r * 1024, SC1));
-          }
-#endif
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (also retires the in-flight prefetches and stores)
-    if (lane == 0) {
-      const unsigned done = __hip_atomic_fetch_add(&spt_cnt[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (done == 7u) __hip_atomic_store(spt_flag, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+      for (int r = 0; r < 4; ++r) {
+        const float x = acc[qm][qn][i][0][r], y = acc[qm][qn][i][1][r];
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+        v[r] = __uint_as_float(sw[0]);
+        v[4 + r] = __uint_as_float(sw[1]);
+      }
+      const int64_t row = (int64_t)c.m0 - (int64_t)e.tail_r0 * 256 + qm * 128 + i * 16 + lrow;
+      const int n = c.n0 + qn * 128 + lcol;
+      const uint32_t off = row < Mt && n < N ? (uint32_t)((row * N + n) * 4) : OOR;
+      store8(rsW, off, v, (float*)nullptr);
+    };
+#define CAPK_TSEG(QM, QN, I) \
+  seg(std::integral_constant<int, QM>{}, std::integral_constant<int, QN>{}, std::integral_constant<int, I>{});
+    CAPK_TSEG(0, 0, 0) CAPK_TSEG(0, 0, 1) CAPK_TSEG(0, 0, 2) CAPK_TSEG(0, 0, 3)
+    CAPK_TSEG(0, 1, 0) CAPK_TSEG(0, 1, 1) CAPK_TSEG(0, 1, 2) CAPK_TSEG(0, 1, 3)
+    CAPK_TSEG(1, 0, 0) CAPK_TSEG(1, 0, 1) CAPK_TSEG(1, 0, 2) CAPK_TSEG(1, 0, 3)
+    CAPK_TSEG(1, 1, 0) CAPK_TSEG(1, 1, 1) CAPK_TSEG(1, 1, 2) CAPK_TSEG(1, 1, 3)
+#undef CAPK_TSEG
+    return 32;  // two 16-B stores per segment
   };
 
   // ---- main loop: gemm8p's two phases per K-tile over the continuous step sequence ----
@@ -583,11 +530,10 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
   // Step u is K-tile k of item j (u = j nk + k); steps u+1, u+2 lie in item j or j+1 (nk >= 2).
   // Wait counts: Q1(u) leaves Q2(u-1)'s loads (6, +1 with a bias DMA) younger, Q2(u) leaves
   // Q1(u)'s 2; both + S when the epilogue of item j-1 ran since the awaited issue (k == 0).
-  // SPT: segments start at K-tile cur.k0 and end at cur.k1, each >= 2 K-tiles (host: nk >= 4)
+  // TAIL: the last segment starts at K-tile cur.k0 and ends at cur.k1 (>= 4 K-tiles: host)
   Item cur = item_at(0), nxt = item_at(nseg > 1 ? 1 : 0);
-  int j = 0, k = SPT ? cur.k0 : 0;
+  int j = 0, k = TAIL ? cur.k0 : 0;
   zero_acc();
-  if (SPT && tid == 0) spt_cnt[0] = spt_cnt[1] = 0u;  // (published by the prologue's barrier)
   // prologue: A0 B0 B1 (+bias) of step 0, A1 of step 0, A0 B0 B1 of step 1
   load(0, cur, k, 0);
   load(2, cur, k, 0);
@@ -610,8 +556,8 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     readA(fa, u, 0);
     readB(fb0, u, 2);
     readB(fb1, u, 3);
-    const int kend = SPT ? cur.k1 : nk, kbn = SPT ? nxt.k0 : 0;  // this segment's end, the next's start
-    const int k0c = SPT ? cur.k0 : 0;
+    const int kend = TAIL ? cur.k1 : nk, kbn = TAIL ? nxt.k0 : 0;  // this segment's end, the next's start
+    const int k0c = TAIL ? cur.k0 : 0;
     const int e1 = k == k0c ? S : 0;
     {
       const int n1 = q2prev + e1;  // steady state: 6, +1 with a bias DMA in that phase
@@ -646,7 +592,7 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
       load(2, t2, k2, u + 2);
       load(3, t2, k2, u + 2);
       q2prev = 6;
-      if ((SPT ? !same && k + 2 == kend : k2 == 0) && has_bias) {  // the next segment's first K-tile
+      if ((TAIL ? !same && k + 2 == kend : k2 == 0) && has_bias) {  // the next segment's first K-tile
         bias_dma(t2, j + 1);
         q2prev = 7;
       }
@@ -661,25 +607,15 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     if (++k == kend) {  // the segment's last K-tile: epilogue, stores left in flight
       stamp(j, 0);
       fence();
-      if constexpr (SPT) {
-        S = (hasT && j == 0) ? spt_publish() : epilogue(cur, j);  // upper half of the tail item: hand it on
-        if (++j == nseg) break;
-        if (hasH && j == nseg - 1) {  // lower half of the tail item: start from the partner's accumulators
-          spt_consume();
-          S = 0;
-        } else {
-          zero_acc();
-        }
-        fence();
-      } else {
-        S = epilogue(cur, j);
+      {
+        S = (TAIL && hasTail && j == nseg - 1) ? tail_store(cur) : epilogue(cur, j);
         zero_acc();
         fence();
         stamp(j, 1);
         if (++j == nseg) break;
       }
       cur = nxt;
-      k = SPT ? cur.k0 : 0;
+      k = TAIL ? cur.k0 : 0;
       nxt = item_at(j + 1 < nseg ? j + 1 : j);
     }
   }
@@ -708,7 +644,6 @@ bool gemm8q_supports(const Epi& e, bool out_f32) {
   return sides <= (out_f32 ? 0 : 1) && (!(e.act & CAPK_ACT_BWD) || (e.act & CAPK_ACT_DERIV));
 }
 
-size_t gemm8q_spt_workspace() { return SPT_WS_BYTES; }
 
 #if defined(CAPK_DIAG_TRACE)
 static size_t diag_trace_bytes() { return (size_t)256 * 2 * 64 * 4 * 8; }
@@ -719,31 +654,38 @@ static void* diag_trace_buf() {
 }
 #endif
 
-// The split tail round pays when the last round is at most half full (its leftover items are
-// cut in halves over 2 * rem <= 256 WGs) and the halves are >= 2 K-tiles.  capk_gemm_set_spt /
-// CAPK_GEMM_SPT=0 turn it off (A/B).
-static int g_spt_mode = -1;
-static bool use_spt(int items, int nk) {
+// The split-K tail round: after the whole rounds, the row blocks [r0, ntm) as S K-splits per
+// tile in one more round (T tail tiles, T * S <= 256).  It pays when the tail round is long
+// enough that cutting it to 1/S plus the reduce launch (~12 us for the ViT shapes) wins: K >=
+// 1536 (24 K-tiles), S >= 2, each split >= 8 K-tiles.  capk_gemm_set_tail / CAPK_GEMM_TAIL=0
+// turn it off (A/B).
+static int g_tail_mode = -1;
+bool gemm8q_tail_plan(int M, int N, int K, int* r0, int* splits) {
   static const int env_mode = [] {
-    const char* v = getenv("CAPK_GEMM_SPT");
-    return v ? atoi(v) : 0;  // default off until it measures faster (profiles/round4/spt_ab.txt)
+    const char* v = getenv("CAPK_GEMM_TAIL");
+    return v ? atoi(v) : 1;
   }();
-  const int mode = g_spt_mode >= 0 ? g_spt_mode : env_mode;
-  const int rem = items & 255;
-  return mode != 0 && rem != 0 && rem <= 128 && nk >= 4;
+  const int mode = g_tail_mode >= 0 ? g_tail_mode : env_mode;
+  const int ntm = cdiv(M, 256), ntn = cdiv(N, 256), items = ntm * ntn, nk = cdiv(K, 64);
+  const int rounds = items >> 8;
+  if (mode == 0 || rounds < 1 || (items & 255) == 0 || nk < 24) return false;
+  const int rr0 = (rounds * 256) / ntn, T = (ntm - rr0) * ntn;
+  if (rr0 < 1 || T <= 0) return false;
+  const int S = std::min(256 / T, nk / 8);
+  if (S < 2) return false;
+  *r0 = rr0;
+  *splits = S;
+  return true;
 }
-
-static unsigned long long next_token() {
-  static std::atomic<unsigned long long> ctr{0x2545F4914F6CDD1Dull ^ (unsigned long long)time(nullptr)};
-  unsigned long long t;
-  do t = ctr.fetch_add(0x9E3779B97F4A7C15ull) + 0x9E3779B97F4A7C15ull;
-  while (t == 0);
-  return t;
+size_t gemm8q_tail_workspace(int M, int N, int K) {
+  int r0, S;
+  if (!gemm8q_tail_plan(M, N, K, &r0, &S)) return 0;
+  return (size_t)S * (size_t)(M - r0 * 256) * N * sizeof(float);
 }
 
 int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int64_t lda, const void* B, int64_t ldb,
                   int M, int N, int K, int splits, const Epi& e, float* slab, hipStream_t st, float* dsum,
-                  void* spt_ws) {
+                  void* ws, size_t ws_bytes, int* tail_r0, int* tail_splits) {
   CAPK_CHECK_ARG((a_kmajor ? (int64_t)M * lda : (int64_t)K * lda) * 2 < (1ll << 31) &&
                      (b_kmajor ? (int64_t)N * ldb : (int64_t)K * ldb) * 2 < (1ll << 31),
                  "capk_gemm(bf16, 256x256): operand larger than 2 GiB");
@@ -780,10 +722,18 @@ int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int
                  "capk_gemm(bf16, 256x256): output or side operand larger than 2 GiB");
   const int items = cdiv(M, 256) * cdiv(N, 256);
   CAPK_CHECK_ARG(items > 256, "capk_gemm(gemm8q): persistent kernel for grids of more than 256 items");
-  // (not the DSUM form, whose register budget has no room for the hand-off; bf16 outputs only)
-  if (spt_ws && !dsum && !out_f32 && use_spt(items, cdiv(K, 64))) {
-    p.sk = (char*)spt_ws;
-    p.token = next_token();
+  // the split-K tail round (not the DSUM form; bf16 outputs): the caller reduces the slabs
+  if (tail_r0) *tail_r0 = -1;
+  {
+    int r0, S;
+    if (tail_r0 && ws && !dsum && !out_f32 && gemm8q_tail_plan(M, N, K, &r0, &S) &&
+        ws_bytes >= (size_t)S * (size_t)(M - r0 * 256) * N * sizeof(float)) {
+      p.tail_ws = (float*)ws;
+      p.tail_r0 = r0;
+      p.tail_splits = S;
+      *tail_r0 = r0;
+      *tail_splits = S;
+    }
   }
   CAPK_CHECK_ARG(!fwd_act || (a_kmajor && b_kmajor), "capk_gemm(gemm8q): forward activations need K-major operands");
 #if defined(CAPK_DIAG_TRACE)
@@ -794,9 +744,9 @@ int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int
   const dim3 grid(256), block(512);
 #define L8(AK, BKM, OT, ACTK, DVK, SKK, DS)                                                                        \
   do {                                                                                                          \
-    constexpr bool SPTV = std::is_same<OT, bf16>::value && !DS;                                                 \
-    if (SPTV && p.sk)                                                                                           \
-      hipLaunchKernelGGL((gemm8q_kernel<AK, BKM, OT, ACTK, DVK, SKK, DS, SPTV>), grid, block, 0, st, A, lda, B,  \
+    constexpr bool TAILV = std::is_same<OT, bf16>::value && !DS;                                                \
+    if (TAILV && p.tail_ws)                                                                                     \
+      hipLaunchKernelGGL((gemm8q_kernel<AK, BKM, OT, ACTK, DVK, SKK, DS, TAILV>), grid, block, 0, st, A, lda, B, \
                          ldb, M, N, K, 1, p);                                                                   \
     else                                                                                                        \
       hipLaunchKernelGGL((gemm8q_kernel<AK, BKM, OT, ACTK, DVK, SKK, DS, false>), grid, block, 0, st, A, lda, B, \
@@ -857,8 +807,8 @@ extern "C" int capk_gemm_diag_trace(void* host_dst, size_t bytes) {
 }
 #endif
 
-extern "C" int capk_gemm_set_spt(int mode) {
-  CAPK_CHECK_ARG(mode >= -1 && mode <= 1, "capk_gemm_set_spt: mode must be -1 (environment), 0 or 1");
-  capk::g_spt_mode = mode;
+extern "C" int capk_gemm_set_tail(int mode) {
+  CAPK_CHECK_ARG(mode >= -1 && mode <= 1, "capk_gemm_set_tail: mode must be -1 (environment), 0 or 1");
+  capk::g_tail_mode = mode;
   return CAPK_OK;
 }

@@ -78,10 +78,11 @@ int capk_gemm_last_config(void);
 /* Test / benchmark control: force the tile configuration (cfg 1..5; 0 = automatic choice;
  * -1 = CAPK_GEMM_CFG environment value) for every later capk_gemm call. */
 int capk_gemm_force_config(int cfg);
-/* Split tail round of the persistent 256x256 kernel (grids of more than 256 items whose last
- * round is at most half full: its items are run as two K halves on two workgroups, handed
- * off through capk_gemm's workspace): 0 off (default), 1 on, -1 back to CAPK_GEMM_SPT. */
-int capk_gemm_set_spt(int mode);
+/* Split-K tail round of the persistent 256x256 kernel (grids of more than 256 items with a
+ * partial last round and K >= 1536: the row blocks past the whole rounds run as 2+ K-splits
+ * per tile into fp32 slabs in capk_gemm's workspace, then one reduce + epilogue launch):
+ * 1 on (default), 0 off, -1 back to CAPK_GEMM_TAIL. */
+int capk_gemm_set_tail(int mode);
 int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K,
               const void* A, int64_t lda, int a_kmajor,
               const void* B, int64_t ldb, int b_kmajor,

@@ -27,6 +27,11 @@ S=${STEPS:-tests}
 [[ ,$S, == *,prof3,* ]] && run prof3 420 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof3 -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --beam-batch 0
 [[ ,$S, == *,prof5,* ]] && run prof5 420 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof5 -o run -- python3 bench.py --workload config5 --steps 3 --warmup 1 --no-cpu-baseline --beam-batch 0
 [[ ,$S, == *,prof2,* ]] && run prof2 420 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof2 -o run -- python3 bench.py --workload config2 --steps 3 --warmup 2 --no-cpu-baseline
+if [[ ,$S, == *,traffic,* ]]; then  # GEMM bytes per launch for bench.py's roofline.traffic (-> profiles/round4/gemm_traffic.json)
+  run fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/fetch -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --beam-batch 0
+  run write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/write -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --beam-batch 0
+  python3 tools/pmc_traffic.py $OUT/fetch $OUT/write --out $OUT/gemm_traffic.json --cmd "python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --beam-batch 0" > /dev/null
+fi
 [[ ,$S, == *,gemmb,* ]] && run gemmb 400 python tools/gemm_bench.py ${GEMMB_ARGS:-}
 [[ ,$S, == *,extra,* ]] && run extra ${EXTRA_SECS:-300} ${EXTRA}
 exit 0

@@ -16,11 +16,6 @@ run() {  # name seconds cmd...
 }
 [[ -n "${TESTS:-}" ]] && TAILN=3 run tsel 600 python -u -m pytest -x -q -rf --timeout 120 --timeout-method thread ${TESTS}
 export GEMM_SHAPES="${GEMM_SHAPES:-dx768_197:50432:768:768:dx,dx3072_197:50432:768:3072:dx,dx2304_197:50432:768:2304:dx,res768_197:50432:768:768:fwd_res,res3072_197:50432:768:3072:fwd_res,fc1g_197:50432:3072:768:fwd_gelu_deriv,lmfwd:5120:50304:768:fwd}"
-[[ ${SKIP_SPT:-0} == 0 ]] && CAPK_GEMM_SPT=1 run spt_on 200 python tools/gemm_bench.py
-[[ ${SKIP_SPT:-0} == 0 ]] && CAPK_GEMM_SPT=0 run spt_off 200 python tools/gemm_bench.py
-[[ ${SKIP_SPT:-0} == 0 ]] && CAPK_GEMM_SPT=1 CAPK_LIB_PATH=image-captioning-ml-project_amd/capk/libcapk_diag_sptnoho.so run spt_noho 200 python tools/gemm_bench.py
-[[ ${SKIP_SPT:-0} == 0 ]] && CAPK_GEMM_SPT=1 CAPK_LIB_PATH=image-captioning-ml-project_amd/capk/libcapk_diag_sptnostore.so run spt_nostore 200 python tools/gemm_bench.py
-[[ ${SKIP_SPT:-0} == 0 ]] && CAPK_GEMM_SPT=1 CAPK_LIB_PATH=image-captioning-ml-project_amd/capk/libcapk_diag_sptnoload.so run spt_noload 200 python tools/gemm_bench.py
 [[ ${SKIP_BENCH:-0} == 0 ]] && TAILN=1 run bench_xdec 400 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --beam-batch 0
 [[ ${SKIP_BENCH:-0} == 0 ]] && TAILN=1 run bench_b 400 env ${BENCH_B_ENV:-CAPK_XDEC=0} python bench.py --steps 10 --warmup 3 --no-cpu-baseline --beam-batch 0
 [[ ${PROF:-1} == 1 ]] && TAILN=2 run prof3 420 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof3 -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --beam-batch 0

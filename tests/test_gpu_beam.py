@@ -273,11 +273,12 @@ def test_transformer_beam5_config3_bf16_vs_fp32():
     """The benchmarked path end to end: config-3 model (ViT-B/16 + 6L/8H decoder, V = 50 257),
     256 images, bf16 beam-5 through ``generate`` (graph-replayed KV-cached decode).
 
-    1. Search exactness at full size: an eager device search over the same bf16 decode steps,
-       whose logits are recorded, equals ``generate``'s graph-replayed search, and the HF
-       ``_beam_search`` restatement (oracle/beam.py) replayed on the recorded logits picks the
-       same sequences (bf16 logits can tie exactly, and torch.topk leaves the order of ties
-       unspecified: >= 95 % of the images, and the best scores to 1e-4).
+    1. Search exactness at full size: an eager device search over the same bf16 decode steps
+       equals ``generate``'s graph-replayed search, and at every step the k rows it keeps carry
+       the k best non-EOS candidate scores (running score + log-prob, recomputed in torch) to
+       1e-4 -- HF ``_beam_search``'s running-set rule, checked as values so that exact ties
+       (frequent with bf16 logits; torch.topk leaves their order unspecified) may be kept in
+       either order.
     2. Precision: against the fp32 capk search on the same weights (fp32 beam-5 is pinned
        bit-exactly to the CPU reference by test_transformer_beam5_config3_fp32_vs_oracle), the
        fp32 search is re-run with the bf16 decoder fed the same hypotheses, which gives every
@@ -308,24 +309,31 @@ def test_transformer_beam5_config3_bf16_vs_fp32():
         f32 = m32.encoder(images)["features"]
         f16 = m16.encoder(images)["features"]
         ids16, info16 = m16.generate(images=images, max_length=L, num_beams=k)
-        # 1. the eager search over recorded bf16 logits, and the oracle replay
+        # 1. an eager device search over the same bf16 decode steps, every selection checked
         r16 = KVDecodeRunner(m16.decoder, f16, k, L)
-        rec = []
+        st1 = {"S": None, "c": None, "ok": torch.ones(B, dtype=torch.bool, device="cuda"), "n": 0}
+        slot_img = torch.arange(B * k, device="cuda") // k
 
         def step16(cur_len, ids, reorder):
+            if reorder is None:
+                S = torch.full((B, k), -1e9, device="cuda")
+                S[:, 0] = 0.0
+            else:  # the rows the device kept: their scores must be the k best non-EOS candidates
+                par = reorder.long() - slot_img * k
+                S = st1["c"][slot_img, par * V + ids].view(B, k)
+                masked = st1["c"].view(B, k, V).clone()
+                masked[:, :, eos] = -float("inf")
+                best = masked.view(B, k * V).topk(k, -1).values
+                st1["ok"] &= (S.sort(1, descending=True).values - best).abs().amax(1) <= 1e-4
+                st1["n"] += 1
             lg = r16.step(cur_len, ids, reorder)
-            rec.append(lg[:, :V].float().cpu())
+            lp = torch.log_softmax(lg[:, :V].float(), -1)
+            st1["c"] = (S[:, :, None] + lp.view(B, k, V)).view(B, k * V)
             return lg
 
         e16 = beam_search(step16, B, k, L, prompt, eos, pad_token_id=pad, vocab_size=V)
     assert torch.equal(padded(e16["sequences"]), padded(ids16))
-    steps = iter(rec)
-    ref = oracle_beam(lambda seqs: next(steps, rec[-1]), B, k, L, bos=None, eos=eos, pad=pad, prompt=prompt.cpu()[:, None],
-                      vocab_size=V)
-    same_ref = (padded(ref["sequences"]) == padded(ids16).cpu()).all(1)
-    assert float(same_ref.float().mean()) >= 0.95, float(same_ref.float().mean())
-    torch.testing.assert_close(info16["sequences_scores"].cpu()[same_ref], ref["sequences_scores"][same_ref],
-                               rtol=1e-4, atol=1e-4)
+    assert st1["n"] >= 2 and bool(st1["ok"].all()), torch.nonzero(~st1["ok"]).flatten().tolist()
     # 2. bf16 vs fp32 along the fp32 path
     with torch.no_grad():
         r32 = KVDecodeRunner(m32.decoder, f32, k, L)
@@ -359,8 +367,7 @@ def test_transformer_beam5_config3_bf16_vs_fp32():
     sc = out["all_scores"]
     stable = st["stable"] & ((sc[:, 0] - sc[:, 1]) > 2 * st["err"])
     same = (padded(out["sequences"]) == padded(ids16)).all(1)
-    print(f"bf16 beam-5 at config-3 size: device search = oracle replay on its logits for "
-          f"{int(same_ref.sum())}/{B}; vs fp32: identical best sequence {float(same.float().mean()):.3f}, "
+    print(f"bf16 beam-5 at config-3 size: {st1['n']} selections x {B} images checked; vs fp32: identical best sequence {float(same.float().mean()):.3f}, "
           f"stable {int(stable.sum())}/{B} (identical {int((same & stable).sum())}), "
           f"median max candidate error {float(st['err'].median()):.3f}")
     assert bool(same[stable].all()), torch.nonzero(stable & ~same).flatten().tolist()

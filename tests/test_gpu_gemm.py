@@ -186,27 +186,27 @@ def test_dx_act_colsum_fused(M):
 @cuda
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
-def test_split_tail_exact(mode, ak, bk):
-    """The persistent kernel's split tail round (capk_gemm_set_spt(1): the leftover items of a
-    last round at most half full run as two K halves on a pair of workgroups, the upper half
-    handed to the lower through the workspace) vs whole items (0): a 273-item grid (21 x 13
-    tiles, 17 leftover items, each split) with K = 640 (10 K-tiles, halves of 5), exact
-    small-integer operands (every partial sum exact in fp32, so the hand-off must reproduce the
+def test_tail_round_exact(mode, ak, bk):
+    """The persistent kernel's split-K tail round (capk_gemm_set_tail(1): after the whole
+    round, the remaining row blocks run as K-splits into fp32 slabs, reduced with the epilogue by
+    one more launch) vs whole items (0): a 273-item grid (21 x 13 tiles: 19 row blocks of whole
+    items, 26 tail tiles x 3 splits) with K = 1536 (24 K-tiles, splits of 8), exact
+    small-integer operands (every partial sum exact in fp32, so the slabs must reproduce the
     product bit for bit), plain / bias + residual / beta * C / GELU + act' / backward * aux
-    epilogues, element by element; then two launches on one workspace (the flag words cleared)."""
+    epilogues, element by element; then two launches on one workspace."""
     from capk import _lib, ops
     from capk._lib import ACT_DERIV, ACT_GELU_ERF
     L = _lib.load()
     L.capk_gemm_force_config(6)
-    L.capk_gemm_set_spt(mode)
+    L.capk_gemm_set_tail(mode)
     try:
         g = torch.Generator(device="cuda").manual_seed(21 + 2 * ak + bk)
-        M, N, K = 20 * 256 + 72, 13 * 256, 640
+        M, N, K = 20 * 256 + 72, 13 * 256, 1536
         a = torch.randint(-2, 3, (M, K), device="cuda", generator=g).bfloat16()
         w = torch.randint(-2, 3, (N, K), device="cuda", generator=g).bfloat16()
         A = a if ak else a.t().contiguous()
         B = w if bk else w.t().contiguous()
-        ref = a.float() @ w.float().t()  # |x| <= 2560: exact in fp32; C = its bf16 rounding
+        ref = a.float() @ w.float().t()  # |x| <= 6144: exact in fp32; C = its bf16 rounding
         C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         kw = dict(lda=A.stride(0), ldb=B.stride(0), ldc=N)
         ops.gemm(A, ak, B, bk, M, N, K, C, **kw)
@@ -240,5 +240,5 @@ def test_split_tail_exact(mode, ak, bk):
                                    ws.data_ptr(), ws.numel(), ops._stream()), "capk_gemm")
             assert torch.equal(C1.float(), ref.bfloat16().float())
     finally:
-        L.capk_gemm_set_spt(-1)
+        L.capk_gemm_set_tail(-1)
         L.capk_gemm_force_config(-1)
