@@ -5,7 +5,6 @@ Every function here launches hand-written HIP kernels from libcapk.so on
 allocator), streams and autograd bookkeeping.  There is deliberately no CPU or
 eager-PyTorch fallback: a missing library or a non-GPU tensor raises.
 """
-import threading
 
 import torch
 
@@ -53,20 +52,22 @@ class KernelTimer:
 
     def __init__(self):
         self.enabled = False
-        self.thread = None
+        self.stream = None
         self.records = []  # (start_event, end_event, flops, in_dtype, algorithmic HBM bytes)
 
     def start(self):
-        """Record the GEMMs launched by the calling thread only: the config-5 SCST update runs
-        its baseline search on a side stream from a second thread, whose overlapping (and
-        mutually stretched) launches would otherwise be summed into the main stream's."""
+        """Record the GEMMs launched on the calling thread's current stream, from any thread:
+        the backward runs on autograd's device thread with the forward's stream current, while
+        the config-5 SCST baseline search runs on its own side stream from a second host thread
+        (its overlapping, mutually stretched launches would otherwise be summed in) -- as do the
+        weight gradients under CAPK_DW_STREAM=1."""
         self.records = []
-        self.thread = threading.get_ident()
+        self.stream = torch.cuda.current_stream().cuda_stream
         self.enabled = True
 
     def active(self):
-        return (self.enabled and threading.get_ident() == self.thread
-                and not torch.cuda.is_current_stream_capturing())
+        return (self.enabled and not torch.cuda.is_current_stream_capturing()
+                and torch.cuda.current_stream().cuda_stream == self.stream)
 
     def stop(self):
         self.enabled = False

@@ -654,3 +654,38 @@ def test_attention_bwd_batch_slices_identical(ops):
     assert bool(torch.isfinite(outs[0].float()).all())
     for d in outs[1:]:
         assert torch.equal(d, outs[0])
+
+
+@cuda
+def test_gemm_timer_follows_the_stream(ops):
+    """bench.py's live GEMM timer (ops.GEMM_TIMER) records the GEMMs launched on the stream it
+    was started on from any host thread -- those of a backward pass run on autograd's device
+    thread -- and none launched on another stream (the config-5 baseline search's side stream)."""
+    A = torch.randn(256, 256, device="cuda").bfloat16()
+    C = torch.empty(256, 256, device="cuda", dtype=torch.bfloat16)
+
+    def g():
+        ops.gemm(A, True, A, True, 256, 256, 256, C, lda=256, ldb=256, ldc=256)
+
+    class Fn(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x):
+            return x * 2
+
+        @staticmethod
+        def backward(ctx, gy):
+            g()
+            return gy * 2
+
+    x = torch.randn(8, device="cuda", requires_grad=True)
+    side = torch.cuda.Stream()
+    ops.GEMM_TIMER.start()
+    try:
+        g()  # main stream, this thread
+        Fn.apply(x).sum().backward()  # main stream, autograd's thread
+        with torch.cuda.stream(side):
+            g()  # another stream: not recorded
+        side.synchronize()
+    finally:
+        ops.GEMM_TIMER.stop()
+    assert ops.GEMM_TIMER.summary()["launches"] == 2
