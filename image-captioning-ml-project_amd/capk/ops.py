@@ -6,6 +6,8 @@ allocator), streams and autograd bookkeeping.  There is deliberately no CPU or
 eager-PyTorch fallback: a missing library or a non-GPU tensor raises.
 """
 
+import os
+
 import torch
 
 from . import _lib
@@ -54,6 +56,12 @@ class KernelTimer:
         self.enabled = False
         self.stream = None
         self.records = []  # (start_event, end_event, flops, in_dtype, algorithmic HBM bytes)
+        # every `stride`-th launch is bracketed: an event pair costs ~3 us of GPU time (config 3:
+        # events on all 279 launches of a step cost 3.7 % of the step); the per-step launch
+        # sequence (279 launches) is coprime to the default stride, so successive steps sample
+        # every launch position
+        self.stride = max(1, int(os.environ.get("CAPK_GEMM_TIMER_STRIDE", "5")))
+        self.seen = 0
 
     def start(self):
         """Record the GEMMs launched on the calling thread's current stream, from any thread:
@@ -62,12 +70,16 @@ class KernelTimer:
         (its overlapping, mutually stretched launches would otherwise be summed in) -- as do the
         weight gradients under CAPK_DW_STREAM=1."""
         self.records = []
+        self.seen = 0
         self.stream = torch.cuda.current_stream().cuda_stream
         self.enabled = True
 
     def active(self):
-        return (self.enabled and not torch.cuda.is_current_stream_capturing()
-                and torch.cuda.current_stream().cuda_stream == self.stream)
+        if not (self.enabled and not torch.cuda.is_current_stream_capturing()
+                and torch.cuda.current_stream().cuda_stream == self.stream):
+            return False
+        self.seen += 1
+        return (self.seen - 1) % self.stride == 0
 
     def stop(self):
         self.enabled = False
@@ -88,7 +100,8 @@ class KernelTimer:
         by_route = {name: {"launches": r[0], "total_ms": r[1], "tflops": (r[2] / (r[1] * 1e-3) / 1e12) if r[1] else 0.0}
                     for name, r in (("gemm_bf16_kernel", route[0]), ("gemm_f8", route[2]))}
         return {"launches": n, "total_ms": tot_ms, "flops": tot_flops, "by_route": by_route,
-                "avg_ms": tot_ms / max(n, 1), "avg_flops": tot_flops / max(n, 1), "avg_bytes": tot_bytes / max(n, 1)}
+                "avg_ms": tot_ms / max(n, 1), "avg_flops": tot_flops / max(n, 1), "avg_bytes": tot_bytes / max(n, 1),
+                "stride": self.stride, "launches_seen": self.seen}
 
 
 GEMM_TIMER = KernelTimer()

@@ -214,10 +214,14 @@ def test_clip_gpt2_fp8_logits_vs_oracle(fp8_everywhere):
     model, store, cfg, sd = _clip_gpt2("fp8")
     model.eval()
     images, caps = _inputs()
+    stride, ops.GEMM_TIMER.stride = ops.GEMM_TIMER.stride, 1  # bracket every launch
     ops.GEMM_TIMER.start()
-    with torch.no_grad():
-        got = model(images=images.cuda(), captions=caps.cuda())["logits"].float().cpu()
-    ops.GEMM_TIMER.stop()
+    try:
+        with torch.no_grad():
+            got = model(images=images.cuda(), captions=caps.cuda())["logits"].float().cpu()
+    finally:
+        ops.GEMM_TIMER.stop()
+        ops.GEMM_TIMER.stride = stride
     launches = ops.GEMM_TIMER.summary()["by_route"]["gemm_f8"]["launches"]
     assert launches >= 12 * 4 + 12 * 4 + 1, launches  # every CLIP / GPT-2 block product + LM head
     with torch.no_grad():

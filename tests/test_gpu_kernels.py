@@ -679,6 +679,7 @@ def test_gemm_timer_follows_the_stream(ops):
 
     x = torch.randn(8, device="cuda", requires_grad=True)
     side = torch.cuda.Stream()
+    stride, ops.GEMM_TIMER.stride = ops.GEMM_TIMER.stride, 1  # bracket every launch
     ops.GEMM_TIMER.start()
     try:
         g()  # main stream, this thread
@@ -688,4 +689,15 @@ def test_gemm_timer_follows_the_stream(ops):
         side.synchronize()
     finally:
         ops.GEMM_TIMER.stop()
+        ops.GEMM_TIMER.stride = stride
     assert ops.GEMM_TIMER.summary()["launches"] == 2
+    ops.GEMM_TIMER.stride = 2  # sampling: launches 1, 3, 5 of 6 on the stream
+    ops.GEMM_TIMER.start()
+    try:
+        for _ in range(6):
+            g()
+    finally:
+        ops.GEMM_TIMER.stop()
+        ops.GEMM_TIMER.stride = stride
+    sm = ops.GEMM_TIMER.summary()
+    assert sm["launches"] == 3 and sm["launches_seen"] == 6
