@@ -21,6 +21,7 @@ buffers are t-major ([T, B, ...]); the LM head works on b-major rows so the logi
 the [B, T, V] view the CE kernel consumes.
 """
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -29,6 +30,11 @@ from .. import ops
 from .common import G, CapkModule, W, next_seed
 from .transformer import _pad64, _pad_bias, _pad_bias_grad, _padded_grad
 from .attention import build_attention
+
+# bf16 teacher-forced pass: each step-and-layer recurrence as ONE two-segment product into
+# fp32 split-K slabs that the cell kernel sums (capk_gemm_pair_slabs), instead of two GEMMs
+# and two split-K reduces.  CAPK_LSTM_PAIR=0 restores the per-GEMM route (A/B).
+_PAIR = os.environ.get("CAPK_LSTM_PAIR", "1") != "0"
 
 
 class _LSTMParams(nn.Module):
@@ -111,8 +117,26 @@ class _LSTMFn(torch.autograd.Function):
         Hd = [torch.empty(T, B, D, dtype=dt, device=dev) for _ in range(L - 1)] if p > 0 else None
         drops = [[drop() for _ in range(L - 1)] for _ in range(T)]
         gates = torch.empty(B, 4 * D, dtype=dt, device=dev)
+        pair = dt == torch.bfloat16 and _PAIR and D % 128 == 0  # (seams on 128-column tiles)
+        if pair:
+            # gates = [x | h] [W_ih | W_hh]^T (K seam at D) as fp32 slabs summed in the cell
+            wsf = torch.empty(ops.pair_slabs_plan(B, 4 * D, 2 * D)[1], dtype=torch.float32, device=dev)
         for t in range(T):
             for layer in range(L):
+                if pair:
+                    if layer == 0:  # x = ctx_{t-1} against W_ih0[:, E:]; pre0 carries the embedding half + b_ih
+                        a1, b1, ldb1, res, ba = CtxT[t], w_ih0[:, E:], E + D, pre0[t * B:(t + 1) * B], None
+                    else:
+                        a1 = Hd[layer - 1][t] if Hd is not None else Hs[layer - 1][t + 1]
+                        b1, ldb1, res = W(lstm.w("weight_ih", layer), dt), D, None
+                        ba = lstm.w("bias_ih", layer).detach()
+                    sf = ops.gemm_pair_slabs(B, 4 * D, 2 * D, a1, D, b1, ldb1, True, wsf, A2=Hs[layer][t], lda2=D,
+                                             B2=W(lstm.w("weight_hh", layer), dt), ldb2=D, k1=D)
+                    hd = Hd[layer][t] if (Hd is not None and layer < L - 1) else None
+                    ops.lstm_cell_fwd_slabs(wsf, sf, 4 * D, ba, lstm.w("bias_hh", layer).detach(), res, Cs[layer][t],
+                                            Cs[layer][t + 1], Hs[layer][t + 1], acts[layer][t], h_drop=hd,
+                                            drop=drops[t][layer] if hd is not None else ops.NO_DROP)
+                    continue
                 if layer == 0:
                     ops.gemm(CtxT[t], True, w_ih0[:, E:], True, B, 4 * D, D, gates, lda=D, ldb=E + D, ldc=4 * D,
                              residual=pre0[t * B:(t + 1) * B], ldr=4 * D)
@@ -173,11 +197,37 @@ class _LSTMFn(torch.autograd.Function):
         dctx_carry = torch.empty(B, D, dtype=dt, device=dev)
         dh_tot = torch.empty(B, D, dtype=dt, device=dev)
         w_ih0 = W(lstm.weight_ih_l0, dt)
+        pair = dt == torch.bfloat16 and _PAIR and L > 1 and D % 128 == 0
+        if pair:
+            # layers >= 1: [dh_below | dnext] = dG [W_ih | W_hh] (N seam at D) as fp32 slabs P[l];
+            # the layer below's cell sums the first half (under its dropout mask), this layer's
+            # cell at t-1 the second (the top layer's: instead of the attention's dq residual)
+            sb, nb = ops.pair_slabs_plan(B, 2 * D, 4 * D)
+            P = [None] + [torch.empty(nb, dtype=torch.float32, device=dev) for _ in range(1, L)]
         for t in range(T - 1, -1, -1):
             dctx_t = dCtxT[t] if t == T - 1 else dctx_carry
             # attention: d(query) + recurrent grad of the top layer
-            att.step_bwd(H, t, dctx_t, dh_tot, dq_residual=dh[L - 1], dc_mem_out=dc[L - 1])
-            for layer in range(L - 1, -1, -1):
+            att.step_bwd(H, t, dctx_t, dh_tot, dq_residual=None if pair else dh[L - 1], dc_mem_out=dc[L - 1])
+            for layer in range(L - 1, -1, -1) if pair else ():
+                rec = (P[layer], sb, 2 * D, D) if (layer > 0 and t < T - 1) else None
+                if layer == L - 1:
+                    ops.lstm_cell_bwd_slabs(acts[layer][t], Cs[layer][t], dc[layer], dG[layer][t], dh=dh_tot, rec=rec)
+                else:
+                    ops.lstm_cell_bwd_slabs(acts[layer][t], Cs[layer][t], dc[layer], dG[layer][t],
+                                            dh=dh[0] if layer == 0 else None, up=(P[layer + 1], sb, 2 * D),
+                                            drop=drops[t][layer] if Hd is not None else ops.NO_DROP, rec=rec)
+                if layer > 0:
+                    ops.gemm_pair_slabs(B, 2 * D, 4 * D, dG[layer][t], 4 * D, W(lstm.w("weight_ih", layer), dt), D,
+                                        False, P[layer], B2=W(lstm.w("weight_hh", layer), dt), ldb2=D, n1=D)
+                    continue
+                dnext = torch.empty(B, D, dtype=dt, device=dev)
+                ops.linear_dx(dG[0][t], W(lstm.weight_hh_l0, dt), out=dnext)
+                ops.gemm(dG[0][t], True, w_ih0[:, :E], False, B, E, 4 * D, dEmb[t], lda=4 * D, ldb=E + D, ldc=E)
+                if t > 0:
+                    ops.gemm(dG[0][t], True, w_ih0[:, E:], False, B, D, 4 * D, dctx_carry, lda=4 * D, ldb=E + D,
+                             ldc=D, residual=dCtxT[t - 1], ldr=D)
+                dh[0] = dnext
+            for layer in range(L - 1, -1, -1) if not pair else ():
                 src = dh_tot if layer == L - 1 else dh_below
                 ops.lstm_cell_bwd(acts[layer][t], Cs[layer][t], src, dc[layer], dG[layer][t])
                 # recurrent state gradient for step t-1
@@ -195,6 +245,9 @@ class _LSTMFn(torch.autograd.Function):
                         ops.gemm(dG[0][t], True, w_ih0[:, E:], False, B, D, 4 * D, dctx_carry, lda=4 * D,
                                  ldb=E + D, ldc=D, residual=dCtxT[t - 1], ldr=D)
                 dh[layer] = dnext
+        if pair:  # the recurrent gradients w.r.t. the initial states of layers >= 1
+            for layer in range(1, L):
+                dh[layer] = ops.slab_sum(P[layer], sb, B, 2 * D, D, torch.empty(B, D, dtype=dt, device=dev))
         # batched weight gradients over all steps
         for layer in range(L):
             g = dG[layer].view(T * B, 4 * D)

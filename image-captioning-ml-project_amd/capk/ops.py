@@ -6,6 +6,7 @@ allocator), streams and autograd bookkeeping.  There is deliberately no CPU or
 eager-PyTorch fallback: a missing library or a non-GPU tensor raises.
 """
 
+import ctypes
 import os
 
 import torch
@@ -656,6 +657,64 @@ def lstm_cell_bwd(act, c_prev, dh, dc, dgates):
     B, D = c_prev.shape
     check(lib().capk_lstm_cell_bwd(dtype_code(act), B, D, _p(act), _p(c_prev), _p(dh), dh.stride(0), _p(dc),
                                    _p(dgates), _stream()), "capk_lstm_cell_bwd")
+
+
+def pair_slabs_plan(M, N, K):
+    """(split count, fp32 elements) of capk_gemm_pair_slabs' slabs for an (M, N, K) product."""
+    s = ctypes.c_int(0)
+    nbytes = lib().capk_gemm_pair_workspace(M, N, K, ctypes.byref(s))
+    return s.value, nbytes // 4
+
+
+def gemm_pair_slabs(M, N, K, A, lda, B, ldb, b_kmajor, ws, *, A2=None, lda2=0, B2=None, ldb2=0, k1=0, n1=0):
+    """Two-segment bf16 product into fp32 split-K slabs ws[s][M][N] (capk.h): K seam k1
+    ([A | A2] [B | B2]^T) or N seam n1 (C[:, :n1] = A B^T, C[:, n1:] = A B2^T).  Returns
+    the split count."""
+    _need_gpu(A, B, B2, ws)
+    L = lib()
+    s = ctypes.c_int(0)
+    timed = GEMM_TIMER.active()
+    if timed:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    check(L.capk_gemm_pair_slabs(M, N, K, _p(A), lda, 1, _p(B), ldb, int(b_kmajor), _p(A2), lda2, _p(B2), ldb2,
+                                 int(k1), int(n1), _p(ws), ws.numel() * ws.element_size(), ctypes.byref(s),
+                                 _stream()), "capk_gemm_pair_slabs")
+    if timed:
+        ev1.record()
+        # operands read once, the slabs written once
+        nbytes = A.element_size() * (M * K + N * K) + 4 * s.value * M * N
+        GEMM_TIMER.records.append((ev0, ev1, 2.0 * M * N * K, dtype_code(A), nbytes, 0))
+    return s.value
+
+
+def lstm_cell_fwd_slabs(ws, splits, ldw, bias_a, bias_b, res, c_prev, c_out, h_out, act, h_drop=None, drop=NO_DROP):
+    B, D = c_prev.shape
+    check(lib().capk_lstm_cell_fwd_slabs(B, D, _p(ws), int(splits), ldw, _p(bias_a), _p(bias_b), _p(res),
+                                         res.stride(0) if res is not None else 0, _p(c_prev), _p(c_out), _p(h_out),
+                                         h_out.stride(0), _p(h_drop), h_drop.stride(0) if h_drop is not None else 0,
+                                         _p(act), float(drop[0]), int(drop[1]) & 0xFFFFFFFF, _stream()),
+          "capk_lstm_cell_fwd_slabs")
+
+
+def lstm_cell_bwd_slabs(act, c_prev, dc, dgates, *, dh=None, up=None, drop=NO_DROP, rec=None):
+    """up / rec: (slab tensor, splits, ld[, col]) -- the layer above's input-gradient slabs
+    (columns 0:D, under the forward's dropout mask) and this layer's recurrent slabs."""
+    B, D = c_prev.shape
+    uw, us, ul = up if up is not None else (None, 0, 0)
+    rw, rs, rl, rc = rec if rec is not None else (None, 0, 0, 0)
+    check(lib().capk_lstm_cell_bwd_slabs(B, D, _p(act), _p(c_prev), _p(dh), dh.stride(0) if dh is not None else 0,
+                                         _p(uw), int(us), ul, float(drop[0]), int(drop[1]) & 0xFFFFFFFF, _p(rw),
+                                         int(rs), rl, int(rc), _p(dc), _p(dgates), _stream()),
+          "capk_lstm_cell_bwd_slabs")
+
+
+def slab_sum(ws, splits, M, ldw, col0, out):
+    """out [M, ncols] bf16 view = sum over the splits of ws[s][:, col0:col0+ncols]."""
+    check(lib().capk_slab_sum(M, out.shape[1], _p(ws), int(splits), ldw, int(col0), _p(out), out.stride(0),
+                              _stream()), "capk_slab_sum")
+    return out
 
 
 def soft_attn_fwd(qp, kp, v, we, be, inv_temp, ctx, w_out, key_pad=None):

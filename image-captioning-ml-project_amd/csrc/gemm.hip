@@ -24,10 +24,22 @@ namespace capk {
 // Main loop: an NST-deep LDS ring.  Before reading K-tile kt a counted
 // `s_waitcnt vmcnt` retires only that tile (the NST-2 younger ones stay in flight),
 // then a raw s_barrier publishes it and the slot freed one iteration ago is refilled.
-template <int BMX, int BKX, int NST, bool AK, bool BK, typename OutT>
+// Second operand pair of a two-segment product (PAIR instantiations; the LSTM recurrences):
+// K-concatenated, C = [A | A2] [B | B2]^T with K-tiles k >= k1 read from A2 / B2 at k - k1
+// (both operands K-major), or N-concatenated, columns n >= n1 of C = A B2^T (n - n1) and
+// columns n < n1 = A B^T.  k1 % BKX == 0 and n1 % BN == 0, so no tile straddles the seam.
+struct Seg2 {
+  const bf16* A2;
+  int64_t lda2;
+  const bf16* B2;
+  int64_t ldb2;
+  int k1, n1;
+};
+
+template <int BMX, int BKX, int NST, bool AK, bool BK, typename OutT, bool PAIR = false>
 __global__ __launch_bounds__(BMX / 32 * 64) void gemm_bf16_kernel(
     const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb, int M, int N, int K, int splits,
-    Epi e, float* __restrict__ ws) {
+    Epi e, float* __restrict__ ws, Seg2 g2) {
   using C = Cfg<BMX, BKX, NST>;
   __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -41,15 +53,31 @@ __global__ __launch_bounds__(BMX / 32 * 64) void gemm_bf16_kernel(
   const int kt0 = split * kt_per;
   const int kt1 = min(nk_all, kt0 + kt_per);
   const int nk = max(0, kt1 - kt0);
+  // this tile's B operand: the N-concatenated pair's second matrix past column n1
+  const bf16* Bt = B;
+  int64_t ldbt = ldb;
+  int nb = N, nb0 = n0;
+  if constexpr (PAIR) {
+    if (g2.n1 > 0) {
+      if (n0 >= g2.n1) Bt = g2.B2, ldbt = g2.ldb2, nb = N - g2.n1, nb0 = n0 - g2.n1;
+      else nb = g2.n1;
+    }
+  }
   // range-checked descriptors for MN-major operands: [0, K*ld) elements are valid
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)((int64_t)K * lda * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, (int)((int64_t)K * ldb * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bt, (short)0, (int)((int64_t)K * ldbt * 2), 0x00020000);
 
   auto stage = [&](int kt, int slot) {
     char* base = smem + slot * C::STAGE;
-    stage_tile<AK, BMX, BKX, C::A_PIECES>(A, lda, M, m0, (kt0 + kt) * BKX, base, wave * C::A_PIECES, lane, rsA);
-    stage_tile<BK, BN, BKX, C::B_PIECES>(B, ldb, N, n0, (kt0 + kt) * BKX, base + C::A_BYTES, wave * C::B_PIECES,
-                                         lane, rsB);
+    int kg = (kt0 + kt) * BKX;
+    const bf16* As = A;
+    const bf16* Bs = Bt;
+    int64_t las = lda, lbs = ldbt;
+    if constexpr (PAIR) {
+      if (g2.k1 > 0 && kg >= g2.k1) As = g2.A2, las = g2.lda2, Bs = g2.B2, lbs = g2.ldb2, kg -= g2.k1;
+    }
+    stage_tile<AK, BMX, BKX, C::A_PIECES>(As, las, M, m0, kg, base, wave * C::A_PIECES, lane, rsA);
+    stage_tile<BK, BN, BKX, C::B_PIECES>(Bs, lbs, nb, nb0, kg, base + C::A_BYTES, wave * C::B_PIECES, lane, rsB);
   };
 
   f32x4 acc[4][4];
@@ -458,7 +486,7 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
   float* slab = splits > 1 ? (float*)ws : nullptr;
 #define LAUNCH1(BMX, BKX, NST, AK, BKM, OT)                                                                     \
   hipLaunchKernelGGL((gemm_bf16_kernel<BMX, BKX, NST, AK, BKM, OT>), dim3(grid), dim3(BMX / 32 * 64), 0, st, \
-                     (const bf16*)A, lda, (const bf16*)B, ldb, M, N, K, splits, e, slab)
+                     (const bf16*)A, lda, (const bf16*)B, ldb, M, N, K, splits, e, slab, Seg2{})
 #define LAUNCH(AK, BKM, OT)                                    \
   do {                                                         \
     switch (cfg) {                                             \
@@ -543,6 +571,61 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
       hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)ws, splits, e);
     CAPK_LAUNCH_CHECK("splitk_reduce_kernel");
   }
+  return CAPK_OK;
+}
+
+// Two-segment products into fp32 split-K slabs, no epilogue: the LSTM recurrences, whose
+// consumers (the cell kernels, lstm.hip) sum the slabs themselves -- one launch per step and
+// layer in place of two GEMMs and two split-K reduces.  128x128 ring tiles; splits so that
+// about one round of WGs runs, every split >= CAPK_PAIR_MINKT (4) K-tiles.
+static int pair_splits(int M, int N, int K) {
+  static const int min_kt = [] {
+    const char* v = getenv("CAPK_PAIR_MINKT");
+    return v ? std::max(1, atoi(v)) : 4;
+  }();
+  const int tiles = cdiv(M, 128) * cdiv(N, BN), nk = cdiv(K, 64);
+  const int s = std::max(1, std::min(256 / tiles, nk / min_kt));
+  return cdiv(nk, cdiv(nk, s));  // effective count: every split owns >= 1 K-tile
+}
+
+extern "C" size_t capk_gemm_pair_workspace(int M, int N, int K, int* splits) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  const int s = pair_splits(M, N, K);
+  if (splits) *splits = s;
+  return (size_t)s * M * N * sizeof(float);
+}
+
+extern "C" int capk_gemm_pair_slabs(int M, int N, int K, const void* A, int64_t lda, int a_kmajor, const void* B,
+                                    int64_t ldb, int b_kmajor, const void* A2, int64_t lda2, const void* B2,
+                                    int64_t ldb2, int k1, int n1, float* ws, size_t ws_bytes, int* splits_out,
+                                    void* stream) {
+  CAPK_CHECK_ARG(M > 0 && N > 0 && K > 0 && A && B && B2 && ws, "capk_gemm_pair_slabs: bad arguments");
+  CAPK_CHECK_ARG((k1 > 0) != (n1 > 0), "capk_gemm_pair_slabs: exactly one of k1 (K seam) / n1 (N seam)");
+  CAPK_CHECK_ARG(a_kmajor, "capk_gemm_pair_slabs: A must be K-major");
+  CAPK_CHECK_ARG(k1 == 0 || (A2 && b_kmajor && k1 % 64 == 0 && (K - k1) % 64 == 0 && k1 < K),
+                 "capk_gemm_pair_slabs: K seam k1=%d needs K-major A2/B2 and k1, K-k1 multiples of 64", k1);
+  CAPK_CHECK_ARG(n1 == 0 || (n1 % BN == 0 && n1 < N), "capk_gemm_pair_slabs: N seam n1=%d must be a multiple of %d",
+                 n1, BN);
+  CAPK_CHECK_ARG(K % 64 == 0 && N % 8 == 0, "capk_gemm_pair_slabs: K=%d %% 64, N=%d %% 8", K, N);
+  CAPK_CHECK_ARG(b_kmajor || (int64_t)K * std::max(ldb, ldb2) * 2 < (1ll << 31), "capk_gemm_pair_slabs: B too large");
+  CAPK_CHECK_ARG(((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && ((uintptr_t)B2 % 16 == 0) &&
+                     (!A2 || (uintptr_t)A2 % 16 == 0) && lda % 8 == 0 && ldb % 8 == 0 && lda2 % 8 == 0 &&
+                     ldb2 % 8 == 0,
+                 "capk_gemm_pair_slabs: operands must be 16-B aligned with leading dimensions %% 8 == 0");
+  const int splits = pair_splits(M, N, K);
+  CAPK_CHECK_ARG(ws_bytes >= (size_t)splits * M * N * sizeof(float), "capk_gemm_pair_slabs: workspace too small");
+  Epi e{nullptr, N, 1.f, 0.f, nullptr, nullptr, 0, 0, nullptr, nullptr, 0, M, N, make_drop(0.f, 0)};
+  const Seg2 g2{(const bf16*)A2, lda2, (const bf16*)B2, ldb2, k1, n1};
+  const int grid = cdiv(M, 128) * cdiv(N, BN) * splits;
+  g_last_cfg = 1;
+  if (b_kmajor)
+    hipLaunchKernelGGL((gemm_bf16_kernel<128, 64, 2, true, true, bf16, true>), dim3(grid), dim3(256), 0, S(stream),
+                       (const bf16*)A, lda, (const bf16*)B, ldb, M, N, K, splits, e, ws, g2);
+  else
+    hipLaunchKernelGGL((gemm_bf16_kernel<128, 64, 2, true, false, bf16, true>), dim3(grid), dim3(256), 0, S(stream),
+                       (const bf16*)A, lda, (const bf16*)B, ldb, M, N, K, splits, e, ws, g2);
+  CAPK_LAUNCH_CHECK("gemm_bf16_kernel(pair)");
+  if (splits_out) *splits_out = splits;
   return CAPK_OK;
 }
 

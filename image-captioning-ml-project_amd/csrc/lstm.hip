@@ -67,6 +67,100 @@ __global__ __launch_bounds__(256) void lstm_cell_bwd_kernel(int B, int D, const 
   }
 }
 
+// The same cells fed by the recurrent pair product's fp32 split-K slabs (capk_gemm_pair_slabs:
+// slab s of a [B, ldw] product at ws + s * B * ldw), summed here instead of by a reduce
+// launch.  Forward: gates = sum_s slab[s] + bias_a + bias_b (+ res, bf16).
+__global__ __launch_bounds__(256) void lstm_cell_fwd_slabs_kernel(
+    int B, int D, const float* __restrict__ ws, int splits, int64_t ldw, const float* __restrict__ ba,
+    const float* __restrict__ bb, const bf16* __restrict__ res, int64_t ldr, const float* __restrict__ c_prev,
+    float* __restrict__ c_out, bf16* __restrict__ h_out, int64_t ldh, bf16* __restrict__ h_drop, int64_t ldhd,
+    bf16* __restrict__ act, Drop drop) {
+  const int64_t n = (int64_t)B * D, ss = (int64_t)B * ldw;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int b = (int)(e / D), d = (int)(e % D);
+    float g[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int col = q * D + d;
+      g[q] = (ba ? ba[col] : 0.f) + (bb ? bb[col] : 0.f) + (res ? to_f32(res[(int64_t)b * ldr + col]) : 0.f);
+    }
+    const float* w = ws + (int64_t)b * ldw + d;
+    int s = 0;
+    for (; s + 2 <= splits; s += 2, w += 2 * ss) {  // 8 independent loads in flight per thread
+      float x[8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[q] = w[q * D], x[4 + q] = w[ss + q * D];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) g[q] += x[q] + x[4 + q];
+    }
+    if (s < splits) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) g[q] += w[q * D];
+    }
+    const float i = sigm(g[0]), f = sigm(g[1]), gg = tanhf(g[2]), o = sigm(g[3]);
+    const float c = f * c_prev[e] + i * gg;
+    const float h = o * tanhf(c);
+    c_out[e] = c;
+    h_out[(int64_t)b * ldh + d] = from_f32<bf16>(h);
+    if (h_drop) h_drop[(int64_t)b * ldhd + d] = from_f32<bf16>(drop.on() ? h * drop.mul((uint64_t)e) : h);
+    bf16* a = act + (int64_t)b * 4 * D;
+    a[d] = from_f32<bf16>(i);
+    a[D + d] = from_f32<bf16>(f);
+    a[2 * D + d] = from_f32<bf16>(gg);
+    a[3 * D + d] = from_f32<bf16>(o);
+  }
+}
+
+// sum over n slabs of one element (slab stride ss), 4 loads in flight, fixed order
+__device__ __forceinline__ float slab_col_sum(const float* __restrict__ w, int n, int64_t ss) {
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int s = 0;
+  for (; s + 4 <= n; s += 4, w += 4 * ss) a0 += w[0], a1 += w[ss], a2 += w[2 * ss], a3 += w[3 * ss];
+  for (; s < n; ++s, w += ss) a0 += *w;
+  return (a0 + a1) + (a2 + a3);
+}
+
+// Backward: the gradient w.r.t. h' = dh (bf16, optional) + drop(sum_s up[s][:, 0:D]) (the layer
+// above's input gradient through the forward's dropout mask, index b*D + d) + sum_s rec[s][:, colr:colr+D]
+// (this layer's recurrent gradient from step t+1).
+__global__ __launch_bounds__(256) void lstm_cell_bwd_slabs_kernel(
+    int B, int D, const bf16* __restrict__ act, const float* __restrict__ c_prev, const bf16* __restrict__ dh,
+    int64_t lddh, const float* __restrict__ wsu, int su, int64_t ldu, Drop drop, const float* __restrict__ wsr, int sr,
+    int64_t ldrr, int colr, float* __restrict__ dc, bf16* __restrict__ dgates) {
+  const int64_t n = (int64_t)B * D;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int b = (int)(e / D), d = (int)(e % D);
+    float gh = dh ? to_f32(dh[(int64_t)b * lddh + d]) : 0.f;
+    if (wsu) {
+      const float u = slab_col_sum(wsu + (int64_t)b * ldu + d, su, (int64_t)B * ldu);
+      gh += drop.on() ? u * drop.mul((uint64_t)e) : u;
+    }
+    if (wsr) gh += slab_col_sum(wsr + (int64_t)b * ldrr + colr + d, sr, (int64_t)B * ldrr);
+    const bf16* a = act + (int64_t)b * 4 * D;
+    const float i = to_f32(a[d]), f = to_f32(a[D + d]), g = to_f32(a[2 * D + d]), o = to_f32(a[3 * D + d]);
+    const float cp = c_prev[e];
+    const float c = f * cp + i * g;
+    const float tc = tanhf(c);
+    const float dct = dc[e] + gh * o * (1.f - tc * tc);
+    bf16* dg = dgates + (int64_t)b * 4 * D;
+    dg[d] = from_f32<bf16>(dct * g * i * (1.f - i));
+    dg[D + d] = from_f32<bf16>(dct * cp * f * (1.f - f));
+    dg[2 * D + d] = from_f32<bf16>(dct * i * (1.f - g * g));
+    dg[3 * D + d] = from_f32<bf16>(gh * tc * o * (1.f - o));
+    dc[e] = dct * f;
+  }
+}
+
+// out[m][j] = sum_s ws[s][m][col0 + j] (slabs of a [M, ldw] product), bf16.
+__global__ __launch_bounds__(256) void slab_sum_kernel(int M, int ncols, const float* __restrict__ ws, int splits,
+                                                       int64_t ldw, int col0, bf16* __restrict__ out, int64_t ldo) {
+  const int64_t n = (int64_t)M * ncols, ss = (int64_t)M * ldw;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int m = (int)(e / ncols), j = (int)(e % ncols);
+    out[(int64_t)m * ldo + j] = from_f32<bf16>(slab_col_sum(ws + (int64_t)m * ldw + col0 + j, splits, ss));
+  }
+}
+
 // ------------------------------------------------------------ soft attention --
 static constexpr int SA_MAXS = 256;
 // energy nonlinearity: 0 = tanh (SoftAttention, attention.py:100), 1 = ReLU (legacy
@@ -248,6 +342,45 @@ extern "C" int capk_lstm_cell_bwd(int dtype, int B, int D, const void* act, cons
   DT2(dtype, K, 0);
 #undef K
   CAPK_LAUNCH_CHECK("lstm_cell_bwd_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_lstm_cell_fwd_slabs(int B, int D, const float* ws, int splits, int64_t ldw, const float* bias_a,
+                                        const float* bias_b, const void* res, int64_t ldr, const float* c_prev,
+                                        float* c_out, void* h_out, int64_t ldh, void* h_drop, int64_t ldhd, void* act,
+                                        float drop_p, uint32_t drop_seed, void* stream) {
+  CAPK_CHECK_ARG(B > 0 && D > 0 && ws && splits > 0 && ldw >= 4 * D && ldh >= D && (!res || ldr >= 4 * D) &&
+                     c_prev && c_out && h_out && act,
+                 "capk_lstm_cell_fwd_slabs: bad arguments");
+  hipLaunchKernelGGL(lstm_cell_fwd_slabs_kernel, dim3(grid_n((int64_t)B * D)), dim3(256), 0, S(stream), B, D, ws,
+                     splits, ldw, bias_a, bias_b, (const bf16*)res, ldr, c_prev, c_out, (bf16*)h_out, ldh,
+                     (bf16*)h_drop, ldhd, (bf16*)act, make_drop(drop_p, drop_seed));
+  CAPK_LAUNCH_CHECK("lstm_cell_fwd_slabs_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_lstm_cell_bwd_slabs(int B, int D, const void* act, const float* c_prev, const void* dh,
+                                        int64_t lddh, const float* ws_up, int splits_up, int64_t ld_up, float drop_p,
+                                        uint32_t drop_seed, const float* ws_rec, int splits_rec, int64_t ld_rec,
+                                        int col_rec, float* dc, void* dgates, void* stream) {
+  CAPK_CHECK_ARG(B > 0 && D > 0 && act && c_prev && dc && dgates && (!dh || lddh >= D) &&
+                     (!ws_up || (splits_up > 0 && ld_up >= D)) &&
+                     (!ws_rec || (splits_rec > 0 && col_rec >= 0 && ld_rec >= col_rec + D)),
+                 "capk_lstm_cell_bwd_slabs: bad arguments");
+  hipLaunchKernelGGL(lstm_cell_bwd_slabs_kernel, dim3(grid_n((int64_t)B * D)), dim3(256), 0, S(stream), B, D,
+                     (const bf16*)act, c_prev, (const bf16*)dh, lddh, ws_up, splits_up, ld_up,
+                     make_drop(drop_p, drop_seed), ws_rec, splits_rec, ld_rec, col_rec, dc, (bf16*)dgates);
+  CAPK_LAUNCH_CHECK("lstm_cell_bwd_slabs_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_slab_sum(int M, int ncols, const float* ws, int splits, int64_t ldw, int col0, void* out,
+                             int64_t ldo, void* stream) {
+  CAPK_CHECK_ARG(M > 0 && ncols > 0 && ws && out && splits > 0 && col0 >= 0 && ldw >= col0 + ncols && ldo >= ncols,
+                 "capk_slab_sum: bad arguments");
+  hipLaunchKernelGGL(slab_sum_kernel, dim3(grid_n((int64_t)M * ncols)), dim3(256), 0, S(stream), M, ncols, ws, splits,
+                     ldw, col0, (bf16*)out, ldo);
+  CAPK_LAUNCH_CHECK("slab_sum_kernel");
   return CAPK_OK;
 }
 

@@ -92,6 +92,19 @@ int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K,
               float drop_p, uint32_t drop_seed,
               void* ws, size_t ws_bytes, void* stream);
 
+/* Two-segment bf16 product into fp32 split-K slabs, no epilogue (the LSTM recurrences of
+ * decoders.py:199 / nn.LSTM: one launch per step and layer instead of the x W_ih^T and
+ * h W_hh^T GEMMs with their reduces; the cell kernels below sum the slabs).
+ *   k1 > 0 (K seam): C = [A | A2] [B | B2]^T, A (M x k1), A2 (M x (K - k1)), B / B2 K-major
+ *     (N x k1 / N x (K - k1)); k1 and K - k1 multiples of 64.
+ *   n1 > 0 (N seam): C[:, :n1] = A B^T, C[:, n1:] = A B2^T (B / B2 as b_kmajor says, n1 % 128 == 0).
+ *   A K-major.  Slab s = ws + s*M*N ([M][N] fp32), s < *splits_out; capk_gemm_pair_workspace
+ *   returns the bytes and the split count for (M, N, K). */
+size_t capk_gemm_pair_workspace(int M, int N, int K, int* splits);
+int capk_gemm_pair_slabs(int M, int N, int K, const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ldb,
+                         int b_kmajor, const void* A2, int64_t lda2, const void* B2, int64_t ldb2, int k1, int n1,
+                         float* ws, size_t ws_bytes, int* splits_out, void* stream);
+
 /* ------------------------------------------------- fp8 (config 5) --------
  * The forward Linear / Conv1D products of BASELINE config 5 ("fp8 MFMA") on OCP e4m3fn
  * operands with one power-of-two scale per row, stored as its E8M0 code (2^(code-127)):
@@ -378,6 +391,22 @@ int capk_lstm_cell_fwd(int dtype, int B, int D, const void* gates, int64_t ldg, 
                        uint32_t drop_seed, void* stream);
 int capk_lstm_cell_bwd(int dtype, int B, int D, const void* act, const float* c_prev, const void* dh, int64_t lddh,
                        float* dc, void* dgates, void* stream);
+/* The cells fed by capk_gemm_pair_slabs' slabs (bf16, slab s of a [B, ld] product at
+ * ws + s*B*ld).  Forward: gates = sum_s ws[s] + bias_a + bias_b (+ res [B, 4D] bf16; biases
+ * fp32, optional).  Backward: grad w.r.t. h' = dh (optional bf16) + dropout(sum_s
+ * ws_up[s][:, 0:D]) (the layer above's input gradient, mask of the forward's h_drop, index
+ * b*D + d) + sum_s ws_rec[s][:, col_rec:col_rec+D] (the recurrent gradient from step t+1);
+ * either slab set optional.  capk_slab_sum: out[m][j] = bf16(sum_s ws[s][m][col0 + j]). */
+int capk_lstm_cell_fwd_slabs(int B, int D, const float* ws, int splits, int64_t ldw, const float* bias_a,
+                             const float* bias_b, const void* res, int64_t ldr, const float* c_prev, float* c_out,
+                             void* h_out, int64_t ldh, void* h_drop, int64_t ldhd, void* act, float drop_p,
+                             uint32_t drop_seed, void* stream);
+int capk_lstm_cell_bwd_slabs(int B, int D, const void* act, const float* c_prev, const void* dh, int64_t lddh,
+                             const float* ws_up, int splits_up, int64_t ld_up, float drop_p, uint32_t drop_seed,
+                             const float* ws_rec, int splits_rec, int64_t ld_rec, int col_rec, float* dc,
+                             void* dgates, void* stream);
+int capk_slab_sum(int M, int ncols, const float* ws, int splits, int64_t ldw, int col0, void* out, int64_t ldo,
+                  void* stream);
 /* SoftAttention (src/models/attention.py:57-118) for one decode step, one query per
  * image: e[b,s] = (sum_d we[d] tanh(qp[b,d] + kp[b,s,d]) + be) * inv_temp, key_pad ->
  * -1e9, w = softmax_s(e), ctx[b] = sum_s w[b,s] v[b,s] (w_out fp32 [B,S]).  kp is the

@@ -184,3 +184,88 @@ def test_lstm_full_size_vs_oracle(precision, tol):
                 ref = p[n].grad
                 err = float((prm._capk_grad.float().cpu() - ref).norm())
                 assert err <= 1e-3 * float(ref.norm()) + 1e-6, (n, err, float(ref.norm()))
+
+
+@cuda
+def test_gemm_pair_slabs_k_and_n_seams():
+    """capk_gemm_pair_slabs: the slabs sum to [A | A2] [B | B2]^T (K seam, both K-major) and
+    to [A B^T | A B2^T] (N seam, N-major B as in dX = dG W) -- fp32 accumulation of bf16
+    products, compared with the fp32 product of the same bf16 values."""
+    from capk import ops
+    torch.manual_seed(5)
+    M, D = 128, 768
+    bf = torch.bfloat16
+    x, h = torch.randn(M, D, device="cuda", dtype=bf), torch.randn(M, D, device="cuda", dtype=bf)
+    wi, wh = torch.randn(4 * D, D, device="cuda", dtype=bf), torch.randn(4 * D, D, device="cuda", dtype=bf)
+    s, n = ops.pair_slabs_plan(M, 4 * D, 2 * D)
+    ws = torch.full((n,), float("nan"), device="cuda")
+    got_s = ops.gemm_pair_slabs(M, 4 * D, 2 * D, x, D, wi, D, True, ws, A2=h, lda2=D, B2=wh, ldb2=D, k1=D)
+    assert got_s == s and s > 1
+    got = ws[:s * M * 4 * D].view(s, M, 4 * D).sum(0)
+    ref = x.float() @ wi.float().t() + h.float() @ wh.float().t()
+    assert float((got - ref).norm() / ref.norm()) < 1e-5
+    # N seam: dG [M, 4D] against W_ih, W_hh as N-major operands -> [dG W_ih | dG W_hh]
+    dg = torch.randn(M, 4 * D, device="cuda", dtype=bf)
+    s, n = ops.pair_slabs_plan(M, 2 * D, 4 * D)
+    ws = torch.full((n,), float("nan"), device="cuda")
+    assert ops.gemm_pair_slabs(M, 2 * D, 4 * D, dg, 4 * D, wi, D, False, ws, B2=wh, ldb2=D, n1=D) == s
+    got = ws[:s * M * 2 * D].view(s, M, 2 * D).sum(0)
+    ref = torch.cat([dg.float() @ wi.float(), dg.float() @ wh.float()], 1)
+    assert float((got - ref).norm() / ref.norm()) < 1e-5
+    out = torch.empty(M, D, device="cuda", dtype=bf)
+    ops.slab_sum(ws, s, M, 2 * D, D, out)
+    assert float((out.float() - ref[:, D:]).norm() / ref[:, D:].norm()) < 4e-3
+
+
+@cuda
+def test_lstm_pair_route_matches_gemm_route_train_bf16():
+    """The bf16 teacher-forced pass with the pair-slab recurrences (default) against the
+    per-GEMM route (two GEMMs + reduces per step and layer) on the same weights, inputs and
+    dropout seeds, in train mode at the config-2 geometry (768 x 6 layers, inter-layer and
+    output dropout on): logits, d(features), d(pooled) and every parameter gradient within
+    3e-2 relative (bf16 rounding of the two routes differs: fp32 slab sums vs bf16 gates)."""
+    import capk.models.lstm as mlstm
+    from capk.models import common
+    from capk.train import CombinedLoss
+    dec, _ = _full_lstm("bf16")
+    dec.train()
+    B, T, S, D = 16, 20, 49, 768
+    g = torch.Generator().manual_seed(4)
+    feats = torch.randn(B, S, D, generator=g).cuda().bfloat16()
+    pooled = torch.randn(B, D, generator=g).cuda().bfloat16()
+    caps = torch.randint(0, 50256, (B, T), generator=g).cuda()
+    runs = []
+    saved = mlstm._PAIR
+    try:
+        for pair in (True, False):
+            mlstm._PAIR = pair
+            common._SEED[0] = 777
+            for p in dec.parameters():
+                if getattr(p, "_capk_grad", None) is not None:
+                    p._capk_grad.zero_()
+            fg = feats.clone().requires_grad_(True)
+            pg = pooled.clone().requires_grad_(True)
+            out = dec({"features": fg, "pooled_features": pg, "attention_mask": None}, caps)
+            loss = CombinedLoss(50256)(logits=out["logits"], targets=caps)["total_loss"]
+            loss.backward()
+            grads = {n: p._capk_grad.float().clone() for n, p in dec.named_parameters()
+                     if getattr(p, "_capk_grad", None) is not None}
+            runs.append((out["logits"].detach().float(), fg.grad.float(), pg.grad.float(), grads))
+    finally:
+        mlstm._PAIR = saved
+
+    def rel(a, b):
+        return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+    (la, fa, pa, ga), (lb, fb, pb, gb) = runs
+    assert rel(la, lb) < 3e-2 and rel(fa, fb) < 3e-2 and rel(pa, pb) < 3e-2
+    checked = 0
+    for n, ref in gb.items():
+        if float(ref.norm()) == 0.0:
+            continue
+        if n.startswith("lstm.") or n.startswith("init_") or n.startswith("attention."):
+            err = float((ga[n] - ref).norm())
+            # the attention energy bias has a true gradient of 0: absolute floor
+            assert err <= 3e-2 * float(ref.norm()) + 1e-3, (n, err, float(ref.norm()))
+            checked += 1
+    assert checked >= 4 * 6
