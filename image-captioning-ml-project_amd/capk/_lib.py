@@ -98,7 +98,7 @@ SIGNATURES = {
                                       _i64, _c_p, _f, _u32, _c_p]),
     "capk_lstm_cell_bwd_slabs": (_i, [_i, _i, _c_p, _c_p, _c_p, _i64, _c_p, _i, _i64, _f, _u32, _c_p, _i, _i64, _i,
                                       _c_p, _c_p, _c_p]),
-    "capk_slab_sum": (_i, [_i, _i, _c_p, _i, _i64, _i, _c_p, _i64, _c_p]),
+    "capk_slab_sum": (_i, [_i, _i, _c_p, _i, _i64, _i, _c_p, _i64, _c_p, _i64, _c_p]),
     "capk_soft_attn_fwd": (_i, [_i, _i, _i, _i, _c_p, _i64, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _c_p, _f, _c_p,
                                 _c_p, _i64, _c_p, _c_p]),
     "capk_soft_attn_bwd": (_i, [_i, _i, _i, _i, _c_p, _i64, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _f, _c_p, _c_p,

@@ -204,6 +204,12 @@ class _LSTMFn(torch.autograd.Function):
             # cell at t-1 the second (the top layer's: instead of the attention's dq residual)
             sb, nb = ops.pair_slabs_plan(B, 2 * D, 4 * D)
             P = [None] + [torch.empty(nb, dtype=torch.float32, device=dev) for _ in range(1, L)]
+            # layer 0: [dEmb | dctx | dnext] = dG0 [W_ih0 | W_hh0] (N seam at E + D) into P0
+            pair0 = (E + D) % 128 == 0
+            if pair0:
+                N0 = E + 2 * D
+                s0, n0 = ops.pair_slabs_plan(B, N0, 4 * D)
+                P0 = torch.empty(n0, dtype=torch.float32, device=dev)
         for t in range(T - 1, -1, -1):
             dctx_t = dCtxT[t] if t == T - 1 else dctx_carry
             # attention: d(query) + recurrent grad of the top layer
@@ -213,12 +219,22 @@ class _LSTMFn(torch.autograd.Function):
                 if layer == L - 1:
                     ops.lstm_cell_bwd_slabs(acts[layer][t], Cs[layer][t], dc[layer], dG[layer][t], dh=dh_tot, rec=rec)
                 else:
+                    if layer == 0 and pair0:
+                        rec = (P0, s0, N0, E + D) if t < T - 1 else None
                     ops.lstm_cell_bwd_slabs(acts[layer][t], Cs[layer][t], dc[layer], dG[layer][t],
-                                            dh=dh[0] if layer == 0 else None, up=(P[layer + 1], sb, 2 * D),
+                                            dh=dh[0] if (layer == 0 and not pair0) else None,
+                                            up=(P[layer + 1], sb, 2 * D),
                                             drop=drops[t][layer] if Hd is not None else ops.NO_DROP, rec=rec)
                 if layer > 0:
                     ops.gemm_pair_slabs(B, 2 * D, 4 * D, dG[layer][t], 4 * D, W(lstm.w("weight_ih", layer), dt), D,
                                         False, P[layer], B2=W(lstm.w("weight_hh", layer), dt), ldb2=D, n1=D)
+                    continue
+                if pair0:
+                    ops.gemm_pair_slabs(B, N0, 4 * D, dG[0][t], 4 * D, w_ih0, E + D, False, P0,
+                                        B2=W(lstm.weight_hh_l0, dt), ldb2=D, n1=E + D)
+                    ops.slab_sum(P0, s0, B, N0, 0, dEmb[t])
+                    if t > 0:
+                        ops.slab_sum(P0, s0, B, N0, E, dctx_carry, res=dCtxT[t - 1])
                     continue
                 dnext = torch.empty(B, D, dtype=dt, device=dev)
                 ops.linear_dx(dG[0][t], W(lstm.weight_hh_l0, dt), out=dnext)
@@ -245,9 +261,11 @@ class _LSTMFn(torch.autograd.Function):
                         ops.gemm(dG[0][t], True, w_ih0[:, E:], False, B, D, 4 * D, dctx_carry, lda=4 * D,
                                  ldb=E + D, ldc=D, residual=dCtxT[t - 1], ldr=D)
                 dh[layer] = dnext
-        if pair:  # the recurrent gradients w.r.t. the initial states of layers >= 1
+        if pair:  # the recurrent gradients w.r.t. the initial states
             for layer in range(1, L):
                 dh[layer] = ops.slab_sum(P[layer], sb, B, 2 * D, D, torch.empty(B, D, dtype=dt, device=dev))
+            if pair0:
+                dh[0] = ops.slab_sum(P0, s0, B, N0, E + D, torch.empty(B, D, dtype=dt, device=dev))
         # batched weight gradients over all steps
         for layer in range(L):
             g = dG[layer].view(T * B, 4 * D)

@@ -710,10 +710,11 @@ def lstm_cell_bwd_slabs(act, c_prev, dc, dgates, *, dh=None, up=None, drop=NO_DR
           "capk_lstm_cell_bwd_slabs")
 
 
-def slab_sum(ws, splits, M, ldw, col0, out):
-    """out [M, ncols] bf16 view = sum over the splits of ws[s][:, col0:col0+ncols]."""
-    check(lib().capk_slab_sum(M, out.shape[1], _p(ws), int(splits), ldw, int(col0), _p(out), out.stride(0),
-                              _stream()), "capk_slab_sum")
+def slab_sum(ws, splits, M, ldw, col0, out, res=None):
+    """out [M, ncols] bf16 view = sum over the splits of ws[s][:, col0:col0+ncols] (+ res)."""
+    check(lib().capk_slab_sum(M, out.shape[1], _p(ws), int(splits), ldw, int(col0), _p(res),
+                              res.stride(0) if res is not None else 0, _p(out), out.stride(0), _stream()),
+          "capk_slab_sum")
     return out
 
 

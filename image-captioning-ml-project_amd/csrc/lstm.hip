@@ -151,13 +151,15 @@ __global__ __launch_bounds__(256) void lstm_cell_bwd_slabs_kernel(
   }
 }
 
-// out[m][j] = sum_s ws[s][m][col0 + j] (slabs of a [M, ldw] product), bf16.
+// out[m][j] = sum_s ws[s][m][col0 + j] (+ res[m][j]) (slabs of a [M, ldw] product), bf16.
 __global__ __launch_bounds__(256) void slab_sum_kernel(int M, int ncols, const float* __restrict__ ws, int splits,
-                                                       int64_t ldw, int col0, bf16* __restrict__ out, int64_t ldo) {
+                                                       int64_t ldw, int col0, const bf16* __restrict__ res,
+                                                       int64_t ldr, bf16* __restrict__ out, int64_t ldo) {
   const int64_t n = (int64_t)M * ncols, ss = (int64_t)M * ldw;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
     const int m = (int)(e / ncols), j = (int)(e % ncols);
-    out[(int64_t)m * ldo + j] = from_f32<bf16>(slab_col_sum(ws + (int64_t)m * ldw + col0 + j, splits, ss));
+    const float r = res ? to_f32(res[(int64_t)m * ldr + j]) : 0.f;
+    out[(int64_t)m * ldo + j] = from_f32<bf16>(slab_col_sum(ws + (int64_t)m * ldw + col0 + j, splits, ss) + r);
   }
 }
 
@@ -374,12 +376,13 @@ extern "C" int capk_lstm_cell_bwd_slabs(int B, int D, const void* act, const flo
   return CAPK_OK;
 }
 
-extern "C" int capk_slab_sum(int M, int ncols, const float* ws, int splits, int64_t ldw, int col0, void* out,
-                             int64_t ldo, void* stream) {
-  CAPK_CHECK_ARG(M > 0 && ncols > 0 && ws && out && splits > 0 && col0 >= 0 && ldw >= col0 + ncols && ldo >= ncols,
+extern "C" int capk_slab_sum(int M, int ncols, const float* ws, int splits, int64_t ldw, int col0, const void* res,
+                             int64_t ldr, void* out, int64_t ldo, void* stream) {
+  CAPK_CHECK_ARG(M > 0 && ncols > 0 && ws && out && splits > 0 && col0 >= 0 && ldw >= col0 + ncols && ldo >= ncols &&
+                     (!res || ldr >= ncols),
                  "capk_slab_sum: bad arguments");
   hipLaunchKernelGGL(slab_sum_kernel, dim3(grid_n((int64_t)M * ncols)), dim3(256), 0, S(stream), M, ncols, ws, splits,
-                     ldw, col0, (bf16*)out, ldo);
+                     ldw, col0, (const bf16*)res, ldr, (bf16*)out, ldo);
   CAPK_LAUNCH_CHECK("slab_sum_kernel");
   return CAPK_OK;
 }

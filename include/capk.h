@@ -396,7 +396,8 @@ int capk_lstm_cell_bwd(int dtype, int B, int D, const void* act, const float* c_
  * fp32, optional).  Backward: grad w.r.t. h' = dh (optional bf16) + dropout(sum_s
  * ws_up[s][:, 0:D]) (the layer above's input gradient, mask of the forward's h_drop, index
  * b*D + d) + sum_s ws_rec[s][:, col_rec:col_rec+D] (the recurrent gradient from step t+1);
- * either slab set optional.  capk_slab_sum: out[m][j] = bf16(sum_s ws[s][m][col0 + j]). */
+ * either slab set optional.  capk_slab_sum: out[m][j] = bf16(sum_s ws[s][m][col0 + j] + res[m][j])
+ * (res bf16, optional). */
 int capk_lstm_cell_fwd_slabs(int B, int D, const float* ws, int splits, int64_t ldw, const float* bias_a,
                              const float* bias_b, const void* res, int64_t ldr, const float* c_prev, float* c_out,
                              void* h_out, int64_t ldh, void* h_drop, int64_t ldhd, void* act, float drop_p,
@@ -405,8 +406,8 @@ int capk_lstm_cell_bwd_slabs(int B, int D, const void* act, const float* c_prev,
                              const float* ws_up, int splits_up, int64_t ld_up, float drop_p, uint32_t drop_seed,
                              const float* ws_rec, int splits_rec, int64_t ld_rec, int col_rec, float* dc,
                              void* dgates, void* stream);
-int capk_slab_sum(int M, int ncols, const float* ws, int splits, int64_t ldw, int col0, void* out, int64_t ldo,
-                  void* stream);
+int capk_slab_sum(int M, int ncols, const float* ws, int splits, int64_t ldw, int col0, const void* res, int64_t ldr,
+                  void* out, int64_t ldo, void* stream);
 /* SoftAttention (src/models/attention.py:57-118) for one decode step, one query per
  * image: e[b,s] = (sum_d we[d] tanh(qp[b,d] + kp[b,s,d]) + be) * inv_temp, key_pad ->
  * -1e9, w = softmax_s(e), ctx[b] = sum_s w[b,s] v[b,s] (w_out fp32 [B,S]).  kp is the

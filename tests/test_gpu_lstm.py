@@ -215,6 +215,10 @@ def test_gemm_pair_slabs_k_and_n_seams():
     out = torch.empty(M, D, device="cuda", dtype=bf)
     ops.slab_sum(ws, s, M, 2 * D, D, out)
     assert float((out.float() - ref[:, D:]).norm() / ref[:, D:].norm()) < 4e-3
+    res = torch.randn(M, D, device="cuda", dtype=bf)
+    ops.slab_sum(ws, s, M, 2 * D, 0, out, res=res)
+    want = ref[:, :D] + res.float()
+    assert float((out.float() - want).norm() / want.norm()) < 4e-3
 
 
 @cuda
