@@ -131,7 +131,7 @@ SIGNATURES = {
                          _c_p]),
     "capk_col2im": (_i, [_i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _c_p, _c_p, _f, _c_p]),
     "capk_bn_workspace": (_sz, [_i, _i]),
-    "capk_bn_stats": (_i, [_i, _i, _i, _c_p, _i64, _f, _f, _c_p, _c_p, _c_p, _c_p, _c_p, _sz, _c_p]),
+    "capk_bn_stats": (_i, [_i, _i, _i, _c_p, _i64, _f, _f, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _sz, _c_p]),
     "capk_bn_eval_stats": (_i, [_i, _c_p, _c_p, _f, _c_p, _c_p, _c_p]),
     "capk_bn_apply": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _c_p, _c_p, _c_p, _c_p, _i64, _i, _c_p, _i64, _c_p]),
     "capk_bn_bwd": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p, _i64, _c_p, _c_p, _c_p, _c_p, _c_p, _i, _c_p, _i64,

@@ -110,8 +110,10 @@ def conv_bwd(conv, dz, col, B, H, W, dt, *, need_dx=True, dx=None, beta=0.0):
 def bn_fwd(bn, z, training, *, residual=None, relu=True):
     """nn.BatchNorm2d (+ residual) (+ ReLU) on channels-last rows; returns (y, mean, rstd)."""
     if training:
-        mean, rstd = ops.bn_stats(z, bn.eps, bn.momentum, bn.running_mean, bn.running_var)
-        bn.num_batches_tracked.add_(1)
+        nbt = bn.num_batches_tracked
+        if nbt is not None and (nbt.dtype != torch.int64 or not nbt.is_cuda):
+            raise TypeError("capk BatchNorm: num_batches_tracked must be an int64 device tensor")
+        mean, rstd = ops.bn_stats(z, bn.eps, bn.momentum, bn.running_mean, bn.running_var, nbt)
     else:
         mean, rstd = ops.bn_eval_stats(bn.running_mean, bn.running_var, bn.eps)
     y = ops.bn_apply(z, mean, rstd, bn.weight.detach(), bn.bias.detach(), residual=residual, relu=relu)

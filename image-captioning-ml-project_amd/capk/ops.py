@@ -827,8 +827,9 @@ def _bn_ws(M, C, device):
     return _ws(lib().capk_bn_workspace(M, C), device)
 
 
-def bn_stats(x, eps, momentum, running_mean=None, running_var=None):
-    """Training-mode BatchNorm statistics of the rows of x [M, C]: (mean, rstd) fp32."""
+def bn_stats(x, eps, momentum, running_mean=None, running_var=None, num_batches_tracked=None):
+    """Training-mode BatchNorm statistics of the rows of x [M, C]: (mean, rstd) fp32; the
+    running buffers and the int64 batch counter (all optional) are updated in the launch."""
     _need_gpu(x)
     M, C = x.shape
     mean = torch.empty(C, dtype=torch.float32, device=x.device)
@@ -837,7 +838,8 @@ def bn_stats(x, eps, momentum, running_mean=None, running_var=None):
     wsb = L.capk_bn_workspace(M, C)
     ws = _ws(wsb, x.device)
     check(L.capk_bn_stats(dtype_code(x), M, C, _p(x), x.stride(0), float(eps), float(momentum), _p(mean), _p(rstd),
-                          _p(running_mean), _p(running_var), _p(ws), wsb, _stream()), "capk_bn_stats")
+                          _p(running_mean), _p(running_var), _p(num_batches_tracked), _p(ws), wsb, _stream()),
+          "capk_bn_stats")
     return mean, rstd
 
 

@@ -118,6 +118,10 @@ __global__ __launch_bounds__(256) void col2im_kernel(int B, int H, int W, int C,
 //   MODE 0: s0 = sum x
 //   MODE 1: s0 = sum (x - mean)^2
 //   MODE 2: dz = dy * [y > 0] (if ymask), s0 = sum dz, s1 = sum dz * (x - mean) * rstd
+//   MODE 3: s0 = sum x, s1 = sum (x - mean_b)^2 about the block's own mean mean_b = s0 / n_b,
+//           from sums of x - K and (x - K)^2 with the shift K = the block's first row (a sample
+//           of the column, so no cancellation to speak of), merged by bn_finish_stats_kernel --
+//           the forward statistics in one sweep over x
 constexpr int BN_MAX_CPB = 2048;
 
 template <typename T, int MODE>
@@ -126,7 +130,7 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(int M, int C, int rows_p
                                                         const T* __restrict__ ym, int64_t ldym,
                                                         const float* __restrict__ mean,
                                                         const float* __restrict__ rstd, float* __restrict__ part) {
-  constexpr int NACC = MODE == 2 ? 2 : 1;
+  constexpr int NACC = MODE >= 2 ? 2 : 1;
   __shared__ float red[NACC][256 * 8];
   const int cpb = C < BN_MAX_CPB ? C : BN_MAX_CPB;
   const int tpr = cpb / 8, rg = 256 / tpr;
@@ -137,7 +141,8 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(int M, int C, int rows_p
   float a0[8] = {0, 0, 0, 0, 0, 0, 0, 0}, a1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float mu[8], rs[8];
   if (r0 < rg) {
-    if (MODE >= 1) Vec8<float>::load(mean + c, mu);
+    if (MODE == 3) Vec8<T>::load(x + (int64_t)m0 * ldx + c, mu);  // the shift K
+    if (MODE == 1 || MODE == 2) Vec8<float>::load(mean + c, mu);
     if (MODE == 2) Vec8<float>::load(rstd + c, rs);
     for (int m = m0 + r0; m < m1; m += rg) {
       float v[8];
@@ -145,6 +150,9 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(int M, int C, int rows_p
       if (MODE == 0) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) a0[j] += v[j];
+      } else if (MODE == 3) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { const float d = v[j] - mu[j]; a0[j] += d; a1[j] += d * d; }
       } else if (MODE == 1) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) { const float d = v[j] - mu[j]; a0[j] += d * d; }
@@ -169,17 +177,26 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(int M, int C, int rows_p
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     red[0][tid * 8 + j] = a0[j];
-    if (MODE == 2) red[NACC - 1][tid * 8 + j] = a1[j];
+    if (MODE >= 2) red[NACC - 1][tid * 8 + j] = a1[j];
   }
   __syncthreads();
   for (int e = tid; e < cpb; e += 256) {
     const int l = e / 8, j = e % 8;
+    float sq[NACC];
 #pragma unroll
     for (int q = 0; q < NACC; ++q) {
       float s = 0.f;
       for (int r = 0; r < rg; ++r) s += red[q][(r * tpr + l) * 8 + j];
-      part[((int64_t)blockIdx.y * NACC + q) * C + blockIdx.x * cpb + e] = s;
+      sq[q] = s;
     }
+    if constexpr (MODE == 3) {  // shifted sums -> (sum x, M2 about the block mean)
+      const float K = to_f32(x[(int64_t)m0 * ldx + blockIdx.x * cpb + e]), nb = (float)(m1 - m0);
+      const float S = sq[0], Q = sq[1];
+      sq[0] = nb * K + S;
+      sq[1] = fmaxf(0.f, Q - S * (S / nb));
+    }
+#pragma unroll
+    for (int q = 0; q < NACC; ++q) part[((int64_t)blockIdx.y * NACC + q) * C + blockIdx.x * cpb + e] = sq[q];
   }
 }
 
@@ -198,7 +215,7 @@ __global__ __launch_bounds__(1024) void bn_finish_kernel(int M, int C, int split
                                                          float* __restrict__ out1, float* __restrict__ run_mean,
                                                          float* __restrict__ run_var, const float* __restrict__ mean,
                                                          float* __restrict__ g0, float* __restrict__ g1,
-                                                         int accumulate) {
+                                                         int accumulate, int64_t* __restrict__ nbt) {
   constexpr int NACC = MODE == 2 ? 2 : 1;
   float s0 = finish_parts16(part, (int64_t)NACC * C, splits, C), s1 = 0.f;
   if (MODE == 2) {
@@ -206,6 +223,7 @@ __global__ __launch_bounds__(1024) void bn_finish_kernel(int M, int C, int split
     s1 = finish_parts16(part + C, (int64_t)NACC * C, splits, C);
   }
   const int c = blockIdx.x * BNF_COLS + threadIdx.x;
+  if (MODE == 1 && nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
   if (threadIdx.x >= BNF_COLS || c >= C) return;
   if (MODE == 0) {
     out0[c] = s0 / (float)M;
@@ -223,6 +241,63 @@ __global__ __launch_bounds__(1024) void bn_finish_kernel(int M, int C, int split
     if (g0) g0[c] = accumulate ? g0[c] + s1 : s1;  // dgamma
     if (g1) g1[c] = accumulate ? g1[c] + s0 : s0;  // dbeta
   }
+}
+
+// Forward statistics from MODE-3 partials (s0_b = sum x, M2_b over n_b = min(rps, M - b*rps)
+// rows), one sweep: with K = split 0's mean, M*var = sum_b [M2_b + n_b (s0_b/n_b - K)^2]
+// - M (mean - K)^2 (exact; K within a few sigma / sqrt(n_0) of the mean, so nothing cancels);
+// rstd, the running statistics and num_batches_tracked (+1, block 0) as nn.BatchNorm2d's
+// training forward.  16 columns x 64 split phases per block as finish_parts16.
+__global__ __launch_bounds__(1024) void bn_finish_stats_kernel(int M, int C, int splits, int rps,
+                                                               const float* __restrict__ part, float eps,
+                                                               float momentum, float* __restrict__ mean,
+                                                               float* __restrict__ rstd, float* __restrict__ run_mean,
+                                                               float* __restrict__ run_var, int64_t* __restrict__ nbt) {
+  __shared__ float red_s[64][BNF_COLS + 1], red_q[64][BNF_COLS + 1];
+  const int cc = threadIdx.x & 15, ph = threadIdx.x >> 4, i = blockIdx.x * BNF_COLS + cc;
+  const int64_t ld = 2 * (int64_t)C;
+  float K = 0.f, S0 = 0.f, S1 = 0.f, Q0 = 0.f, Q1 = 0.f;
+  if (i < C) {
+    K = part[i] / (float)min(rps, M);
+    int b = ph;
+    for (; b + 64 < splits; b += 128) {  // two parts in flight
+      const float na = (float)min(rps, M - b * rps), nb = (float)min(rps, M - (b + 64) * rps);
+      const float sa = part[b * ld + i], ma = part[b * ld + C + i];
+      const float sb = part[(b + 64) * ld + i], mb = part[(b + 64) * ld + C + i];
+      const float da = sa / na - K, db = sb / nb - K;
+      S0 += sa, S1 += sb;
+      Q0 += ma + na * da * da;
+      Q1 += mb + nb * db * db;
+    }
+    if (b < splits) {
+      const float na = (float)min(rps, M - b * rps), sa = part[b * ld + i];
+      const float da = sa / na - K;
+      S0 += sa;
+      Q0 += part[b * ld + C + i] + na * da * da;
+    }
+  }
+  red_s[ph][cc] = S0 + S1;
+  red_q[ph][cc] = Q0 + Q1;
+  __syncthreads();
+  if (threadIdx.x < 64) {  // 4 lanes per column, 16 phases each, then two shuffles
+    const int q = threadIdx.x >> 4;
+    float ts = 0.f, tq = 0.f;
+#pragma unroll
+    for (int p = 0; p < 16; ++p) ts += red_s[q * 16 + p][cc], tq += red_q[q * 16 + p][cc];
+    ts += __shfl_xor(ts, 16, 64);
+    ts += __shfl_xor(ts, 32, 64);
+    tq += __shfl_xor(tq, 16, 64);
+    tq += __shfl_xor(tq, 32, 64);
+    if (threadIdx.x < BNF_COLS && i < C) {
+      const float mu = ts / (float)M, dm = mu - K;
+      const float m2 = fmaxf(0.f, tq - (float)M * dm * dm), var = m2 / (float)M;
+      mean[i] = mu;
+      rstd[i] = 1.0f / sqrtf(var + eps);
+      if (run_mean) run_mean[i] = (1.f - momentum) * run_mean[i] + momentum * mu;
+      if (run_var) run_var[i] = (1.f - momentum) * run_var[i] + momentum * (M > 1 ? m2 / (float)(M - 1) : var);
+    }
+  }
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
 }
 
 __global__ void bn_eval_kernel(int C, const float* __restrict__ rm, const float* __restrict__ rv, float eps,
@@ -542,8 +617,8 @@ extern "C" size_t capk_bn_workspace(int M, int C) {
 }
 
 extern "C" int capk_bn_stats(int dtype, int M, int C, const void* x, int64_t ldx, float eps, float momentum,
-                             float* mean, float* rstd, float* running_mean, float* running_var, void* ws,
-                             size_t ws_bytes, void* stream) {
+                             float* mean, float* rstd, float* running_mean, float* running_var,
+                             int64_t* num_batches_tracked, void* ws, size_t ws_bytes, void* stream) {
   CAPK_CHECK_ARG(M > 0 && bn_shape_ok(C) && ldx % 8 == 0, "capk_bn_stats: bad shape M=%d C=%d", M, C);
   CAPK_CHECK_ARG(ws && ws_bytes >= capk_bn_workspace(M, C), "capk_bn_stats: workspace too small");
   const BnGeom g = bn_geom(M, C);
@@ -553,17 +628,30 @@ extern "C" int capk_bn_stats(int dtype, int M, int C, const void* x, int64_t ldx
 #define L(T, MODE)                                                                                                \
   hipLaunchKernelGGL((bn_reduce_kernel<T, MODE>), grid, dim3(256), 0, st, M, C, g.rps, (const T*)x, ldx,         \
                      (const T*)nullptr, (int64_t)0, (const T*)nullptr, (int64_t)0, (const float*)mean, (const float*)rstd, part)
+  // one sweep (shifted per-block sums, merged exactly) unless CAPK_BN_TWOPASS=1 (the global two-pass A/B)
+  static const bool two_pass = [] {
+    const char* v = getenv("CAPK_BN_TWOPASS");
+    return v && v[0] == '1';
+  }();
+  if (!two_pass) {
+    DT_DISPATCH(dtype, L, 3)
+    CAPK_LAUNCH_CHECK("bn_reduce_kernel<3>");
+    hipLaunchKernelGGL(bn_finish_stats_kernel, dim3(cdiv(C, BNF_COLS)), dim3(1024), 0, st, M, C, g.splits, g.rps,
+                       (const float*)part, eps, momentum, mean, rstd, running_mean, running_var, num_batches_tracked);
+    CAPK_LAUNCH_CHECK("bn_finish_stats_kernel");
+    return CAPK_OK;
+  }
   DT_DISPATCH(dtype, L, 0)
   CAPK_LAUNCH_CHECK("bn_reduce_kernel<0>");
   hipLaunchKernelGGL(bn_finish_kernel<0>, dim3(cdiv(C, BNF_COLS)), dim3(1024), 0, st, M, C, g.splits, (const float*)part,
                      eps, momentum, mean, rstd, (float*)nullptr, (float*)nullptr, (const float*)nullptr,
-                     (float*)nullptr, (float*)nullptr, 0);
+                     (float*)nullptr, (float*)nullptr, 0, (int64_t*)nullptr);
   DT_DISPATCH(dtype, L, 1)
   CAPK_LAUNCH_CHECK("bn_reduce_kernel<1>");
 #undef L
   hipLaunchKernelGGL(bn_finish_kernel<1>, dim3(cdiv(C, BNF_COLS)), dim3(1024), 0, st, M, C, g.splits, (const float*)part,
                      eps, momentum, mean, rstd, running_mean, running_var, (const float*)mean, (float*)nullptr,
-                     (float*)nullptr, 0);
+                     (float*)nullptr, 0, num_batches_tracked);
   CAPK_LAUNCH_CHECK("bn_finish_kernel");
   return CAPK_OK;
 }
@@ -612,7 +700,7 @@ extern "C" int capk_bn_bwd(int dtype, int M, int C, const void* dy, int64_t lddy
   CAPK_LAUNCH_CHECK("bn_reduce_kernel<2>");
   hipLaunchKernelGGL(bn_finish_kernel<2>, dim3(cdiv(C, BNF_COLS)), dim3(1024), 0, st, M, C, g.splits, (const float*)part,
                      0.f, 0.f, sdb, sdg, (float*)nullptr, (float*)nullptr, (const float*)nullptr, dgamma, dbeta,
-                     accumulate);
+                     accumulate, (int64_t*)nullptr);
   CAPK_LAUNCH_CHECK("bn_finish_kernel<2>");
   if (dx || dz_out) {
     const int64_t work = (int64_t)M * C / 8;

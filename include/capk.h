@@ -464,7 +464,9 @@ int capk_attention_probs_mean_bwd(int dtype, int B, int H, int Nq, int Nk, int h
  * capk_col2im: dx = beta*dx + the adjoint of capk_im2col (gather-sum, deterministic).
  * capk_bn_stats: training-mode nn.BatchNorm2d statistics over the M rows of [M, C]:
  *   mean, rstd = 1/sqrt(biased var + eps); running_mean/var (nullable) updated with
- *   `momentum` (running_var from the unbiased variance).  capk_bn_eval_stats: mean,
+ *   `momentum` (running_var from the unbiased variance), num_batches_tracked (nullable,
+ *   int64) += 1; one sweep over x: per-block sums and squared deviations about the block
+ *   mean, merged exactly (CAPK_BN_TWOPASS=1: two global passes).  capk_bn_eval_stats: mean,
  *   rstd from the running buffers (eval mode).
  * capk_bn_apply: y = [relu]((x - mean)*rstd*gamma + beta [+ residual]).
  * capk_bn_bwd: dz = dy * [y_mask > 0] (y_mask nullable: the ReLU output), dgamma,
@@ -485,7 +487,8 @@ int capk_col2im(int dtype, int B, int H, int W, int C, int KH, int KW, int strid
                 const void* dcol, void* dx, float beta, void* stream);
 size_t capk_bn_workspace(int M, int C);
 int capk_bn_stats(int dtype, int M, int C, const void* x, int64_t ldx, float eps, float momentum, float* mean,
-                  float* rstd, float* running_mean, float* running_var, void* ws, size_t ws_bytes, void* stream);
+                  float* rstd, float* running_mean, float* running_var, int64_t* num_batches_tracked, void* ws,
+                  size_t ws_bytes, void* stream);
 int capk_bn_eval_stats(int C, const float* running_mean, const float* running_var, float eps, float* mean,
                        float* rstd, void* stream);
 int capk_bn_apply(int dtype, int M, int C, const void* x, int64_t ldx, const float* mean, const float* rstd,

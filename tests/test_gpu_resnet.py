@@ -105,6 +105,30 @@ def test_batchnorm_train_fwd_bwd(ops, dtype, M, C):
 
 
 @cuda
+@pytest.mark.parametrize("M,C", [(401408, 64), (6272, 2048), (25088, 1024), (3, 4096)])
+def test_batchnorm_one_sweep_stats_vs_fp64(ops, M, C):
+    """capk_bn_stats' one sweep (per-block sums and squared deviations about the block mean,
+    merged exactly) against fp64 on offset data (mean 50, std 0.5: a sum-of-squares formula
+    would cancel), at ResNet-101 layer shapes (bs 128: 56x56x64, 7x7x2048, 14x14x1024 rows);
+    running statistics and num_batches_tracked as nn.BatchNorm2d."""
+    g = torch.Generator(device="cuda").manual_seed(7)
+    z = torch.randn(M, C, device="cuda", generator=g) * 0.5 + 50.0
+    rm = torch.zeros(C, device="cuda")
+    rv = torch.ones(C, device="cuda")
+    nbt = torch.tensor(5, dtype=torch.int64, device="cuda")
+    mean, rstd = ops.bn_stats(z, 1e-5, 0.1, rm, rv, nbt)
+    zd = z.double()
+    mu = zd.mean(0)
+    var = zd.var(0, unbiased=False)
+    assert _rel(mean, mu.float()) < 1e-6
+    assert _rel(rstd, (1.0 / torch.sqrt(var + 1e-5)).float()) < 1e-5
+    assert _rel(rm, (0.1 * mu).float()) < 1e-6
+    unb = zd.var(0, unbiased=True) if M > 1 else var
+    assert _rel(rv, (0.9 + 0.1 * unb).float()) < 1e-5
+    assert int(nbt) == 6
+
+
+@cuda
 def test_batchnorm_eval_stats(ops):
     g = torch.Generator(device="cuda").manual_seed(4)
     C, M = 128, 50
