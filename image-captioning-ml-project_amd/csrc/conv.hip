@@ -47,27 +47,38 @@ __global__ __launch_bounds__(256) void im2col_vec_kernel(int B, int H, int W, in
   }
 }
 
+// Strided / odd-C inputs (the stem: NCHW fp32 images, C = 3): eight consecutive k of one row
+// per thread -- one 16-B store, the row / tap decomposition done once and then stepped (the
+// per-element form spent its time in 64-bit divisions: ~1 ms for config 2's stem).
 template <typename TI, typename TO>
-__global__ __launch_bounds__(256) void im2col_scalar_kernel(int B, int H, int W, int C, int64_t sb, int64_t sh,
-                                                            int64_t sw, int64_t sc, int KH, int KW, int st, int pad,
-                                                            int OH, int OW, int Kp, const TI* __restrict__ x,
-                                                            TO* __restrict__ col) {
-  const int64_t total = (int64_t)B * OH * OW * Kp;
+__global__ __launch_bounds__(256) void im2col_gather8_kernel(int B, int H, int W, int C, int64_t sb, int64_t sh,
+                                                             int64_t sw, int64_t sc, int KH, int KW, int st, int pad,
+                                                             int OH, int OW, int Kp, const TI* __restrict__ x,
+                                                             TO* __restrict__ col) {
+  const int k8n = Kp / 8;
+  const int64_t total = (int64_t)B * OH * OW * k8n;
   const int Kr = KH * KW * C;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t m = i / Kp;
-    const int k = (int)(i % Kp);
-    float v = 0.f;
-    if (k < Kr) {
-      const int tap = k / C, c = k % C;
-      const int kh = tap / KW, kw = tap % KW;
-      const int ow = (int)(m % OW);
-      const int64_t t = m / OW;
-      const int oh = (int)(t % OH), b = (int)(t / OH);
-      const int ih = oh * st - pad + kh, iw = ow * st - pad + kw;
-      if (ih >= 0 && ih < H && iw >= 0 && iw < W) v = to_f32(x[b * sb + ih * sh + iw * sw + c * sc]);
+    const int64_t m = i / k8n;
+    const int k0 = (int)(i - m * k8n) * 8;
+    const int ow = (int)(m % OW);
+    const int64_t t = m / OW;
+    const int oh = (int)(t % OH), b = (int)(t / OH);
+    const int ih0 = oh * st - pad, iw0 = ow * st - pad;
+    const int tap = k0 / C;
+    int c = k0 - tap * C, kh = tap / KW, kw = tap - (tap / KW) * KW;
+    const TI* xb = x + b * sb;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int ih = ih0 + kh, iw = iw0 + kw;
+      v[j] = (k0 + j < Kr && ih >= 0 && ih < H && iw >= 0 && iw < W) ? to_f32(xb[ih * sh + iw * sw + c * sc]) : 0.f;
+      if (++c == C) {
+        c = 0;
+        if (++kw == KW) kw = 0, ++kh;
+      }
     }
-    col[i] = from_f32<TO>(v);
+    Vec8<TO>::store(col + m * Kp + k0, v);
   }
 }
 
@@ -583,8 +594,8 @@ extern "C" int capk_im2col(int in_dtype, int out_dtype, int B, int H, int W, int
       hipLaunchKernelGGL((im2col_vec_kernel<TI, TO>), dim3(grid_for(M * Kp / 8)), dim3(256), 0, st, B, H, W, C, sb, \
                          sh, sw, KH, KW, stride, pad, OH, OW, Kp, (const TI*)x, (TO*)col);                         \
     else                                                                                                           \
-      hipLaunchKernelGGL((im2col_scalar_kernel<TI, TO>), dim3(grid_for(M * Kp)), dim3(256), 0, st, B, H, W, C, sb, \
-                         sh, sw, sc, KH, KW, stride, pad, OH, OW, Kp, (const TI*)x, (TO*)col);                     \
+      hipLaunchKernelGGL((im2col_gather8_kernel<TI, TO>), dim3(grid_for(M * Kp / 8)), dim3(256), 0, st, B, H, W, C, \
+                         sb, sh, sw, sc, KH, KW, stride, pad, OH, OW, Kp, (const TI*)x, (TO*)col);               \
   } while (0)
   if (in_dtype == CAPK_F32 && out_dtype == CAPK_F32) GO(float, float);
   else if (in_dtype == CAPK_F32 && out_dtype == CAPK_BF16) GO(float, bf16);
