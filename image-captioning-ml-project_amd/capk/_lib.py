@@ -92,6 +92,9 @@ SIGNATURES = {
     "capk_lstm_cell_fwd": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _c_p, _c_p, _i64, _c_p, _i64, _c_p, _f, _u32, _c_p]),
     "capk_lstm_cell_bwd": (_i, [_i, _i, _i, _c_p, _c_p, _c_p, _i64, _c_p, _c_p, _c_p]),
     "capk_gemm_pair_workspace": (_sz, [_i, _i, _i, _c_p]),
+    "capk_gemm_slabs_workspace": (_sz, [_i, _i, _i, _c_p]),
+    "capk_layernorm_fwd_slabs": (_i, [_i, _i, _c_p, _i, _c_p, _c_p, _i64, _c_p, _i64, _c_p, _c_p, _f, _c_p, _i64,
+                                      _c_p]),
     "capk_gemm_pair_slabs": (_i, [_i, _i, _i, _c_p, _i64, _i, _c_p, _i64, _i, _c_p, _i64, _c_p, _i64, _i, _i, _c_p,
                                   _sz, _c_p, _c_p]),
     "capk_lstm_cell_fwd_slabs": (_i, [_i, _i, _c_p, _i, _i64, _c_p, _c_p, _c_p, _i64, _c_p, _c_p, _c_p, _i64, _c_p,

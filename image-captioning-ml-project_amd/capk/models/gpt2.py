@@ -378,10 +378,17 @@ class GPT2KVRunner:
             else:  # (the 10 prefix positions are the same row content for every beam of an image)
                 _history_reorder(self.hist, self.hist_tmp, reorder_idx, pos)
         x = ops.embedding_fwd(ids.view(R, 1), tr.wte.weight.detach(), tr.wpe.weight.detach(), pos, dt)
+        # the MLP projection of block l is summed by block l+1's ln_1 (ln_f after the last),
+        # the attention projection by ln_2 (ops.product_ln: split-K slabs read by the LayerNorm)
+        mlp_out = None  # (f, W, bias, residual) of the previous block's MLP projection
         for li, blk in enumerate(tr.h):
             at, mlp = blk.attn, blk.mlp
             cl = self.cache[li]
-            h1, _, _ = ops.layernorm_fwd(x, blk.ln_1.weight.detach(), blk.ln_1.bias.detach(), blk.ln_1.eps)
+            if mlp_out is None:
+                h1, _, _ = ops.layernorm_fwd(x, blk.ln_1.weight.detach(), blk.ln_1.bias.detach(), blk.ln_1.eps)
+            else:
+                h1, x = ops.product_ln(*mlp_out, blk.ln_1.weight.detach(), blk.ln_1.bias.detach(), blk.ln_1.eps,
+                                       keep=True)
             ops.conv1d(h1, W(at.c_attn.weight, dt), at.c_attn.bias.detach(), out=cl[:, pos, :])
             a = torch.empty(R, D, dtype=dt, device=x.device)
             qv, kv_, vv = HeadView(cl, pos * 3 * D, Lc3, 3 * D), HeadView(cl, D, Lc3, 3 * D), HeadView(cl, 2 * D, Lc3, 3 * D)
@@ -390,9 +397,9 @@ class GPT2KVRunner:
             else:
                 ops.attention_decode_rows(qv, kv_, vv, HeadView(a, 0, D, D), self.hist, R, H, 1, pos + 1, hd,
                                           self.scale)
-            x1 = ops.conv1d(a, W(at.c_proj.weight, dt), at.c_proj.bias.detach(), residual=x)
-            h2, _, _ = ops.layernorm_fwd(x1, blk.ln_2.weight.detach(), blk.ln_2.bias.detach(), blk.ln_2.eps)
+            h2, x1 = ops.product_ln(a, W(at.c_proj.weight, dt), True, at.c_proj.bias.detach(), x,
+                                    blk.ln_2.weight.detach(), blk.ln_2.bias.detach(), blk.ln_2.eps, keep=True)
             f = ops.conv1d(h2, W(mlp.c_fc.weight, dt), mlp.c_fc.bias.detach(), act=ACT_GELU_TANH)
-            x = ops.conv1d(f, W(mlp.c_proj.weight, dt), mlp.c_proj.bias.detach(), residual=x1)
-        xf, _, _ = ops.layernorm_fwd(x, tr.ln_f.weight.detach(), tr.ln_f.bias.detach(), tr.ln_f.eps)
+            mlp_out = (f, W(mlp.c_proj.weight, dt), True, mlp.c_proj.bias.detach(), x1)
+        xf, _ = ops.product_ln(*mlp_out, tr.ln_f.weight.detach(), tr.ln_f.bias.detach(), tr.ln_f.eps)
         return ops.linear(xf, self.wout, None)

@@ -411,17 +411,18 @@ class KVDecodeRunner:
             else:
                 ops.attention_decode_rows(qv, kv_, vv, HeadView(a, 0, D, D), self.hist, R, H, 1, t + 1, hd,
                                           self.scale)
-            s1 = ops.linear(a, W(sa.out_proj.weight, dt), sa.out_proj.bias.detach(), residual=x)
-            x1, _, _ = ops.layernorm_fwd(s1, L.norm1.weight.detach(), L.norm1.bias.detach(), L.norm1.eps)
+            # post-LN: each sublayer's output projection is summed by its LayerNorm (ops.product_ln)
+            x1, _ = ops.product_ln(a, W(sa.out_proj.weight, dt), False, sa.out_proj.bias.detach(), x,
+                                   L.norm1.weight.detach(), L.norm1.bias.detach(), L.norm1.eps)
             qc = ops.linear(x1, W(ca.in_proj_weight, dt)[:D], ca.in_proj_bias.detach()[:D])
             c = torch.empty(R, D, dtype=dt, device=x.device)
             kv = self.mem_kv[li]
             ops.attention_fwd(HeadView(qc, 0, k * D, D), HeadView(kv, 0, self.rpb * 2 * D, 2 * D),
                               HeadView(kv, D, self.rpb * 2 * D, 2 * D), HeadView(c, 0, k * D, D), self.B, H, k,
                               self.S, hd, self.scale)
-            s2 = ops.linear(c, W(ca.out_proj.weight, dt), ca.out_proj.bias.detach(), residual=x1)
-            x2, _, _ = ops.layernorm_fwd(s2, L.norm2.weight.detach(), L.norm2.bias.detach(), L.norm2.eps)
+            x2, _ = ops.product_ln(c, W(ca.out_proj.weight, dt), False, ca.out_proj.bias.detach(), x1,
+                                   L.norm2.weight.detach(), L.norm2.bias.detach(), L.norm2.eps)
             f = ops.linear(x2, W(L.linear1.weight, dt), L.linear1.bias.detach(), act=ACT_GELU_ERF)
-            s3 = ops.linear(f, W(L.linear2.weight, dt), L.linear2.bias.detach(), residual=x2)
-            x, _, _ = ops.layernorm_fwd(s3, L.norm3.weight.detach(), L.norm3.bias.detach(), L.norm3.eps)
+            x, _ = ops.product_ln(f, W(L.linear2.weight, dt), False, L.linear2.bias.detach(), x2,
+                                  L.norm3.weight.detach(), L.norm3.bias.detach(), L.norm3.eps)
         return ops.linear(x, self.wout, self.bout)

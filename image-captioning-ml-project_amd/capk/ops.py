@@ -689,6 +689,36 @@ def gemm_pair_slabs(M, N, K, A, lda, B, ldb, b_kmajor, ws, *, A2=None, lda2=0, B
     return s.value
 
 
+# Decode steps: a GEMM whose output only feeds a LayerNorm (and the residual stream) writes
+# split-K slabs that the LayerNorm sums (capk_layernorm_fwd_slabs), bit-identical to the
+# product + reduce + LayerNorm launches it replaces.  CAPK_DECODE_SLABS=0: the separate route.
+DECODE_SLABS = os.environ.get("CAPK_DECODE_SLABS", "1") != "0"
+
+
+def product_ln(x, w, conv1d_weight, b, residual, ln_w, ln_b, eps, *, keep=False):
+    """(LayerNorm(s), s or None) for s = x W^T + b + residual (nn.Linear weight [out, in]) or
+    x W + b + residual (conv1d_weight: HF Conv1D [in, out]); s is materialised only with keep
+    (the pre-LN residual stream).  Products that take the fp8 route, non-bf16 inputs and
+    shapes outside the slab kernel's K % 64 take the separate launches."""
+    M, K = x.shape
+    N = w.shape[1] if conv1d_weight else w.shape[0]
+    if (not DECODE_SLABS or x.dtype != torch.bfloat16 or K % 64 or N % 8 or N > 2048 or x.stride(0) % 8
+            or _fp8_route(x, w, M, N, K, 0, conv1d_weight) is not None):
+        s = (conv1d if conv1d_weight else linear)(x, w, b, residual=residual)
+        return layernorm_fwd(s, ln_w, ln_b, eps)[0], s
+    L = lib()
+    sp = ctypes.c_int(0)
+    ws = torch.empty(L.capk_gemm_slabs_workspace(M, N, K, ctypes.byref(sp)) // 4, dtype=torch.float32,
+                     device=x.device)
+    splits = gemm_pair_slabs(M, N, K, x, x.stride(0), w, w.stride(0), not conv1d_weight, ws)
+    y = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    s = torch.empty(M, N, dtype=x.dtype, device=x.device) if keep else None
+    check(L.capk_layernorm_fwd_slabs(M, N, _p(ws), splits, _p(b), _p(residual),
+                                     residual.stride(0) if residual is not None else 0, _p(s), N, _p(ln_w), _p(ln_b),
+                                     float(eps), _p(y), N, _stream()), "capk_layernorm_fwd_slabs")
+    return y, s
+
+
 def lstm_cell_fwd_slabs(ws, splits, ldw, bias_a, bias_b, res, c_prev, c_out, h_out, act, h_drop=None, drop=NO_DROP):
     B, D = c_prev.shape
     check(lib().capk_lstm_cell_fwd_slabs(B, D, _p(ws), int(splits), ldw, _p(bias_a), _p(bias_b), _p(res),

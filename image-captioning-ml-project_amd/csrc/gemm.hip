@@ -578,19 +578,29 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
 // consumers (the cell kernels, lstm.hip) sum the slabs themselves -- one launch per step and
 // layer in place of two GEMMs and two split-K reduces.  128x128 ring tiles; splits so that
 // about one round of WGs runs, every split >= CAPK_PAIR_MINKT (4) K-tiles.
-static int pair_splits(int M, int N, int K) {
+// A single product (no seam: the decode steps' GEMM -> LayerNorm pairs) takes capk_gemm's
+// own split count for the 128x128 ring, so the slabs -- and the sums of their consumers --
+// are bit-identical to capk_gemm + splitk_reduce.
+static int pair_splits(int M, int N, int K, bool seam) {
   static const int min_kt = [] {
     const char* v = getenv("CAPK_PAIR_MINKT");
     return v ? std::max(1, atoi(v)) : 4;
   }();
   const int tiles = cdiv(M, 128) * cdiv(N, BN), nk = cdiv(K, 64);
-  const int s = std::max(1, std::min(256 / tiles, nk / min_kt));
+  const int s = seam ? std::max(1, std::min(256 / tiles, nk / min_kt)) : choose_splits(1, M, N, K);
   return cdiv(nk, cdiv(nk, s));  // effective count: every split owns >= 1 K-tile
 }
 
 extern "C" size_t capk_gemm_pair_workspace(int M, int N, int K, int* splits) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
-  const int s = pair_splits(M, N, K);
+  const int s = pair_splits(M, N, K, true);
+  if (splits) *splits = s;
+  return (size_t)s * M * N * sizeof(float);
+}
+
+extern "C" size_t capk_gemm_slabs_workspace(int M, int N, int K, int* splits) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  const int s = pair_splits(M, N, K, false);
   if (splits) *splits = s;
   return (size_t)s * M * N * sizeof(float);
 }
@@ -599,8 +609,9 @@ extern "C" int capk_gemm_pair_slabs(int M, int N, int K, const void* A, int64_t 
                                     int64_t ldb, int b_kmajor, const void* A2, int64_t lda2, const void* B2,
                                     int64_t ldb2, int k1, int n1, float* ws, size_t ws_bytes, int* splits_out,
                                     void* stream) {
-  CAPK_CHECK_ARG(M > 0 && N > 0 && K > 0 && A && B && B2 && ws, "capk_gemm_pair_slabs: bad arguments");
-  CAPK_CHECK_ARG((k1 > 0) != (n1 > 0), "capk_gemm_pair_slabs: exactly one of k1 (K seam) / n1 (N seam)");
+  CAPK_CHECK_ARG(M > 0 && N > 0 && K > 0 && A && B && ws && (k1 == 0 && n1 == 0 || B2),
+                 "capk_gemm_pair_slabs: bad arguments");
+  CAPK_CHECK_ARG(!(k1 > 0 && n1 > 0), "capk_gemm_pair_slabs: at most one of k1 (K seam) / n1 (N seam)");
   CAPK_CHECK_ARG(a_kmajor, "capk_gemm_pair_slabs: A must be K-major");
   CAPK_CHECK_ARG(k1 == 0 || (A2 && b_kmajor && k1 % 64 == 0 && (K - k1) % 64 == 0 && k1 < K),
                  "capk_gemm_pair_slabs: K seam k1=%d needs K-major A2/B2 and k1, K-k1 multiples of 64", k1);
@@ -608,11 +619,11 @@ extern "C" int capk_gemm_pair_slabs(int M, int N, int K, const void* A, int64_t 
                  n1, BN);
   CAPK_CHECK_ARG(K % 64 == 0 && N % 8 == 0, "capk_gemm_pair_slabs: K=%d %% 64, N=%d %% 8", K, N);
   CAPK_CHECK_ARG(b_kmajor || (int64_t)K * std::max(ldb, ldb2) * 2 < (1ll << 31), "capk_gemm_pair_slabs: B too large");
-  CAPK_CHECK_ARG(((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && ((uintptr_t)B2 % 16 == 0) &&
+  CAPK_CHECK_ARG(((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && ((uintptr_t)B2 % 16 == 0) &&  // (null passes)
                      (!A2 || (uintptr_t)A2 % 16 == 0) && lda % 8 == 0 && ldb % 8 == 0 && lda2 % 8 == 0 &&
                      ldb2 % 8 == 0,
                  "capk_gemm_pair_slabs: operands must be 16-B aligned with leading dimensions %% 8 == 0");
-  const int splits = pair_splits(M, N, K);
+  const int splits = pair_splits(M, N, K, k1 > 0 || n1 > 0);
   CAPK_CHECK_ARG(ws_bytes >= (size_t)splits * M * N * sizeof(float), "capk_gemm_pair_slabs: workspace too small");
   Epi e{nullptr, N, 1.f, 0.f, nullptr, nullptr, 0, 0, nullptr, nullptr, 0, M, N, make_drop(0.f, 0)};
   const Seg2 g2{(const bf16*)A2, lda2, (const bf16*)B2, ldb2, k1, n1};

@@ -58,6 +58,87 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int cols, const T
   }
 }
 
+// LayerNorm of x = bf16(sum_s slab[s] + bias + res), the decode steps' GEMM -> LayerNorm pairs
+// (capk_gemm_pair_slabs with no seam writes the slabs): the slab sum, bias and residual in
+// splitk_reduce / epilogue8 order and the statistics in ln_fwd_kernel's order, so y (and x,
+// kept in x_out for the pre-LN residual stream) are bit-identical to capk_gemm followed by
+// capk_layernorm_fwd -- one launch instead of a reduce and a LayerNorm.
+template <int MAXC>
+__global__ __launch_bounds__(256) void ln_fwd_slabs_kernel(int rows, int cols, const float* __restrict__ ws,
+                                                           int splits, const float* __restrict__ bias,
+                                                           const bf16* __restrict__ res, int64_t ldr,
+                                                           bf16* __restrict__ x_out, int64_t ldxo,
+                                                           const float* __restrict__ w, const float* __restrict__ b,
+                                                           float eps, bf16* __restrict__ y, int64_t ldy) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nch = cols >> 3;
+  const int64_t ss = (int64_t)rows * cols;
+  float v[MAXC][8];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      const float* p = ws + (int64_t)row * cols + ch * 8;
+      for (int k = 0; k < splits; ++k, p += ss) {
+        float t[8];
+        Vec8<float>::load(p, t);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] += t[i];
+      }
+      if (bias) {
+        float bb[8];
+        Vec8<float>::load(bias + ch * 8, bb);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] += bb[i];
+      }
+      if (res) {
+        float r[8];
+        Vec8<bf16>::load(res + (int64_t)row * ldr + ch * 8, r);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] += r[i];
+      }
+      bf16x8 hx;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) hx[i] = (bf16)a[i];
+      if (x_out) *(bf16x8*)(x_out + (int64_t)row * ldxo + ch * 8) = hx;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        v[c][i] = (float)hx[i];
+        s += v[c][i];
+      }
+    }
+  }
+  const float mean = wave_sum(s) / cols;
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { const float d = v[c][i] - mean; q += d * d; }
+    }
+  }
+  const float var = wave_sum(q) / cols;
+  const float rstd = rsqrtf(var + eps);
+  bf16* yr = y + (int64_t)row * ldy;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      float wv[8], bv[8], o[8];
+      Vec8<float>::load(w + ch * 8, wv);
+      Vec8<float>::load(b + ch * 8, bv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (v[c][i] - mean) * rstd * wv[i] + bv[i];
+      Vec8<bf16>::store(yr + ch * 8, o);
+    }
+  }
+}
+
 // Raw 8-element row segment kept in registers between its load and its use (the row loop
 // is software-pipelined: the next row's operands are in flight while this row reduces).
 template <typename T> struct Seg8;
@@ -332,6 +413,23 @@ extern "C" int capk_layernorm_fwd(int dtype, int rows, int cols, const void* x, 
   else { set_error("capk_layernorm_fwd: dtype"); return CAPK_EINVAL; }
 #undef L
   CAPK_LAUNCH_CHECK("ln_fwd_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_layernorm_fwd_slabs(int rows, int cols, const float* ws, int splits, const float* bias,
+                                        const void* res, int64_t ldr, void* x_out, int64_t ldxo, const float* w,
+                                        const float* b, float eps, void* y, int64_t ldy, void* stream) {
+  CAPK_CHECK_ARG(rows > 0 && cols > 0 && cols % 8 == 0 && cols <= 2048 && ws && splits > 0 && w && b && y,
+                 "capk_layernorm_fwd_slabs: bad arguments (cols=%d)", cols);
+  CAPK_CHECK_ARG(ldy % 8 == 0 && (!res || ldr % 8 == 0) && (!x_out || ldxo % 8 == 0),
+                 "capk_layernorm_fwd_slabs: strides must be multiples of 8");
+  const dim3 grid(cdiv(rows, 4)), block(256);
+#define L(MC)                                                                                                   \
+  hipLaunchKernelGGL((ln_fwd_slabs_kernel<MC>), grid, block, 0, S(stream), rows, cols, ws, splits, bias,      \
+                     (const bf16*)res, ldr, (bf16*)x_out, ldxo, w, b, eps, (bf16*)y, ldy)
+  if (cols <= 1024) L(2); else L(4);
+#undef L
+  CAPK_LAUNCH_CHECK("ln_fwd_slabs_kernel");
   return CAPK_OK;
 }
 

@@ -101,6 +101,10 @@ int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K,
  *   A K-major.  Slab s = ws + s*M*N ([M][N] fp32), s < *splits_out; capk_gemm_pair_workspace
  *   returns the bytes and the split count for (M, N, K). */
 size_t capk_gemm_pair_workspace(int M, int N, int K, int* splits);
+/* The same entry with k1 = n1 = 0 (A2 / B2 unused) is a plain product C = A B^T whose split
+ * count is capk_gemm's own for the shape (capk_gemm_slabs_workspace): its slabs, summed in
+ * order, are bit-identical to capk_gemm's split-K partials (consumer: capk_layernorm_fwd_slabs). */
+size_t capk_gemm_slabs_workspace(int M, int N, int K, int* splits);
 int capk_gemm_pair_slabs(int M, int N, int K, const void* A, int64_t lda, int a_kmajor, const void* B, int64_t ldb,
                          int b_kmajor, const void* A2, int64_t lda2, const void* B2, int64_t ldb2, int k1, int n1,
                          float* ws, size_t ws_bytes, int* splits_out, void* stream);
@@ -138,6 +142,14 @@ int capk_gemm_f8(int out_dtype, int M, int N, int K, const void* A, int64_t lda,
 int capk_layernorm_fwd(int dtype, int rows, int cols, const void* x, int64_t ldx,
                        const float* w, const float* b, float eps,
                        void* y, int64_t ldy, float* mean, float* rstd, void* stream);
+/* y = LayerNorm(x), x = bf16(sum_s ws[s] + bias + res) from the no-seam slabs of
+ * capk_gemm_pair_slabs ([rows][cols] fp32 each, in order); x_out (optional) keeps x.  bf16,
+ * bit-identical to capk_gemm (+ bias + residual) followed by capk_layernorm_fwd: the decode
+ * steps' out-projection / MLP-projection -> LayerNorm pairs (GPT-2 modeling_gpt2.py:
+ * 324-331,397-409 / nn.TransformerDecoderLayer norm1..3) in one launch after the GEMM. */
+int capk_layernorm_fwd_slabs(int rows, int cols, const float* ws, int splits, const float* bias, const void* res,
+                             int64_t ldr, void* x_out, int64_t ldxo, const float* w, const float* b, float eps,
+                             void* y, int64_t ldy, void* stream);
 /* dx = LN'(dy) (+ dres if non-NULL); dw/db (fp32 [cols]) = sum over rows
  * (accumulate into existing dw/db when accumulate != 0); dsum (optional, fp32 [cols])
  * (+)= the column sums of dx -- the bias gradient of the Linear whose output gradient dx

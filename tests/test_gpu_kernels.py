@@ -701,3 +701,36 @@ def test_gemm_timer_follows_the_stream(ops):
         ops.GEMM_TIMER.stride = stride
     sm = ops.GEMM_TIMER.summary()
     assert sm["launches"] == 3 and sm["launches_seen"] == 6
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+@pytest.mark.parametrize("M,K,N,conv", [(256, 768, 768, True), (256, 3072, 768, True), (1024, 3072, 768, True),
+                                        (1280, 768, 768, False), (1280, 3072, 768, False), (40, 512, 512, False)])
+def test_product_ln_slabs_bit_identical(M, K, N, conv):
+    """ops.product_ln (split-K slabs summed by capk_layernorm_fwd_slabs) against the separate
+    route (capk_gemm + bias + residual, then capk_layernorm_fwd): LayerNorm output and the
+    kept pre-LN sum bit-identical, for the GPT-2 Conv1D [in, out] and nn.Linear [out, in]
+    weights of the decode steps (split and unsplit shapes)."""
+    from capk import ops
+    g = torch.Generator(device="cuda").manual_seed(M + K)
+    bf = torch.bfloat16
+    x = torch.randn(M, K, device="cuda", generator=g).to(bf)
+    w = (torch.randn(K, N, device="cuda", generator=g) if conv else torch.randn(N, K, device="cuda", generator=g))
+    w = (w / K ** 0.5).to(bf)
+    b = torch.randn(N, device="cuda", generator=g)
+    res = torch.randn(M, N, device="cuda", generator=g).to(bf)
+    lw, lb = torch.rand(N, device="cuda", generator=g) + 0.5, torch.randn(N, device="cuda", generator=g)
+    saved = ops.DECODE_SLABS
+    try:
+        ops.DECODE_SLABS = True
+        y1, s1 = ops.product_ln(x, w, conv, b, res, lw, lb, 1e-5, keep=True)
+        ops.DECODE_SLABS = False
+        y0, s0 = ops.product_ln(x, w, conv, b, res, lw, lb, 1e-5, keep=True)
+    finally:
+        ops.DECODE_SLABS = saved
+    assert torch.equal(s1, s0)
+    assert torch.equal(y1, y0)
+    ref = torch.nn.functional.layer_norm((x.float() @ (w.float() if conv else w.float().t())) + b + res.float(),
+                                         (N,), lw, lb, 1e-5)
+    assert float((y1.float() - ref).norm() / ref.norm()) < 2e-2
