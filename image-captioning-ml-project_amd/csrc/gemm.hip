@@ -349,6 +349,18 @@ static int choose_cfg(int M, int N, int K, int a_kmajor, int b_kmajor, int act) 
   if ((o == 2 || big_tile(o)) && M < 256) o = 1;
   if ((o == 3 || o == 4) && (a_kmajor || b_kmajor) && K % 32) o = 1;
   if (o >= 1 && o <= 6) return o;
+  // Huge-M products with a short K (ResNet layer-1 convolutions at bs 128: M = 401 408 rows of
+  // 56x56; the 1x1 expansion forward and backward-data and the 3x3 dcol have K = 64): with one
+  // K-tile per item the 256x256 kernels are store-bound at one WG per CU and the 3-WG/CU BK-32
+  // ring measured 3.5-4.3x faster; on that layer's N <= 128, K <= 1024 products it is 7-13 %
+  // faster than the 2-WG/CU ring (graph-replayed, profiles/round4/conv_shapes.txt).
+  static const bool short_k = [] {  // CAPK_GEMM_SHORTK=0: without this rule (A/B)
+    const char* v = getenv("CAPK_GEMM_SHORTK");
+    return !(v && v[0] == '0');
+  }();
+  if (short_k && a_kmajor && K % 32 == 0 &&
+      ((K <= 64 && (int64_t)cdiv(M, 128) * cdiv(N, BN) >= 1024) || (M >= 65536 && N <= 128 && K <= 1024)))
+    return 4;
   // the 256x256 phased kernel (gemm8p.hip) whenever its grid (x split-K for the weight
   // gradients) fills most of the chip: measured faster than the 128-row tiles on every
   // config-3 shape of that size (tools/gemm_bench.py, profiles/round2/)
