@@ -403,7 +403,10 @@ static int choose_splits(int cfg, int M, int N, int K) {
   // grid fill the chip only with more than 16 splits (each split still >= 4 K-tiles)
   // (K >= 16384: the ViT O-projection weight gradient, 768 x 768 = 9 tiles, fills 252 CUs
   // with 28 splits instead of 144 with 16)
-  const int max_split = max_split_env ? max_split_env : (K >= 65536 ? 64 : K >= 16384 ? 32 : 16);
+  // (K >= 262144: ResNet layer-1 / stem weight gradients, 2-tile grids over 4e5-1.6e6 rows,
+  // fill the chip with 128 splits instead of half of it with 64)
+  const int max_split = max_split_env ? max_split_env
+                                      : (K >= 262144 ? 128 : K >= 65536 ? 64 : K >= 16384 ? 32 : 16);
   const int bk = (cfg == 3 || cfg == 4) ? 32 : 64;
   const int tiles = tiles_of(cfg, M, N), slots = slots_of(cfg);
   const int nk = cdiv(K, bk);
