@@ -137,8 +137,8 @@ SIGNATURES = {
     "capk_bn_stats": (_i, [_i, _i, _i, _c_p, _i64, _f, _f, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _sz, _c_p]),
     "capk_bn_eval_stats": (_i, [_i, _c_p, _c_p, _f, _c_p, _c_p, _c_p]),
     "capk_bn_apply": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _c_p, _c_p, _c_p, _c_p, _i64, _i, _c_p, _i64, _c_p]),
-    "capk_bn_bwd": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p, _i64, _c_p, _c_p, _c_p, _c_p, _c_p, _i, _c_p, _i64,
-                         _f, _c_p, _i64, _i, _c_p, _sz, _c_p]),
+    "capk_bn_bwd": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p, _i64, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _i, _c_p,
+                         _i64, _f, _c_p, _i64, _i, _c_p, _sz, _c_p]),
     "capk_maxpool_fwd": (_i, [_i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _c_p, _c_p, _c_p, _c_p]),
     "capk_maxpool_bwd": (_i, [_i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _c_p, _c_p, _c_p, _c_p]),
     "capk_avgpool_fwd": (_i, [_i, _i, _i, _i, _i, _i, _i, _c_p, _c_p, _i64, _c_p]),

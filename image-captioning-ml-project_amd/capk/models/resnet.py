@@ -22,6 +22,8 @@ in (kh, kw, cin) order, zero-padded to Kp = roundup(KH*KW*Cin, 64) for the MFMA
 K tiles; ``conv.weight`` is a strided ``[Cout, Cin, KH, KW]`` view of that block,
 so state dicts keep PyTorch's layout.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -107,6 +109,11 @@ def conv_bwd(conv, dz, col, B, H, W, dt, *, need_dx=True, dx=None, beta=0.0):
     return dx
 
 
+# bottleneck BatchNorms followed directly by their ReLU: backward recomputes the ReLU mask from
+# z (already read) instead of re-reading y -- CAPK_BN_OWN_RELU=0 re-reads y (A/B)
+_OWN_RELU = os.environ.get("CAPK_BN_OWN_RELU", "1") != "0"
+
+
 def bn_fwd(bn, z, training, *, residual=None, relu=True):
     """nn.BatchNorm2d (+ residual) (+ ReLU) on channels-last rows; returns (y, mean, rstd)."""
     if training:
@@ -120,11 +127,13 @@ def bn_fwd(bn, z, training, *, residual=None, relu=True):
     return y, mean, rstd
 
 
-def bn_bwd(bn, dy, z, mean, rstd, training, *, y_mask=None, dx=None, dz_out=None):
+def bn_bwd(bn, dy, z, mean, rstd, training, *, y_mask=None, own_relu=False, dx=None, dz_out=None):
+    """own_relu: the ReLU mask is that of this BatchNorm's own output (no residual in
+    between), recomputed from z in the kernels instead of re-reading y."""
     if dx is None:
         dx = torch.empty_like(z)
     ops.bn_bwd(dy, z, mean, rstd, bn.weight.detach(), bn.weight._capk_grad, bn.bias._capk_grad, y_mask=y_mask,
-               dx=dx, dz_out=dz_out, batch_stats=training)
+               dx=dx, dz_out=dz_out, batch_stats=training, relu_beta=bn.bias.detach() if own_relu else None)
     return dx
 
 
@@ -338,9 +347,9 @@ class _BottleneckFn(torch.autograd.Function):
             dzs = bn_bwd(ns, dout, zs, mus, rss, tr, y_mask=out)
             dx = conv_bwd(ks, dzs, cols, B, H, W, dt)
         dy2 = conv_bwd(k3, dz3, y2, B, H2, W2, dt)
-        dz2 = bn_bwd(n2, dy2, z2, mu2, rs2, tr, y_mask=y2, dx=dy2)
+        dz2 = bn_bwd(n2, dy2, z2, mu2, rs2, tr, own_relu=_OWN_RELU, y_mask=None if _OWN_RELU else y2, dx=dy2)
         dy1 = conv_bwd(k2, dz2, col2, B, H1, W1, dt)
-        dz1 = bn_bwd(n1, dy1, z1, mu1, rs1, tr, y_mask=y1, dx=dy1)
+        dz1 = bn_bwd(n1, dy1, z1, mu1, rs1, tr, own_relu=_OWN_RELU, y_mask=None if _OWN_RELU else y1, dx=dy1)
         conv_bwd(k1, dz1, col1, B, H, W, dt, dx=dx, beta=1.0)
         return dx, None, None, None, None, None
 

@@ -893,16 +893,18 @@ def bn_apply(x, mean, rstd, gamma, beta, *, residual=None, relu=False, out=None)
 
 
 def bn_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, *, y_mask=None, dx=None, beta_acc=0.0, dz_out=None,
-           accumulate=False, batch_stats=True):
+           accumulate=False, batch_stats=True, relu_beta=None):
     """BatchNorm backward (training statistics): dgamma/dbeta written (or added), dx
-    (optional, += with beta_acc), dz_out (optional) = dy * [y_mask > 0]."""
+    (optional, += with beta_acc), dz_out (optional) = dy * [y_mask > 0]; relu_beta (the
+    BatchNorm's beta) instead of y_mask: the mask of its own ReLU output, recomputed from x."""
     L = lib()
     M, C = x.shape
     wsb = L.capk_bn_workspace(M, C)
     ws = _ws(wsb, x.device)
     check(L.capk_bn_bwd(dtype_code(x), M, C, _p(dy), dy.stride(0), _p(y_mask),
                         y_mask.stride(0) if y_mask is not None else 0, _p(x), x.stride(0), _p(mean), _p(rstd),
-                        _p(gamma), _p(dgamma), _p(dbeta), int(accumulate), _p(dx), dx.stride(0) if dx is not None else 0,
+                        _p(gamma), _p(relu_beta), _p(dgamma), _p(dbeta), int(accumulate), _p(dx),
+                        dx.stride(0) if dx is not None else 0,
                         float(beta_acc), _p(dz_out), dz_out.stride(0) if dz_out is not None else 0,
                         int(batch_stats), _p(ws), wsb,
                         _stream()), "capk_bn_bwd")

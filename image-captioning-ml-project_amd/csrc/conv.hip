@@ -140,7 +140,8 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(int M, int C, int rows_p
                                                         int64_t ldx, const T* __restrict__ dy, int64_t lddy,
                                                         const T* __restrict__ ym, int64_t ldym,
                                                         const float* __restrict__ mean,
-                                                        const float* __restrict__ rstd, float* __restrict__ part) {
+                                                        const float* __restrict__ rstd, float* __restrict__ part,
+                                                        const float* __restrict__ mg, const float* __restrict__ mb) {
   constexpr int NACC = MODE >= 2 ? 2 : 1;
   __shared__ float red[NACC][256 * 8];
   const int cpb = C < BN_MAX_CPB ? C : BN_MAX_CPB;
@@ -155,6 +156,8 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(int M, int C, int rows_p
     if (MODE == 3) Vec8<T>::load(x + (int64_t)m0 * ldx + c, mu);  // the shift K
     if (MODE == 1 || MODE == 2) Vec8<float>::load(mean + c, mu);
     if (MODE == 2) Vec8<float>::load(rstd + c, rs);
+    float mgv[8], mbv[8];
+    if (MODE == 2 && mb) Vec8<float>::load(mg + c, mgv), Vec8<float>::load(mb + c, mbv);
     for (int m = m0 + r0; m < m1; m += rg) {
       float v[8];
       Vec8<T>::load(x + (int64_t)m * ldx + c, v);
@@ -175,6 +178,9 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(int M, int C, int rows_p
           Vec8<T>::load(ym + (int64_t)m * ldym + c, y);
 #pragma unroll
           for (int j = 0; j < 8; ++j) g[j] = y[j] > 0.f ? g[j] : 0.f;
+        } else if (mb) {  // ReLU mask of this BatchNorm's own output, recomputed from x
+#pragma unroll
+          for (int j = 0; j < 8; ++j) g[j] = (v[j] - mu[j]) * rs[j] * mgv[j] + mbv[j] > 0.f ? g[j] : 0.f;
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -363,7 +369,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(int M, int C, const T
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ sdb, const float* __restrict__ sdg,
                                                            T* __restrict__ dx, int64_t lddx, float beta_acc,
-                                                           T* __restrict__ dz_out, int64_t lddz, int batch_stats) {
+                                                           T* __restrict__ dz_out, int64_t lddz, int batch_stats,
+                                                           const float* __restrict__ mb) {
   const int c8n = C / 8;
   const int64_t total = (int64_t)M * c8n;
   const float invM = 1.0f / (float)M;
@@ -372,18 +379,26 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(int M, int C, const T
     const int c = (int)(i % c8n) * 8;
     float g[8], v[8], mu[8], rs[8], ga[8], db[8], dg[8];
     Vec8<T>::load(dy + m * lddy + c, g);
+    const bool need_x = dx || mb;
+    if (need_x) {
+      Vec8<T>::load(x + m * ldx + c, v);
+      Vec8<float>::load(mean + c, mu);
+      Vec8<float>::load(rstd + c, rs);
+      Vec8<float>::load(gamma + c, ga);
+    }
     if (ym) {
       float y[8];
       Vec8<T>::load(ym + m * ldym + c, y);
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = y[j] > 0.f ? g[j] : 0.f;
+    } else if (mb) {  // ReLU mask of this BatchNorm's own output (bn_apply's expression), from x
+      float bb[8];
+      Vec8<float>::load(mb + c, bb);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = (v[j] - mu[j]) * rs[j] * ga[j] + bb[j] > 0.f ? g[j] : 0.f;
     }
     if (dz_out) Vec8<T>::store(dz_out + m * lddz + c, g);
     if (!dx) continue;
-    Vec8<T>::load(x + m * ldx + c, v);
-    Vec8<float>::load(mean + c, mu);
-    Vec8<float>::load(rstd + c, rs);
-    Vec8<float>::load(gamma + c, ga);
     Vec8<float>::load(sdb + c, db);
     Vec8<float>::load(sdg + c, dg);
     float o[8];
@@ -638,7 +653,8 @@ extern "C" int capk_bn_stats(int dtype, int M, int C, const void* x, int64_t ldx
   dim3 grid(g.col_blocks, g.splits);
 #define L(T, MODE)                                                                                                \
   hipLaunchKernelGGL((bn_reduce_kernel<T, MODE>), grid, dim3(256), 0, st, M, C, g.rps, (const T*)x, ldx,         \
-                     (const T*)nullptr, (int64_t)0, (const T*)nullptr, (int64_t)0, (const float*)mean, (const float*)rstd, part)
+                     (const T*)nullptr, (int64_t)0, (const T*)nullptr, (int64_t)0, (const float*)mean, (const float*)rstd, part, \
+                     (const float*)nullptr, (const float*)nullptr)
   // one sweep (shifted per-block sums, merged exactly) unless CAPK_BN_TWOPASS=1 (the global two-pass A/B)
   static const bool two_pass = [] {
     const char* v = getenv("CAPK_BN_TWOPASS");
@@ -693,8 +709,10 @@ extern "C" int capk_bn_apply(int dtype, int M, int C, const void* x, int64_t ldx
 
 extern "C" int capk_bn_bwd(int dtype, int M, int C, const void* dy, int64_t lddy, const void* y_mask, int64_t ldym,
                            const void* x, int64_t ldx, const float* mean, const float* rstd, const float* gamma,
-                           float* dgamma, float* dbeta, int accumulate, void* dx, int64_t lddx, float beta_acc,
-                           void* dz_out, int64_t lddz, int batch_stats, void* ws, size_t ws_bytes, void* stream) {
+                           const float* relu_beta, float* dgamma, float* dbeta, int accumulate, void* dx,
+                           int64_t lddx, float beta_acc, void* dz_out, int64_t lddz, int batch_stats, void* ws,
+                           size_t ws_bytes, void* stream) {
+  CAPK_CHECK_ARG(!(y_mask && relu_beta), "capk_bn_bwd: y_mask and relu_beta are exclusive");
   CAPK_CHECK_ARG(M > 0 && bn_shape_ok(C) && lddy % 8 == 0 && ldx % 8 == 0, "capk_bn_bwd: bad shape M=%d C=%d", M, C);
   CAPK_CHECK_ARG(ws && ws_bytes >= capk_bn_workspace(M, C), "capk_bn_bwd: workspace too small");
   const BnGeom g = bn_geom(M, C);
@@ -705,7 +723,7 @@ extern "C" int capk_bn_bwd(int dtype, int M, int C, const void* dy, int64_t lddy
   dim3 grid(g.col_blocks, g.splits);
 #define L(T, _)                                                                                                   \
   hipLaunchKernelGGL((bn_reduce_kernel<T, 2>), grid, dim3(256), 0, st, M, C, g.rps, (const T*)x, ldx, (const T*)dy, \
-                     lddy, (const T*)y_mask, ldym, mean, rstd, part)
+                     lddy, (const T*)y_mask, ldym, mean, rstd, part, relu_beta ? gamma : nullptr, relu_beta)
   DT_DISPATCH(dtype, L, 0)
 #undef L
   CAPK_LAUNCH_CHECK("bn_reduce_kernel<2>");
@@ -718,7 +736,7 @@ extern "C" int capk_bn_bwd(int dtype, int M, int C, const void* dy, int64_t lddy
 #define L(T, _)                                                                                                      \
   hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(work)), dim3(256), 0, st, M, C, (const T*)dy, lddy,     \
                      (const T*)y_mask, ldym, (const T*)x, ldx, mean, rstd, gamma, (const float*)sdb,                \
-                     (const float*)sdg, (T*)dx, lddx, beta_acc, (T*)dz_out, lddz, batch_stats)
+                     (const float*)sdg, (T*)dx, lddx, beta_acc, (T*)dz_out, lddz, batch_stats, relu_beta)
     DT_DISPATCH(dtype, L, 0)
 #undef L
     CAPK_LAUNCH_CHECK("bn_bwd_apply_kernel");

@@ -404,9 +404,11 @@ static int choose_splits(int cfg, int M, int N, int K) {
   // (K >= 16384: the ViT O-projection weight gradient, 768 x 768 = 9 tiles, fills 252 CUs
   // with 28 splits instead of 144 with 16)
   // (K >= 262144: ResNet layer-1 / stem weight gradients, 2-tile grids over 4e5-1.6e6 rows,
-  // fill the chip with 128 splits instead of half of it with 64)
+  // fill the chip with 128 splits instead of half of it with 64; the stem's 1.6e6 rows take
+  // 256: 275 -> 216 us, while 256 on the 4e5-row ones lost, 89 -> 108 us)
   const int max_split = max_split_env ? max_split_env
-                                      : (K >= 262144 ? 128 : K >= 65536 ? 64 : K >= 16384 ? 32 : 16);
+                                      : (K >= 1048576 ? 256 : K >= 262144 ? 128 : K >= 65536 ? 64
+                                         : K >= 16384 ? 32 : 16);
   const int bk = (cfg == 3 || cfg == 4) ? 32 : 64;
   const int tiles = tiles_of(cfg, M, N), slots = slots_of(cfg);
   const int nk = cdiv(K, bk);

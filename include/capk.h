@@ -481,7 +481,9 @@ int capk_attention_probs_mean_bwd(int dtype, int B, int H, int Nq, int Nk, int h
  *   mean, merged exactly (CAPK_BN_TWOPASS=1: two global passes).  capk_bn_eval_stats: mean,
  *   rstd from the running buffers (eval mode).
  * capk_bn_apply: y = [relu]((x - mean)*rstd*gamma + beta [+ residual]).
- * capk_bn_bwd: dz = dy * [y_mask > 0] (y_mask nullable: the ReLU output), dgamma,
+ * capk_bn_bwd: dz = dy * [y_mask > 0] (y_mask nullable: the ReLU output; or, with relu_beta
+ *   (the BatchNorm's beta) instead, the mask of this BatchNorm's own ReLU output recomputed
+ *   from x as capk_bn_apply computes it, so y is not re-read), dgamma,
  *   dbeta = column sums (written, or added with accumulate), dx (nullable) =
  *   beta_acc*dx + gamma*rstd*(dz - mean(dz) - xhat*mean(dz*xhat)); dz_out (nullable)
  *   receives dz.  batch_stats = 0: statistics were the running buffers (eval mode),
@@ -507,9 +509,10 @@ int capk_bn_apply(int dtype, int M, int C, const void* x, int64_t ldx, const flo
                   const float* gamma, const float* beta, const void* residual, int64_t ldr, int relu, void* y,
                   int64_t ldy, void* stream);
 int capk_bn_bwd(int dtype, int M, int C, const void* dy, int64_t lddy, const void* y_mask, int64_t ldym,
-                const void* x, int64_t ldx, const float* mean, const float* rstd, const float* gamma, float* dgamma,
-                float* dbeta, int accumulate, void* dx, int64_t lddx, float beta_acc, void* dz_out, int64_t lddz,
-                int batch_stats, void* ws, size_t ws_bytes, void* stream);
+                const void* x, int64_t ldx, const float* mean, const float* rstd, const float* gamma,
+                const float* relu_beta, float* dgamma, float* dbeta, int accumulate, void* dx, int64_t lddx,
+                float beta_acc, void* dz_out, int64_t lddz, int batch_stats, void* ws, size_t ws_bytes,
+                void* stream);
 int capk_maxpool_fwd(int dtype, int B, int H, int W, int C, int K, int stride, int pad, int OH, int OW,
                      const void* x, void* y, uint8_t* idx, void* stream);
 int capk_maxpool_bwd(int dtype, int B, int H, int W, int C, int K, int stride, int pad, int OH, int OW,

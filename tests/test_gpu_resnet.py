@@ -129,6 +129,30 @@ def test_batchnorm_one_sweep_stats_vs_fp64(ops, M, C):
 
 
 @cuda
+@pytest.mark.parametrize("M,C", [(5000, 64), (25088, 256), (300, 2048)])
+def test_batchnorm_bwd_own_relu_mask_identical(ops, M, C):
+    """capk_bn_bwd with relu_beta (the ReLU mask recomputed from x as bn_apply computes it)
+    against the same backward reading the stored ReLU output y: dx, dgamma, dbeta, dz
+    bit-identical (the bottleneck's first two BatchNorms, no residual before the ReLU)."""
+    g = torch.Generator(device="cuda").manual_seed(11)
+    z = (torch.randn(M, C, device="cuda", generator=g) * 2 + 0.3).bfloat16()
+    gamma = torch.rand(C, device="cuda", generator=g) + 0.5
+    beta = torch.randn(C, device="cuda", generator=g)
+    mean, rstd = ops.bn_stats(z, 1e-5, 0.1)
+    y = ops.bn_apply(z, mean, rstd, gamma, beta, relu=True)
+    dy = torch.randn(M, C, device="cuda", generator=g).bfloat16()
+    outs = []
+    for own in (False, True):
+        dg, db = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+        dx, dz = torch.empty_like(z), torch.empty_like(z)
+        ops.bn_bwd(dy, z, mean, rstd, gamma, dg, db, y_mask=None if own else y, dx=dx, dz_out=dz,
+                   relu_beta=beta if own else None)
+        outs.append((dx, dg, db, dz))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+@cuda
 def test_batchnorm_eval_stats(ops):
     g = torch.Generator(device="cuda").manual_seed(4)
     C, M = 128, 50
