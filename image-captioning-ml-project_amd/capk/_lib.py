@@ -106,6 +106,10 @@ SIGNATURES = {
                                 _c_p, _i64, _c_p, _c_p]),
     "capk_soft_attn_bwd": (_i, [_i, _i, _i, _i, _c_p, _i64, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _f, _c_p, _c_p,
                                 _i64, _c_p, _c_p, _i64, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "capk_soft_attn_bwd_step": (_i, [_i, _i, _i, _i, _c_p, _i64, _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _f, _c_p,
+                                     _c_p, _i64, _c_p, _c_p, _i64, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "capk_soft_attn_kv_grad": (_i, [_i, _i, _i, _i, _i, _c_p, _c_p, _i64, _i64, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
+                                    _c_p]),
     "capk_ew_mul": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p, _i64, _c_p]),
     "capk_tanh_gate_fwd": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p, _i64, _c_p]),
     "capk_tanh_gate_bwd": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p, _i64, _c_p, _i64, _c_p, _i64, _c_p]),

@@ -17,6 +17,8 @@ step (the reference recomputes it every step; the values are identical):
 contract (query [B, D] or [B, Q, D], key-padding mask, AdaptiveAttention's memory_state /
 cell_state, differentiable returned weights) via the same protocol, one step per query.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -24,6 +26,8 @@ from .. import _lib as ops_act_lib
 from .. import ops
 from ..config import AttentionConfig, AttentionType
 from .common import G, CapkModule, W
+
+_SOFT_DEFER = os.environ.get("CAPK_SOFT_DEFER", "1") != "0"
 
 
 class ops_act:  # activation codes of the GEMM epilogue / act_bwd
@@ -88,8 +92,16 @@ class SoftAttention(AttentionMechanism, CapkModule):
 
     def begin_bwd(self, H):
         B, S, D, dev = H.B, H.S, H.D, H.kp.device
-        H.dkp = torch.zeros(B, S, D, dtype=torch.float32, device=dev)
-        H.dv = torch.zeros(B, S, D, dtype=torch.float32, device=dev)
+        steps = H.qp.shape[0]
+        # deferred key / value gradients (capk_soft_attn_kv_grad after the last step) unless
+        # CAPK_SOFT_DEFER=0: the steps stash their energies' gradients and output gradients
+        H.defer = _SOFT_DEFER
+        alloc = torch.empty if H.defer else torch.zeros
+        H.dkp = alloc(B, S, D, dtype=torch.float32, device=dev)
+        H.dv = alloc(B, S, D, dtype=torch.float32, device=dev)
+        if H.defer:
+            H.de_all = torch.zeros(steps, B, S, dtype=torch.float32, device=dev)
+            H.dctx_all = torch.zeros(steps, B, D, dtype=self.cdtype, device=dev)
         H.dwe = torch.zeros(B, D, dtype=torch.float32, device=dev)
         H.dbe = torch.zeros(B, dtype=torch.float32, device=dev)
         H.dqp = torch.empty_like(H.qp)
@@ -98,8 +110,13 @@ class SoftAttention(AttentionMechanism, CapkModule):
         """Writes dq_out = d(query) (+ dq_residual).  Soft attention does not read the LSTM states.
         dw: optional gradient on the returned weights (fp32 [B, S])."""
         dt = self.cdtype
-        ops.soft_attn_bwd(H.qp[t], H.kp.view(H.B, H.S, H.D), self._v(H), self.energy.weight.detach().view(-1),
-                          1.0 / self.temperature, H.w[t], dctx, H.dqp[t], H.dkp, H.dv, H.dwe, H.dbe, dw_in=dw)
+        if H.defer:
+            ops.soft_attn_bwd_step(H.qp[t], H.kp.view(H.B, H.S, H.D), self._v(H),
+                                   self.energy.weight.detach().view(-1), 1.0 / self.temperature, H.w[t], dctx,
+                                   H.dqp[t], H.dwe, H.dbe, H.de_all[t], H.dctx_all[t], dw_in=dw)
+        else:
+            ops.soft_attn_bwd(H.qp[t], H.kp.view(H.B, H.S, H.D), self._v(H), self.energy.weight.detach().view(-1),
+                              1.0 / self.temperature, H.w[t], dctx, H.dqp[t], H.dkp, H.dv, H.dwe, H.dbe, dw_in=dw)
         ops.gemm(H.dqp[t], True, W(self.query_proj.weight, dt), False, H.B, H.D, H.D, dq_out, lda=H.D,
                  ldb=H.D, ldc=dq_out.stride(0), residual=dq_residual,
                  ldr=dq_residual.stride(0) if dq_residual is not None else 0)
@@ -109,6 +126,9 @@ class SoftAttention(AttentionMechanism, CapkModule):
         """Q: [steps*B, D] queries of every step (t-major).  Returns (dkeys, dvalues or None)."""
         dt = self.cdtype
         B, S, D = H.B, H.S, H.D
+        if H.defer:
+            ops.soft_attn_kv_grad(H.qp, H.kp.view(B, S, D), self.energy.weight.detach().view(-1), H.de_all, H.w,
+                                  H.dctx_all, H.dkp, H.dv)
         steps = H.qp.shape[0]
         dqp = H.dqp.view(steps * B, D)
         ops.linear_dw(dqp, Q, G(self.query_proj.weight))

@@ -764,6 +764,24 @@ def soft_attn_bwd(qp, kp, v, we, inv_temp, w, dctx, dqp, dkp, dv, dwe_part, dbe_
                                    _p(dbe_part), _stream()), "capk_soft_attn_bwd")
 
 
+def soft_attn_bwd_step(qp, kp, v, we, inv_temp, w, dctx, dqp, dwe_part, dbe_part, de_out, dctx_out, dw_in=None):
+    """soft_attn_bwd without the per-step dkp / dv updates: stashes de [B,S] and dctx [B,D]."""
+    B, S, D = kp.shape
+    check(lib().capk_soft_attn_bwd_step(dtype_code(qp), B, S, D, _p(qp), qp.stride(0), _p(kp), kp.stride(0),
+                                        kp.stride(1), _p(v), v.stride(0), v.stride(1), _p(we), float(inv_temp), _p(w),
+                                        _p(dctx), dctx.stride(0), _p(dw_in), _p(dqp), dqp.stride(0), _p(dwe_part),
+                                        _p(dbe_part), _p(de_out), _p(dctx_out), _stream()), "capk_soft_attn_bwd_step")
+
+
+def soft_attn_kv_grad(qp_all, kp, we, de_all, w_all, dctx_all, dkp, dv=None):
+    """dkp (and dv) [B,S,D] fp32 written from the per-step stashes (capk.h)."""
+    steps, B, D = qp_all.shape
+    S = kp.shape[1]
+    check(lib().capk_soft_attn_kv_grad(dtype_code(qp_all), steps, B, S, D, _p(qp_all), _p(kp), kp.stride(0),
+                                       kp.stride(1), _p(we), _p(de_all), _p(w_all), _p(dctx_all), _p(dkp), _p(dv),
+                                       _stream()), "capk_soft_attn_kv_grad")
+
+
 def argmax_rows(x, V, out):
     """out[r] (int64 view, any stride) = argmax(x[r, :V])."""
     check(lib().capk_argmax_rows(dtype_code(x), x.shape[0], V, x.stride(0), _p(x), _p(out), out.stride(0), _stream()),

@@ -237,7 +237,8 @@ __global__ __launch_bounds__(1024) void soft_attn_bwd_kernel(int S, int D, int D
                                                             int64_t lddc, const float* __restrict__ dw_in,
                                                             T* __restrict__ dqp, int64_t lddq,
                                                             float* __restrict__ dkp, float* __restrict__ dv,
-                                                            float* __restrict__ dwe_part, float* __restrict__ dbe_part) {
+                                                            float* __restrict__ dwe_part, float* __restrict__ dbe_part,
+                                                            float* __restrict__ de_out, T* __restrict__ dctx_out) {
   // grid (B, column chunks of blockDim): every chunk block recomputes the step's S-vector
   // (dctx . v[s], softmax Jacobian) -- S*Dv MACs -- and owns blockDim columns of dq / dkp /
   // dwe / dv; chunk 0 also writes dbe.  (One 4-wave block per image left the latency and
@@ -267,11 +268,18 @@ __global__ __launch_bounds__(1024) void soft_attn_bwd_kernel(int S, int D, int D
   }
   __syncthreads();
   const float dot = red[0];
-  for (int s = tid; s < S; s += CH) de[s] = ws[s] * (de[s] - dot) * inv_temp;
+  for (int s = tid; s < S; s += CH) {
+    de[s] = ws[s] * (de[s] - dot) * inv_temp;
+    if (de_out && blockIdx.y == 0) de_out[(int64_t)b * S + s] = de[s];
+  }
+  if (dctx_out) {  // this step's output gradient, for the deferred dv
+    const int Y = gridDim.y, e0 = (int)((int64_t)Dv * blockIdx.y / Y), e1 = (int)((int64_t)Dv * (blockIdx.y + 1) / Y);
+    for (int d = e0 + tid; d < e1; d += CH) dctx_out[(int64_t)b * Dv + d] = g[d];
+  }
   __syncthreads();
   const T* q = qp + (int64_t)b * ldq;
   const T* kb = kp + (int64_t)b * kp_bs;
-  float* dkb = dkp + (int64_t)b * S * D;
+  float* dkb = dkp ? dkp + (int64_t)b * S * D : nullptr;
   float dbe = 0.f;
   for (int s = tid; s < S; s += CH) dbe += de[s];
   for (int d = d0 + tid; d < D && d < d0 + CH; d += CH) {
@@ -284,7 +292,7 @@ __global__ __launch_bounds__(1024) void soft_attn_bwd_kernel(int S, int D, int D
       const float gr = de[s] * wd * energy_act_grad<ACT>(pre, a);
       dq += gr;
       dw += de[s] * a;
-      dkb[(int64_t)s * D + d] += gr;
+      if (dkp) dkb[(int64_t)s * D + d] += gr;
     }
     dqp[(int64_t)b * lddq + d] = from_f32<T>(dq);
     dwe_part[(int64_t)b * D + d] += dw;
@@ -307,6 +315,41 @@ __global__ __launch_bounds__(1024) void soft_attn_bwd_kernel(int S, int D, int D
     float t = 0.f;
     for (int i = 0; i < nw; ++i) t += red[i];
     dbe_part[b] += t;
+  }
+}
+
+// The key / value gradients of all steps at once (the deferred form of soft_attn_bwd's per-step
+// read-modify-write of two [B, S, D] fp32 buffers): dkp[b,s,d] = sum_t de_t[b,s] we[d]
+// act'(qp_t[b,d] + kp[b,s,d]), dv[b,s,d] = sum_t w_t[b,s] dctx_t[b,d], t from the last step
+// down -- the order (and expressions) of the per-step accumulation it replaces.  One block per
+// (image, key), threads over the columns.
+template <typename T, int ACT>
+__global__ __launch_bounds__(256) void soft_attn_kv_grad_kernel(int steps, int B, int S, int D, int Dv,
+                                                                const T* __restrict__ qp, const T* __restrict__ kp,
+                                                                int64_t kp_bs, int64_t kp_rs,
+                                                                const float* __restrict__ we,
+                                                                const float* __restrict__ de_all,
+                                                                const float* __restrict__ w_all,
+                                                                const T* __restrict__ dctx_all,
+                                                                float* __restrict__ dkp, float* __restrict__ dv) {
+  const int b = blockIdx.x / S, s = blockIdx.x % S;
+  const T* k = kp + (int64_t)b * kp_bs + (int64_t)s * kp_rs;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    const float kd = to_f32(k[d]), wd = we[d];
+    float acc = 0.f;
+    for (int t = steps - 1; t >= 0; --t) {
+      const float pre = to_f32(qp[((int64_t)t * B + b) * D + d]) + kd;
+      const float a = energy_act<ACT>(pre);
+      acc += de_all[((int64_t)t * B + b) * S + s] * wd * energy_act_grad<ACT>(pre, a);
+    }
+    dkp[((int64_t)b * S + s) * D + d] = acc;
+  }
+  if (!dv) return;
+  for (int d = threadIdx.x; d < Dv; d += blockDim.x) {
+    float acc = 0.f;
+    for (int t = steps - 1; t >= 0; --t)
+      acc += w_all[((int64_t)t * B + b) * S + s] * to_f32(dctx_all[((int64_t)t * B + b) * Dv + d]);
+    dv[((int64_t)b * S + s) * Dv + d] = acc;
   }
 }
 
@@ -409,10 +452,36 @@ extern "C" int capk_additive_attn_bwd(int dtype, int act, int B, int S, int D, i
   CAPK_CHECK_ARG(B > 0 && S > 0 && S <= SA_MAXS && D > 0 && Dv > 0, "capk_additive_attn_bwd: need 0 < S <= %d",
                  SA_MAXS);
   CAPK_CHECK_ARG(act == 0 || act == 1, "capk_additive_attn_bwd: act must be 0 (tanh) or 1 (relu)");
-#define K(T, A) hipLaunchKernelGGL((soft_attn_bwd_kernel<T, A>), dim3(B, (D + 1023) / 1024), dim3(1024), 0, capk::S(stream), S, D, Dv, (const T*)qp, ldq, (const T*)kp, kp_bs, kp_rs, (const T*)v, v_bs, v_rs, we, inv_temp, w, (const T*)dctx, lddc, dw_in, (T*)dqp, lddq, dkp, dv, dwe_part, dbe_part)
+#define K(T, A) hipLaunchKernelGGL((soft_attn_bwd_kernel<T, A>), dim3(B, (D + 1023) / 1024), dim3(1024), 0, capk::S(stream), S, D, Dv, (const T*)qp, ldq, (const T*)kp, kp_bs, kp_rs, (const T*)v, v_bs, v_rs, we, inv_temp, w, (const T*)dctx, lddc, dw_in, (T*)dqp, lddq, dkp, dv, dwe_part, dbe_part, (float*)nullptr, (T*)nullptr)
   if (act == 0) DT2(dtype, K, 0); else DT2(dtype, K, 1);
 #undef K
   CAPK_LAUNCH_CHECK("soft_attn_bwd_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_soft_attn_bwd_step(int dtype, int B, int S, int D, const void* qp, int64_t ldq, const void* kp,
+                                       int64_t kp_bs, int64_t kp_rs, const void* v, int64_t v_bs, int64_t v_rs,
+                                       const float* we, float inv_temp, const float* w, const void* dctx,
+                                       int64_t lddc, const float* dw_in, void* dqp, int64_t lddq, float* dwe_part,
+                                       float* dbe_part, float* de_out, void* dctx_out, void* stream) {
+  CAPK_CHECK_ARG(B > 0 && S > 0 && S <= SA_MAXS && D > 0 && de_out && dctx_out,
+                 "capk_soft_attn_bwd_step: need 0 < S <= %d and the de / dctx stashes", SA_MAXS);
+#define K(T, A) hipLaunchKernelGGL((soft_attn_bwd_kernel<T, A>), dim3(B, (D + 1023) / 1024), dim3(1024), 0, capk::S(stream), S, D, D, (const T*)qp, ldq, (const T*)kp, kp_bs, kp_rs, (const T*)v, v_bs, v_rs, we, inv_temp, w, (const T*)dctx, lddc, dw_in, (T*)dqp, lddq, (float*)nullptr, (float*)nullptr, dwe_part, dbe_part, de_out, (T*)dctx_out)
+  DT2(dtype, K, 0);
+#undef K
+  CAPK_LAUNCH_CHECK("soft_attn_bwd_kernel(step)");
+  return CAPK_OK;
+}
+
+extern "C" int capk_soft_attn_kv_grad(int dtype, int steps, int B, int S, int D, const void* qp, const void* kp,
+                                      int64_t kp_bs, int64_t kp_rs, const float* we, const float* de_all,
+                                      const float* w_all, const void* dctx_all, float* dkp, float* dv, void* stream) {
+  CAPK_CHECK_ARG(steps > 0 && B > 0 && S > 0 && D > 0 && qp && kp && we && de_all && dkp && (!dv || (w_all && dctx_all)),
+                 "capk_soft_attn_kv_grad: bad arguments");
+#define K(T, _) hipLaunchKernelGGL((soft_attn_kv_grad_kernel<T, 0>), dim3(B * S), dim3(256), 0, capk::S(stream), steps, B, S, D, D, (const T*)qp, (const T*)kp, kp_bs, kp_rs, we, de_all, w_all, (const T*)dctx_all, dkp, dv)
+  DT2(dtype, K, 0);
+#undef K
+  CAPK_LAUNCH_CHECK("soft_attn_kv_grad_kernel");
   return CAPK_OK;
 }
 

@@ -433,6 +433,20 @@ int capk_soft_attn_bwd(int dtype, int B, int S, int D, const void* qp, int64_t l
                        int64_t kp_rs, const void* v, int64_t v_bs, int64_t v_rs, const float* we, float inv_temp,
                        const float* w, const void* dctx, int64_t lddc, const float* dw_in, void* dqp, int64_t lddq,
                        float* dkp, float* dv, float* dwe_part, float* dbe_part, void* stream);
+/* The deferred form: capk_soft_attn_bwd_step writes dqp, accumulates dwe_part / dbe_part and
+ * stashes the step's softmax-Jacobian energies de_out [B,S] (fp32) and output gradient
+ * dctx_out [B,D] instead of updating dkp / dv; after the last step capk_soft_attn_kv_grad WRITES
+ * dkp, dv [B,S,D] (fp32) from the stashes of all steps ([steps,B,S] / [steps,B,D], qp
+ * [steps,B,D], w_all = the forward weights [steps,B,S]), summing t from the last step down as
+ * the per-step accumulation does -- two [B,S,D] read-modify-writes per step become one write. */
+int capk_soft_attn_bwd_step(int dtype, int B, int S, int D, const void* qp, int64_t ldq, const void* kp,
+                            int64_t kp_bs, int64_t kp_rs, const void* v, int64_t v_bs, int64_t v_rs, const float* we,
+                            float inv_temp, const float* w, const void* dctx, int64_t lddc, const float* dw_in,
+                            void* dqp, int64_t lddq, float* dwe_part, float* dbe_part, float* de_out, void* dctx_out,
+                            void* stream);
+int capk_soft_attn_kv_grad(int dtype, int steps, int B, int S, int D, const void* qp, const void* kp, int64_t kp_bs,
+                           int64_t kp_rs, const float* we, const float* de_all, const float* w_all,
+                           const void* dctx_all, float* dkp, float* dv, void* stream);
 
 /* ------------------------------------------- attention-module gates (A8-A10) ----
  * capk_ew_mul: out = a * b (AoA info * gate, attention.py:354).
