@@ -20,6 +20,13 @@ S=${STEPS:-tests}
 [[ ,$S, == *,tsel,* ]] && run tsel 600 $PYT ${TESTS}
 [[ ,$S, == *,tests,* ]] && run tests 900 python -u -m pytest tests -m gpu -q -rf --timeout 240 --timeout-method thread
 [[ ,$S, == *,smoke,* ]] && run smoke 240 python -c "import __graft_entry__ as g; g.smoke()"
+if [[ ,$S, == *,traffic,* ]]; then  # GEMM bytes per launch for bench.py's roofline.traffic (-> profiles/round4/gemm_traffic.json)
+  run fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/fetch -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --beam-batch 0
+  run write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/write -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --beam-batch 0
+  python3 tools/pmc_traffic.py $OUT/fetch $OUT/write --out $OUT/gemm_traffic.json --cmd "python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --beam-batch 0" > /dev/null
+  # later bench steps of this call read the fresh file (the box's copy of the tree)
+  cp $OUT/gemm_traffic.json profiles/round4/gemm_traffic.json
+fi
 [[ ,$S, == *,bench3,* ]] && run bench_config3 480 python bench.py --steps 10 --warmup 3
 [[ ,$S, == *,bench3q,* ]] && run bench_config3q 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --beam-batch 0
 [[ ,$S, == *,bench5,* ]] && run bench_config5 480 python bench.py --workload config5 --steps 5 --warmup 2
@@ -27,11 +34,6 @@ S=${STEPS:-tests}
 [[ ,$S, == *,prof3,* ]] && run prof3 420 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof3 -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --beam-batch 0
 [[ ,$S, == *,prof5,* ]] && run prof5 420 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof5 -o run -- python3 bench.py --workload config5 --steps 3 --warmup 1 --no-cpu-baseline --beam-batch 0
 [[ ,$S, == *,prof2,* ]] && run prof2 420 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof2 -o run -- python3 bench.py --workload config2 --steps 3 --warmup 2 --no-cpu-baseline
-if [[ ,$S, == *,traffic,* ]]; then  # GEMM bytes per launch for bench.py's roofline.traffic (-> profiles/round4/gemm_traffic.json)
-  run fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/fetch -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --beam-batch 0
-  run write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/write -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --beam-batch 0
-  python3 tools/pmc_traffic.py $OUT/fetch $OUT/write --out $OUT/gemm_traffic.json --cmd "python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --beam-batch 0" > /dev/null
-fi
 [[ ,$S, == *,gemmb,* ]] && run gemmb 400 python tools/gemm_bench.py ${GEMMB_ARGS:-}
 [[ ,$S, == *,extra,* ]] && run extra ${EXTRA_SECS:-300} ${EXTRA}
 exit 0
