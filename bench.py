@@ -381,7 +381,7 @@ def run_config5(args, world, rank, device):
                      "launches": f8["launches"], "ms": round(f8["total_ms"], 2),
                      "bf16_gemm": {"launches": bf["launches"], "ms": round(bf["total_ms"], 2),
                                    "tflops": round(bf["tflops"], 1), "frac_of_bf16_peak": round(bf["tflops"] / PEAK_BF16_TFLOPS, 4)},
-                     "gemm_share_of_step": round(gem["total_ms"] * gem["stride"] / (elapsed * 1e3), 3)},
+                     "gemm_share_of_step": round(gem["total_ms"] * gem["launches_seen"] / max(1, gem["launches"]) / (elapsed * 1e3), 3)},
         "model_flops": {"per_image": fpi, "tflops": round(fpi * value / world / 1e12, 1)},
         "phases_ms": dict(phase_ms, note="GPU ms per update between HIP events on the compute stream (2 extra "
                                          "untimed updates); the beam-4 baseline search runs on a side stream "
@@ -487,7 +487,7 @@ def run_config2(args, world, rank, device):
                      "achieved": round(bf["tflops"], 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(bf["tflops"] / PEAK_BF16_TFLOPS, 4), "traffic": None,
                      "traffic_source": "not collected for config 2", "launches": bf["launches"],
-                     "gemm_share_of_step": round(gem["total_ms"] * gem["stride"] / (elapsed * 1e3), 3)},
+                     "gemm_share_of_step": round(gem["total_ms"] * gem["launches_seen"] / max(1, gem["launches"]) / (elapsed * 1e3), 3)},
         "final_loss": round(float(last[0]), 4),
         "process_group": process_group(world),
     }
@@ -636,7 +636,7 @@ def main():
                          "algorithmic_bytes": round(gem["avg_bytes"]),
                          "launches": gem["launches"], "launches_in_steps": gem["launches_seen"],
                          "sample_stride": gem["stride"], "avg_launch_ms": round(gem["avg_ms"], 4),
-                         "gemm_share_of_step": round(gem["total_ms"] * gem["stride"] / (elapsed * 1e3), 3)},
+                         "gemm_share_of_step": round(gem["total_ms"] * gem["launches_seen"] / max(1, gem["launches"]) / (elapsed * 1e3), 3)},
             "model_flops": {"per_image": FLOP_PER_IMAGE,
                             "tflops": round(FLOP_PER_IMAGE * value / world / 1e12, 1),
                             "frac_of_peak": round(FLOP_PER_IMAGE * value / world / 1e12 / PEAK_BF16_TFLOPS, 4)},
@@ -655,7 +655,7 @@ def main():
                             "roofline": {"bound": "mfma", "kernel": "bf16 GEMM family (all capk_gemm launches)",
                                          "achieved": round(bach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                                          "frac": round(bach / PEAK_BF16_TFLOPS, 4),
-                                         "gemm_share": round(bgem["total_ms"] * bgem["stride"] / (bdt * 1e3), 3)},
+                                         "gemm_share": round(bgem["total_ms"] * bgem["launches_seen"] / max(1, bgem["launches"]) / (bdt * 1e3), 3)},
                             "model_flops": {"per_caption": FLOP_PER_CAPTION,
                                             "tflops": round(FLOP_PER_CAPTION * cps / world / 1e12, 1)}}
             if world == 1 and not args.no_cpu_baseline:

@@ -35,6 +35,7 @@ SIGNATURES = {
     "capk_gemm_last_config": (_i, []),
     "capk_gemm_force_config": (_i, [_i]),
     "capk_gemm_set_tail": (_i, [_i]),
+    "capk_gemm_set_group": (_i, [_i]),
     "capk_image_desc_bytes": (_sz, []),
     "capk_resize_normalize": (_i, [_i, _i, _i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "capk_quant_fp8_workspace": (_sz, [_i, _i, _i]),

@@ -708,8 +708,7 @@ def product_ln(x, w, conv1d_weight, b, residual, ln_w, ln_b, eps, *, keep=False)
         return layernorm_fwd(s, ln_w, ln_b, eps)[0], s
     L = lib()
     sp = ctypes.c_int(0)
-    ws = torch.empty(L.capk_gemm_slabs_workspace(M, N, K, ctypes.byref(sp)) // 4, dtype=torch.float32,
-                     device=x.device)
+    ws = _ws(L.capk_gemm_slabs_workspace(M, N, K, ctypes.byref(sp)), x.device).view(torch.float32)
     splits = gemm_pair_slabs(M, N, K, x, x.stride(0), w, w.stride(0), not conv1d_weight, ws)
     y = torch.empty(M, N, dtype=x.dtype, device=x.device)
     s = torch.empty(M, N, dtype=x.dtype, device=x.device) if keep else None

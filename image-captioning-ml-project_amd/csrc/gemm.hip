@@ -524,6 +524,8 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
                                  st, nullptr, slab ? nullptr : ws, slab ? 0 : ws_bytes, &tail_r0, &tail_splits);
     if (rc != CAPK_OK) return rc;
     if (tail_r0 >= 0) {  // the split-K tail round's slabs -> rows [256 r0, M) with the epilogue
+      // the row offsets below are in bf16 elements: launch_gemm8q plans a tail only for bf16 outputs
+      CAPK_CHECK_ARG(out_dtype == CAPK_BF16, "capk_gemm: split-K tail round planned for a non-bf16 output");
       const int64_t r = (int64_t)tail_r0 * 256;
       Epi et = e;
       et.M = M - (int)r;

@@ -120,6 +120,8 @@ struct Epi8q {
   float* dsum;  // DSUM kernels: column-sum partials [2 * tile rows][N]
   float* tail_ws;  // TAIL kernels: fp32 slabs [splits][M - 256 tail_r0][N] of the tail row blocks
   int tail_r0, tail_splits;
+  int group;  // grouped raster: tiles of the whole-item rows in groups of `group` row blocks, column-major
+              // inside a group (0: row-major); host: gemm8q_group()
   unsigned long long* trace;  // CAPK_DIAG_TRACE builds only: per-item timestamps
 };
 
@@ -188,8 +190,18 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
       k0 = tk0;
       k1 = tk1;
     }
-    const int sp = it / ntiles, tile = it - sp * ntiles, tm = tile / ntn;
-    return Item{tm * 256, (tile - tm * ntn) * 256, sp * nk, k0, k1};
+    const int sp = it / ntiles, tile = it - sp * ntiles;
+    int tm, tn;
+    if (e.group > 0 && tile < W) {  // grouped raster over the whole-item rows [0, W / ntn)
+      const int gsz = e.group * ntn, g = tile / gsz, r = tile - g * gsz;
+      const int rows = min(e.group, W / ntn - g * e.group);
+      tn = r / rows;
+      tm = g * e.group + (r - tn * rows);
+    } else {
+      tm = tile / ntn;
+      tn = tile - tm * ntn;
+    }
+    return Item{tm * 256, tn * 256, sp * nk, k0, k1};
   };
 
   // per-lane byte offsets of this wave's two 1-KiB pieces of each half (h: A0 A1 B0 B1) at
@@ -683,6 +695,30 @@ size_t gemm8q_tail_workspace(int M, int N, int K) {
   return (size_t)S * (size_t)(M - r0 * 256) * N * sizeof(float);
 }
 
+// Grouped raster (Epi8q::group).  WG b runs items (b & 7) * 32 + (b >> 3) + 256 j, so the 32
+// WGs of one XCD work on 32 consecutive items at a time, and the operand blocks they read
+// (one 256-row A block per tile row, one 256-column B block per tile column, each
+// 256 x K bf16) come through that XCD's 4 MiB L2: with the 32 WGs in near lockstep, a
+// (block, K-tile) misses once per chunk, so the L2 miss share of the LDS-DMA stream is about
+// distinct blocks / 64.  Row-major order makes a 32-item chunk of a wide product touch 1-3 row
+// blocks and up to 32 column blocks (the LM head: 2 + 32; FC1: 3 + 12, QKV 4 + 9); groups of
+// g row blocks walked column-major make it g rows x 32/g columns.  Measured in one process
+// (tools/gemm_ab.py, profiles/round5/raster_ab.txt): g = 8 on the ViT's wide products (QKV
+// 168.7 -> 163.8 us, FC1 + GELU + act' 309.9 -> 300.4, FC2 dX x act' 287.0 -> 277.9), g = 4 on
+// the 20-row LM head (409.9 -> 371.8), row-major on the N = 768 products (3 column blocks:
+// already 11 rows + 3 columns per chunk; grouping measured neutral to -1 %).
+static int g_group_mode = -2;
+int gemm8q_group(int ntm, int ntn) {
+  static const int env_mode = [] {
+    const char* v = getenv("CAPK_GEMM_GROUP");
+    return v ? atoi(v) : -1;
+  }();
+  const int mode = g_group_mode >= -1 ? g_group_mode : env_mode;
+  if (mode >= 0) return mode;
+  if (ntn <= 4 || ntm < 8) return 0;
+  return ntm <= 32 ? 4 : 8;
+}
+
 int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int64_t lda, const void* B, int64_t ldb,
                   int M, int N, int K, int splits, const Epi& e, float* slab, hipStream_t st, float* dsum,
                   void* ws, size_t ws_bytes, int* tail_r0, int* tail_splits) {
@@ -736,6 +772,8 @@ int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int
     }
   }
   CAPK_CHECK_ARG(!fwd_act || (a_kmajor && b_kmajor), "capk_gemm(gemm8q): forward activations need K-major operands");
+  // grouped raster over the whole-item rows (all rows, or [0, r0) with a tail round)
+  p.group = gemm8q_group(p.tail_ws ? p.tail_r0 : cdiv(M, 256), cdiv(N, 256));
 #if defined(CAPK_DIAG_TRACE)
   p.trace = (unsigned long long*)diag_trace_buf();
   CAPK_CHECK_ARG(p.trace != nullptr, "capk_gemm(gemm8q, trace build): no trace buffer");
@@ -806,6 +844,12 @@ extern "C" int capk_gemm_diag_trace(void* host_dst, size_t bytes) {
   return hipMemcpy(host_dst, b, capk::diag_trace_bytes(), hipMemcpyDeviceToHost) == hipSuccess ? CAPK_OK : CAPK_EINVAL;
 }
 #endif
+
+extern "C" int capk_gemm_set_group(int rows) {
+  CAPK_CHECK_ARG(rows >= -2 && rows <= 64, "capk_gemm_set_group: rows must be -2 (environment), -1 (auto) or 0..64");
+  capk::g_group_mode = rows;
+  return CAPK_OK;
+}
 
 extern "C" int capk_gemm_set_tail(int mode) {
   CAPK_CHECK_ARG(mode >= -1 && mode <= 1, "capk_gemm_set_tail: mode must be -1 (environment), 0 or 1");

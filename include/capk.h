@@ -83,6 +83,12 @@ int capk_gemm_force_config(int cfg);
  * per tile into fp32 slabs in capk_gemm's workspace, then one reduce + epilogue launch):
  * 1 on (default), 0 off, -1 back to CAPK_GEMM_TAIL. */
 int capk_gemm_set_tail(int mode);
+/* Tile raster of the persistent 256x256 kernel: tiles in groups of `rows` row blocks,
+ * column-major inside a group, so the 32 tiles an XCD runs at a time share fewer operand
+ * blocks in its L2.  -1: automatic (default: 8 row blocks for products of more than 4
+ * column blocks, 4 when the grid has <= 32 row blocks, row-major for narrower products),
+ * 0: row-major, n > 0: groups of n row blocks; -2: back to CAPK_GEMM_GROUP. */
+int capk_gemm_set_group(int rows);
 int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K,
               const void* A, int64_t lda, int a_kmajor,
               const void* B, int64_t ldb, int b_kmajor,

@@ -242,3 +242,58 @@ def test_tail_round_exact(mode, ak, bk):
     finally:
         L.capk_gemm_set_tail(-1)
         L.capk_gemm_force_config(-1)
+
+
+@cuda
+@pytest.mark.parametrize("tail", [0, 1])
+@pytest.mark.parametrize("group", [0, 2, 8, -1])
+def test_grouped_raster_exact(group, tail):
+    """The persistent kernel's grouped raster (capk_gemm_set_group: tiles of the whole-item rows
+    walked in groups of `group` row blocks, column-major inside a group; 0 = row-major, -1 =
+    the automatic choice) only reorders the items: a 21 x 13-tile grid (groups 8, 8, 5 -- or
+    8, 8, 3 over the 19 whole-item rows when the split-K tail round is on) with K = 1536 and
+    exact small-integer operands must give the exact product on every layout, with bias +
+    residual, and the fused dX x act' + column sums (DSUM) must give identical outputs and
+    column sums under every raster."""
+    from capk import _lib, ops
+    from capk._lib import ACT_DERIV, ACT_GELU_ERF
+    L = _lib.load()
+    L.capk_gemm_force_config(6)
+    L.capk_gemm_set_tail(tail)
+    L.capk_gemm_set_group(group)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(7)
+        M, N, K = 20 * 256 + 72, 13 * 256, 1536
+        a = torch.randint(-2, 3, (M, K), device="cuda", generator=g).bfloat16()
+        w = torch.randint(-2, 3, (N, K), device="cuda", generator=g).bfloat16()
+        ref = a.float() @ w.float().t()
+        for ak, bk in [(True, True), (True, False), (False, True), (False, False)]:
+            A = a if ak else a.t().contiguous()
+            B = w if bk else w.t().contiguous()
+            C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            ops.gemm(A, ak, B, bk, M, N, K, C, lda=A.stride(0), ldb=B.stride(0), ldc=N)
+            assert L.capk_gemm_last_config() == 6
+            assert torch.equal(C.float(), ref.bfloat16().float()), (ak, bk)
+        bias = torch.randint(-3, 4, (N,), device="cuda", generator=g).float()
+        res = torch.randint(-8, 9, (M, N), device="cuda", generator=g).bfloat16()
+        C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        ops.gemm(a, True, w, True, M, N, K, C, lda=K, ldb=K, ldc=N, bias=bias, residual=res, ldr=N)
+        assert torch.equal(C.float(), (ref + bias + res.float()).bfloat16().float())
+        # DSUM: dX = dY W (W [K', N'] N-major) times aux, plus the column sums (fixed order)
+        dy = torch.randint(-2, 3, (M, K), device="cuda", generator=g).bfloat16()
+        wt = torch.randint(-2, 3, (K, N), device="cuda", generator=g).bfloat16()
+        aux = torch.randint(0, 3, (M, N), device="cuda", generator=g).bfloat16()
+        outs = []
+        for gm in (0, group):
+            L.capk_gemm_set_group(gm)
+            db = torch.zeros(N, device="cuda")
+            out = ops.linear_dx(dy, wt, act_bwd=ACT_GELU_ERF | ACT_DERIV, aux=aux, dsum=db)
+            assert L.capk_gemm_last_config() == 6
+            outs.append((out, db))
+        exact = ((dy.float() @ wt.float()) * aux.float()).bfloat16()
+        assert torch.equal(outs[1][0], exact)
+        assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    finally:
+        L.capk_gemm_set_group(-2)
+        L.capk_gemm_set_tail(-1)
+        L.capk_gemm_force_config(-1)

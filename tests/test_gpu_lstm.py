@@ -126,16 +126,23 @@ def test_lstm_bf16_close_and_trains(name):
     assert all(np.isfinite(losses)) and losses[-1] < losses[0] * 0.9, losses
 
 
-def _full_lstm(precision, kind="soft", heads=1, seed=21):
+def _full_lstm(precision, kind="soft", heads=1, seed=21, embedding_dim=None):
     """Config-2 decoder geometry: LSTM 768 hidden x 6 layers (DecoderConfig defaults),
-    soft attention over the 49 ResNet feature keys, GPT-2 vocabulary."""
+    soft attention over the 49 ResNet feature keys, GPT-2 vocabulary (embedding_dim: the
+    reference LSTMDecoder's optional embedding width, decoders.py:77-100)."""
     import capk
     from capk import config as C
     from capk.models.decoders import build_decoder
+    from capk.models.lstm import LSTMDecoder
     torch.manual_seed(seed)
     V, pad = 50257, 50256
-    dec = build_decoder(C.DecoderConfig(decoder_type="lstm", hidden_dim=768, num_layers=6, num_heads=heads),
-                        C.AttentionConfig(attention_type=kind, num_heads=heads), V, pad, pad, pad)
+    dcfg = C.DecoderConfig(decoder_type="lstm", hidden_dim=768, num_layers=6, num_heads=heads)
+    acfg = C.AttentionConfig(attention_type=kind, num_heads=heads)
+    acfg.hidden_dim = 768
+    if embedding_dim is None:
+        dec = build_decoder(dcfg, acfg, V, pad, pad, pad)
+    else:
+        dec = LSTMDecoder(dcfg, acfg, V, pad, embedding_dim=embedding_dim)
     sd = {k: v.detach().clone() for k, v in dec.state_dict().items()}
     capk.prepare(dec, "cuda", precision)
     dec.eval()
@@ -222,16 +229,20 @@ def test_gemm_pair_slabs_k_and_n_seams():
 
 
 @cuda
-def test_lstm_pair_route_matches_gemm_route_train_bf16():
+@pytest.mark.parametrize("embedding_dim", [None, 320])
+def test_lstm_pair_route_matches_gemm_route_train_bf16(embedding_dim):
     """The bf16 teacher-forced pass with the pair-slab recurrences (default) against the
     per-GEMM route (two GEMMs + reduces per step and layer) on the same weights, inputs and
     dropout seeds, in train mode at the config-2 geometry (768 x 6 layers, inter-layer and
     output dropout on): logits, d(features), d(pooled) and every parameter gradient within
-    3e-2 relative (bf16 rounding of the two routes differs: fp32 slab sums vs bf16 gates)."""
+    3e-2 relative (bf16 rounding of the two routes differs: fp32 slab sums vs bf16 gates).
+    embedding_dim 320 ((E + D) % 128 != 0) takes the mixed backward: layer 0 on the per-GEMM
+    route (dnext by its own product, dh[0] carried as the initial-state gradient) under the
+    slab-summed upper layers."""
     import capk.models.lstm as mlstm
     from capk.models import common
     from capk.train import CombinedLoss
-    dec, _ = _full_lstm("bf16")
+    dec, _ = _full_lstm("bf16", embedding_dim=embedding_dim)
     dec.train()
     B, T, S, D = 16, 20, 49, 768
     g = torch.Generator().manual_seed(4)
@@ -273,3 +284,55 @@ def test_lstm_pair_route_matches_gemm_route_train_bf16():
             assert err <= 3e-2 * float(ref.norm()) + 1e-3, (n, err, float(ref.norm()))
             checked += 1
     assert checked >= 4 * 6
+
+
+@cuda
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-6), ("bf16", 1e-3)])
+def test_soft_attention_deferred_kv_grad_matches_per_step(precision, tol):
+    """The soft-attention backward's deferred key / value gradients (default: each decode step
+    stashes d(energy) [B, S] and d(context) [B, D]; capk_soft_attn_kv_grad writes dK / dV once
+    after the last step, summing in the per-step order) against the per-step read-modify-write
+    route (CAPK_SOFT_DEFER=0) on the same weights and inputs at the config-2 geometry (768 x 6,
+    49 keys): d(features), d(pooled) and every attention / LSTM gradient agree to `tol`
+    (relative; bit-identity is reported, the claim of attention.py's deferral)."""
+    import capk.models.attention as matt
+    from capk.train import CombinedLoss
+    dec, _ = _full_lstm(precision)
+    B, T, S, D = 8, 20, 49, 768
+    g = torch.Generator().manual_seed(6)
+    dt = torch.float32 if precision == "fp32" else torch.bfloat16
+    feats = torch.randn(B, S, D, generator=g).cuda().to(dt)
+    pooled = torch.randn(B, D, generator=g).cuda().to(dt)
+    caps = torch.randint(0, 50256, (B, T), generator=g).cuda()
+    runs = []
+    saved = matt._SOFT_DEFER
+    try:
+        for defer in (True, False):
+            matt._SOFT_DEFER = defer
+            for p in dec.parameters():
+                if getattr(p, "_capk_grad", None) is not None:
+                    p._capk_grad.zero_()
+            fg = feats.clone().requires_grad_(True)
+            pg = pooled.clone().requires_grad_(True)
+            out = dec({"features": fg, "pooled_features": pg, "attention_mask": None}, caps)
+            CombinedLoss(50256)(logits=out["logits"], targets=caps)["total_loss"].backward()
+            grads = {n: p._capk_grad.float().clone() for n, p in dec.named_parameters()
+                     if getattr(p, "_capk_grad", None) is not None}
+            runs.append((fg.grad.float(), pg.grad.float(), grads))
+    finally:
+        matt._SOFT_DEFER = saved
+    (fa, pa, ga), (fb, pb, gb) = runs
+    same = torch.equal(fa, fb) and torch.equal(pa, pb) and all(torch.equal(ga[n], gb[n]) for n in gb)
+    print(f"soft deferral {precision}: bit-identical={same}")
+
+    def rel(a, b):
+        return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+    assert rel(fa, fb) <= tol and rel(pa, pb) <= tol
+    checked = 0
+    for n, ref in gb.items():
+        if float(ref.norm()) == 0.0:
+            continue
+        assert float((ga[n] - ref).norm()) <= tol * float(ref.norm()) + 1e-7, n
+        checked += 1
+    assert checked >= 10
