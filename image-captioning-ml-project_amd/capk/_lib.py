@@ -77,6 +77,12 @@ SIGNATURES = {
     "capk_shifted_ce_workspace": (_sz, [_i, _i]),
     "capk_shifted_ce": (_i, [_i, _i, _i, _i, _i64, _c_p, _c_p, _i, _c_p, _c_p, _c_p, _c_p, _sz, _c_p]),
     "capk_shifted_ce_weighted": (_i, [_i, _i, _i, _i, _i64, _c_p, _c_p, _i, _c_p, _c_p, _c_p, _c_p, _c_p, _sz, _c_p]),
+    "capk_linear_lse_part_bytes": (_sz, [_i, _i]),
+    "capk_linear_lse": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p, _c_p, _i64, _i, _c_p, _sz, _c_p, _c_p, _sz,
+                             _c_p]),
+    "capk_ce_lse_workspace": (_sz, [_i, _i, _i64]),
+    "capk_ce_lse_fwd": (_i, [_i, _i, _i, _i64, _c_p, _c_p, _i, _c_p, _i, _c_p, _c_p, _c_p, _sz, _c_p]),
+    "capk_ce_lse_bwd": (_i, [_i, _i, _i, _i, _i64, _c_p, _c_p, _i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _sz, _c_p]),
     "capk_zero": (_i, [_c_p, _sz, _c_p]),
     "capk_colsum_workspace": (_sz, [_i, _i]),
     "capk_colsum": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i, _c_p, _sz, _c_p]),

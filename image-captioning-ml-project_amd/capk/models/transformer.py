@@ -160,7 +160,15 @@ class _DecoderFn(torch.autograd.Function):
                                  f, s3, mu3, rs3, drops))
         ol = m.output_layer
         wout = ol.weight._capk_pad_bf16 if dt == torch.bfloat16 else ol.weight._capk_pad_master
-        logits_pad = ops.linear(x, wout, _pad_bias(ol))
+        if dt == torch.bfloat16:
+            # the LM head leaves the shifted CE's softmax partials (and where the CE backward may
+            # write this head's bias gradient) on the logits buffer: capk/train/losses.py
+            logits_pad, part = ops.linear_lse(x, wout, _pad_bias(ol), V)
+            if part is not None:
+                logits_pad._capk_ce_part = (part, logits_pad._version)
+                logits_pad._capk_bias_grad = _pad_bias_grad(ol)
+        else:
+            logits_pad = ops.linear(x, wout, _pad_bias(ol))
         ctx.m = m
         ctx.d_emb = d_emb
         ctx.dims = (B, S, T, D, H, hd, scale, V, Vp, rpb, M_ext)
@@ -185,7 +193,8 @@ class _DecoderFn(torch.autograd.Function):
         if dlogits is not None:
             dl = _padded_grad(dlogits, ctx.logits_pad, BT, V, Vp)
             ops.linear_dw(dl, xT, ol.weight._capk_pad_grad)
-            ops.colsum(dl, _pad_bias_grad(ol))
+            if not getattr(dl, "_capk_bias_done", False):  # (else written by the CE backward's pass)
+                ops.colsum(dl, _pad_bias_grad(ol))
             wout = ol.weight._capk_pad_bf16 if dt == torch.bfloat16 else ol.weight._capk_pad_master
             dx = ops.linear_dx(dl, wout)
         else:

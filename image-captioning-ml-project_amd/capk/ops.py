@@ -273,6 +273,62 @@ def linear(x, w, b=None, *, out=None, residual=None, act=0, preact=None, out_dty
     return out
 
 
+def linear_lse(x, w, b, V):
+    """The LM head with the shifted CE's softmax partials (capk_linear_lse): returns
+    (y = x w^T + b [M, N], part) where part (fp32, [4 cdiv(N, 256)][M] (max, sum) pairs) is None
+    when the product did not run on the persistent kernel (then use shifted_ce as usual)."""
+    M, K = x.shape
+    N = w.shape[0]
+    out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    if (x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or not w.is_contiguous()
+            or _fp8_route(x, w, M, N, K, 0, False) is not None):
+        return linear(x, w, b, out=out), None
+    _need_gpu(x, w, out)
+    L = lib()
+    pb = L.capk_linear_lse_part_bytes(M, N)
+    part = torch.empty(pb // 4, dtype=torch.float32, device=x.device)
+    wsb = L.capk_gemm_workspace(BF16, BF16, M, N, K)
+    ws = _ws(wsb, x.device)
+    done = ctypes.c_int(0)
+    timed = GEMM_TIMER.active()
+    if timed:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    check(L.capk_linear_lse(M, N, K, _p(x), x.stride(0), _p(w), w.stride(0), _p(b), _p(out), out.stride(0), int(V),
+                            _p(part), pb, ctypes.byref(done), _p(ws), wsb if ws is not None else 0, _stream()),
+          "capk_linear_lse")
+    if timed:  # (algorithmic bytes: x, w read once, C written once, the partials written once)
+        ev1.record()
+        GEMM_TIMER.records.append((ev0, ev1, 2.0 * M * N * K, BF16, 2 * (M * K + N * K + M * N) + pb, 0))
+    return out, (part if done.value else None)
+
+
+def ce_lse_fwd(logits2d, targets, B, T, V, ignore_index, part):
+    """(loss fp32 [2] = (mean, count), lse fp32 [B*T]) of the shifted CE from linear_lse's partials."""
+    L = lib()
+    M = B * T
+    loss = torch.empty(2, dtype=torch.float32, device=logits2d.device)
+    lse = torch.empty(M, dtype=torch.float32, device=logits2d.device)
+    wsb = L.capk_ce_lse_workspace(B, T, logits2d.stride(0))
+    ws = _ws(wsb, logits2d.device)
+    nparts = part.numel() // (2 * M)
+    check(L.capk_ce_lse_fwd(B, T, V, logits2d.stride(0), _p(logits2d), _p(targets), int(ignore_index), _p(part),
+                            nparts, _p(lse), _p(loss), _p(ws), wsb, _stream()), "capk_ce_lse_fwd")
+    return loss, lse
+
+
+def ce_lse_bwd(logits2d, targets, B, T, V, ignore_index, lse, loss, grad_scale, dlogits, dbias=None):
+    """dlogits (+ the column sums into dbias, written) of the shifted CE from the saved lse / count."""
+    L = lib()
+    wsb = L.capk_ce_lse_workspace(B, T, logits2d.stride(0))
+    ws = _ws(wsb, logits2d.device)
+    check(L.capk_ce_lse_bwd(dtype_code(logits2d), B, T, V, logits2d.stride(0), _p(logits2d), _p(targets),
+                            int(ignore_index), _p(lse), loss[1:].data_ptr(), _p(grad_scale), _p(dlogits), _p(dbias),
+                            _p(ws), wsb, _stream()), "capk_ce_lse_bwd")
+    return dlogits
+
+
 def linear_dx(dy, w, *, out=None, act_bwd=0, aux=None, beta=0.0, drop=NO_DROP, dsum=None):
     """dX[M,K] = dY[M,N] @ W[N,K]  (optionally * act'(aux) * dropout-mask: fused activation backward).
     dsum (fp32 [K], with act_bwd): also the column sums of the result (the bias gradient of the

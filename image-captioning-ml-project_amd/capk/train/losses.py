@@ -25,27 +25,53 @@ def _padded_base(logits):
     raise ValueError("capk CE needs [B,T,V] logits with a unit-stride, 8-aligned row layout")
 
 
+def _lm_partials(base):
+    """The softmax partials the decoder's LM head left on its padded logits buffer
+    (ops.linear_lse), if they still describe it (the buffer not written since)."""
+    info = getattr(base, "_capk_ce_part", None)
+    if info is None or info[1] != base._version:
+        return None
+    return info[0]
+
+
 class _ShiftedCEFn(torch.autograd.Function):
+    """Forward: the loss from the LM head's softmax partials when the decoder left them
+    (capk_ce_lse_fwd: no pass over the logits), else one capk_shifted_ce pass.  Backward: with the
+    partials' row lse, one streaming pass that also writes the LM-head bias gradient the decoder
+    registered on the buffer (capk_ce_lse_bwd); else capk_shifted_ce's gradient."""
+
     @staticmethod
     def forward(ctx, logits, targets, pad):
         B, T, V = logits.shape
         base = _padded_base(logits)
         targets = targets.contiguous()
-        loss = ops.shifted_ce(base, targets, B, T, V, pad, want_loss=True)
-        ctx.save_for_backward(targets)
+        part = _lm_partials(base)
+        if part is not None:
+            loss, lse = ops.ce_lse_fwd(base, targets, B, T, V, pad, part)
+            ctx.save_for_backward(targets, lse, loss)
+        else:
+            loss = ops.shifted_ce(base, targets, B, T, V, pad, want_loss=True)
+            ctx.save_for_backward(targets)
         ctx.base = base
         ctx.dims = (B, T, V, pad)
         return loss[0]
 
     @staticmethod
     def backward(ctx, dloss):
-        (targets,) = ctx.saved_tensors
+        saved = ctx.saved_tensors
         B, T, V, pad = ctx.dims
         base = ctx.base
         ctx.base = None
         dbase = torch.empty_like(base)
-        ops.shifted_ce(base, targets, B, T, V, pad, want_loss=False, dlogits=dbase,
-                       grad_scale=dloss.reshape(1).float().contiguous())
+        gs = dloss.reshape(1).float().contiguous()
+        if len(saved) == 3:
+            targets, lse, loss = saved
+            dbias = getattr(base, "_capk_bias_grad", None)
+            ops.ce_lse_bwd(base, targets, B, T, V, pad, lse, loss, gs, dbase, dbias)
+            if dbias is not None:  # the decoder's LM-head backward then skips its column sums
+                dbase._capk_bias_done = True
+        else:
+            ops.shifted_ce(base, saved[0], B, T, V, pad, want_loss=False, dlogits=dbase, grad_scale=gs)
         return dbase[:, :V].view(B, T, V), None, None
 
 

@@ -524,18 +524,20 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
                                  st, nullptr, slab ? nullptr : ws, slab ? 0 : ws_bytes, &tail_r0, &tail_splits);
     if (rc != CAPK_OK) return rc;
     if (tail_r0 >= 0) {  // the split-K tail round's slabs -> rows [256 r0, M) with the epilogue
-      // the row offsets below are in bf16 elements: launch_gemm8q plans a tail only for bf16 outputs
-      CAPK_CHECK_ARG(out_dtype == CAPK_BF16, "capk_gemm: split-K tail round planned for a non-bf16 output");
-      const int64_t r = (int64_t)tail_r0 * 256;
+      // (bf16 outputs with any one side operand; fp32 outputs carry none: gemm8q_supports)
+      const int64_t r = (int64_t)tail_r0 * 256, es = esz;  // row offsets in output elements
       Epi et = e;
       et.M = M - (int)r;
-      et.C = (char*)e.C + r * e.ldc * 2;  // (bf16 outputs only)
-      if (e.res) et.res = (const char*)e.res + r * e.ldr * 2;
-      if (e.aux) et.aux = (const char*)e.aux + r * e.ldx * 2;
-      if (e.pre) et.pre = (char*)e.pre + r * e.ldx * 2;
+      et.C = (char*)e.C + r * e.ldc * es;
+      if (e.res) et.res = (const char*)e.res + r * e.ldr * es;
+      if (e.aux) et.aux = (const char*)e.aux + r * e.ldx * es;
+      if (e.pre) et.pre = (char*)e.pre + r * e.ldx * es;
       const int64_t n8 = (int64_t)et.M * N / 8;
       const int g = (int)std::min<int64_t>(2048, (n8 + 255) / 256);
-      hipLaunchKernelGGL(splitk_reduce_kernel<bf16>, dim3(g), dim3(256), 0, st, (const float*)ws, tail_splits, et);
+      if (out_dtype == CAPK_BF16)
+        hipLaunchKernelGGL(splitk_reduce_kernel<bf16>, dim3(g), dim3(256), 0, st, (const float*)ws, tail_splits, et);
+      else
+        hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)ws, tail_splits, et);
       CAPK_LAUNCH_CHECK("splitk_reduce_kernel");
     }
   } else if (cfg == 5) {
@@ -591,6 +593,35 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
     CAPK_LAUNCH_CHECK("splitk_reduce_kernel");
   }
   return CAPK_OK;
+}
+
+// The LM head with the shifted cross entropy's forward folded into its epilogue: C = x W^T + b
+// (bf16) and, from the same registers, per (row, column tile, wave) the (max, sum 2^(t - max))
+// pair of t = log2(e) * bf16(C) over the wave's 64 columns below V -- the softmax partials that
+// capk_ce_lse_fwd merges into each row's log-sum-exp, so the [rows, Vp] logits are not re-read
+// for the loss.  Persistent-kernel grids only (the config-3 LM head: 20 x 197 tiles); any other
+// shape runs capk_gemm and reports *done = 0 (the caller then uses capk_shifted_ce).
+extern "C" size_t capk_linear_lse_part_bytes(int M, int N) { return (size_t)cdiv(N, 256) * 4 * M * 2 * sizeof(float); }
+
+extern "C" int capk_linear_lse(int M, int N, int K, const void* x, int64_t ldx, const void* w, int64_t ldw,
+                               const float* bias, void* C, int64_t ldc, int V, float* part, size_t part_bytes,
+                               int* done, void* ws, size_t ws_bytes, void* stream) {
+  CAPK_CHECK_ARG(M > 0 && N > 0 && K > 0 && x && w && C && part && done && V > 0 && V <= N,
+                 "capk_linear_lse: bad arguments");
+  CAPK_CHECK_ARG(part_bytes >= capk_linear_lse_part_bytes(M, N), "capk_linear_lse: partials buffer too small");
+  *done = 0;
+  const bool fits = K % 64 == 0 && cdiv(K, 64) >= 2 && N % 8 == 0 && ldx % 8 == 0 && ldw % 8 == 0 && ldc % 8 == 0 &&
+                    (uintptr_t)x % 16 == 0 && (uintptr_t)w % 16 == 0 && (uintptr_t)C % 16 == 0 &&
+                    choose_cfg(M, N, K, 1, 1, 0) == 6 && tiles_of(6, M, N) > 256;
+  if (!fits)
+    return capk_gemm(CAPK_BF16, CAPK_BF16, M, N, K, x, ldx, 1, w, ldw, 1, C, ldc, 1.f, 0.f, bias, nullptr, 0, 0, nullptr,
+                     nullptr, 0, 0.f, 0, ws, ws_bytes, stream);
+  Epi e{C, ldc, 1.f, 0.f, bias, nullptr, 0, 0, nullptr, nullptr, 0, M, N, make_drop(0.f, 0)};
+  g_last_cfg = 6;
+  const int rc = launch_gemm8q(true, true, false, x, ldx, w, ldw, M, N, K, 1, e, nullptr, S(stream), nullptr, nullptr,
+                               0, nullptr, nullptr, part, V);
+  if (rc == CAPK_OK) *done = 1;
+  return rc;
 }
 
 // Two-segment products into fp32 split-K slabs, no epilogue: the LSTM recurrences, whose

@@ -104,6 +104,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, int64_t
 }
 
 constexpr uint32_t OOR = 0x80000000u;  // a buffer offset past every descriptor's range: dropped / reads 0
+constexpr float kLog2eG = 1.4426950408889634f;
+// 2^x on v_exp_f32 (x <= 0 or -inf -> 0; NaN only from -inf - -inf, which the callers exclude)
+__device__ __forceinline__ float fexp2s(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // side operand kind (at most one per launch: gemm8q_supports)
 enum { SIDE_NONE = 0, SIDE_AUX = 1, SIDE_RES = 2, SIDE_C = 3 };
@@ -120,6 +123,8 @@ struct Epi8q {
   float* dsum;  // DSUM kernels: column-sum partials [2 * tile rows][N]
   float* tail_ws;  // TAIL kernels: fp32 slabs [splits][M - 256 tail_r0][N] of the tail row blocks
   int tail_r0, tail_splits;
+  float* lse_part;  // LSEP kernels: softmax partials [ntn * 4][M] of (max, sum exp) pairs (float2)
+  int lse_v;        // LSEP: columns >= lse_v are padding (excluded from the partials)
   int group;  // grouped raster: tiles of the whole-item rows in groups of `group` row blocks, column-major
               // inside a group (0: row-major); host: gemm8q_group()
   unsigned long long* trace;  // CAPK_DIAG_TRACE builds only: per-item timestamps
@@ -143,7 +148,8 @@ __device__ __forceinline__ void wait_le(int n) {
 // DSUM: also the column sums of the final values (the bias gradient of the Linear whose
 // output gradient this dX is): per (tile row, wm) partial rows [2 ntm][N] into e.dsum,
 // summed in a fixed order by colsum_finish (capk_gemm_dx_act_colsum).
-template <bool AK, bool BK, typename OutT, int ACT, bool DV, int SK, bool DSUM = false, bool TAIL = false>
+template <bool AK, bool BK, typename OutT, int ACT, bool DV, int SK, bool DSUM = false, bool TAIL = false,
+          bool LSEP = false>
 __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A, int64_t lda,
                                                      const void* __restrict__ B, int64_t ldb, int M, int N, int K,
                                                      int splits, Epi8q e) {
@@ -215,7 +221,8 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     vo[2][p] = piece_voff<BK, 2>(wave * 2 + p, lane, 0, 1 << 30, ldb);
     vo[3][p] = piece_voff<BK, 2>(wave * 2 + p, lane, 128, 1 << 30, ldb);
   }
-  auto load = [&](int h, const Item& it, int k, int u) {
+  // piece p (0, 1) of this wave's share of half h of K-tile k of item `it` into stage u & 1
+  auto load_piece = [&](int h, const Item& it, int k, int u, int p) {
     char* dst = smem + (u & 1) * STAGE + h * HALF;
 #if defined(CAPK_DIAG_ROW0)  // diagnostic build: every item reads the A rows of tile row 0 (L2-resident)
     const uint32_t so = h < 2 ? (uint32_t)(it.kb + k) * kstepA : (uint32_t)it.n0 * rowB + (uint32_t)(it.kb + k) * kstepB;
@@ -223,11 +230,13 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     const uint32_t so = h < 2 ? (uint32_t)it.m0 * rowA + (uint32_t)(it.kb + k) * kstepA
                               : (uint32_t)it.n0 * rowB + (uint32_t)(it.kb + k) * kstepB;
 #endif
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(h < 2 ? rsA : rsB,
-                                               (__attribute__((address_space(3))) void*)(dst + (wave * 2 + p) * 1024),
-                                               16, vo[h][p] + so, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(h < 2 ? rsA : rsB,
+                                             (__attribute__((address_space(3))) void*)(dst + (wave * 2 + p) * 1024),
+                                             16, vo[h][p] + so, 0, 0, 0);
+  };
+  auto load = [&](int h, const Item& it, int k, int u) {
+    load_piece(h, it, k, u, 0);
+    load_piece(h, it, k, u, 1);
   };
   const bool has_bias = e.bias != nullptr;
   // the wave's 64 bias columns of item j (lane l: column (l >> 5) * 128 + wn * 32 + (l & 31))
@@ -336,6 +345,14 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     }
     const __amdgpu_buffer_rsrc_t rsC = rsrc_of(e.C, (int64_t)M * e.ldc * ESZ);
     const uint32_t o0 = lane_off(e.ldc, ESZ, 0), o1 = lane_off(e.ldc, ESZ, 1);
+    // LSEP: per row i of the lane, running (max, sum exp) over its columns, in the log2 domain
+    // (values scaled by log2 e), of the stored (bf16-rounded) logits
+    float lm[4], ls[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      lm[i] = -INFINITY;
+      ls[i] = 0.f;
+    }
     const uint32_t p0 = has_pre ? lane_off(e.ldp, ESZ, 0) : OOR, p1 = has_pre ? lane_off(e.ldp, ESZ, 1) : OOR;
     // one 16-row x 32-column segment (qm, qn, i), unrolled by hand (the 16 bodies exceed the
     // unroller's budget, and a rolled loop would index the accumulators dynamically)
@@ -399,6 +416,22 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
 #pragma unroll
         for (int k = 0; k < 8; ++k) cs[qn][k] += row_ok ? v[k] : 0.f;
       }
+      if constexpr (LSEP) {
+        const int n = c.n0 + qn * 128 + lcol;
+        float t[8], mx = lm[i];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          t[k] = n + k < e.lse_v ? (float)(bf16)v[k] * kLog2eG : -INFINITY;
+          mx = fmaxf(mx, t[k]);
+        }
+        if (mx != -INFINITY) {  // (a lane whose columns are all padding keeps (-inf, 0))
+          float sm = ls[i] * fexp2s(lm[i] - mx);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) sm += fexp2s(t[k] - mx);
+          lm[i] = mx;
+          ls[i] = sm;
+        }
+      }
 #if defined(CAPK_DIAG_NOSTORE)  // diagnostic build: the stores issue but are dropped (range check)
       store8(rsC, OOR, v, (OutT*)nullptr);
 #else
@@ -417,7 +450,30 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     // memory instructions issued after the last wait (the stores): per segment one (bf16) or
     // two (fp32) for C, the same again for the pre-activation (dropped when not kept)
     constexpr int per = ESZ == 2 ? 1 : 2;
-    return 8 * per * (ACT != 0 ? 2 : 1);
+    int nst = 8 * per * (ACT != 0 ? 2 : 1);
+    if constexpr (LSEP) {
+      // the lane's rows (i) now hold (max, sum exp) over its 16 columns; merge the four column
+      // groups of the wave (lanes l ^ 16, l ^ 32), then lanes 0-15 store the wave's partial for
+      // its 64 columns: part[(tn * 4 + wn) * M + row]
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int x = 16; x <= 32; x <<= 1) {
+          const float mo = __shfl_xor(lm[i], x, 64), so = __shfl_xor(ls[i], x, 64);
+          const float mn = fmaxf(lm[i], mo);
+          ls[i] = mn == -INFINITY ? 0.f : ls[i] * fexp2s(lm[i] - mn) + so * fexp2s(mo - mn);
+          lm[i] = mn;
+        }
+        const int row = c.m0 + QM * 128 + wm * 64 + i * 16 + (lane & 15);
+        const int64_t pidx = (int64_t)((c.n0 >> 8) * 4 + wn) * M + row;
+        const uint32_t off = (lane < 16 && row < M) ? (uint32_t)(pidx * 8) : OOR;
+        const __amdgpu_buffer_rsrc_t rsP = rsrc_of(e.lse_part, (int64_t)((N + 255) / 256) * 4 * M * 8);
+        __builtin_amdgcn_raw_buffer_store_b64(
+            (__attribute__((ext_vector_type(2))) unsigned){__float_as_uint(lm[i]), __float_as_uint(ls[i])}, rsP, off, 0, 0);
+      }
+      nst += 4;
+    }
+    return nst;
   };
   // The item's epilogue, one quadrant row (half) at a time; a side operand (residual / aux /
   // C) is loaded per half, 8 segments in flight, one wait (the first also retires the next
@@ -546,6 +602,7 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
   Item cur = item_at(0), nxt = item_at(nseg > 1 ? 1 : 0);
   int j = 0, k = TAIL ? cur.k0 : 0;
   zero_acc();
+  bf16x8 fa[2][4], fb0[2][2], fb1[2][2];
   // prologue: A0 B0 B1 (+bias) of step 0, A1 of step 0, A0 B0 B1 of step 1
   load(0, cur, k, 0);
   load(2, cur, k, 0);
@@ -561,7 +618,6 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
   int S = 0;        // stores left in flight by the last epilogue (k == 0 phases only)
   int q2prev = 6;   // loads issued by the previous Q2 (prologue: step 1's three halves)
 
-  bf16x8 fa[2][4], fb0[2][2], fb1[2][2];
   for (int u = 0;; ++u) {
     const bool has1 = u + 1 < total, has2 = u + 2 < total;
     // Q1: (0,0), (0,1).  L: read A0, B0, B1 (u); wait A1 (u); issue A1 (u+1)
@@ -578,10 +634,9 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
       else wait_le(n1);
     }
     if (k == k0c) stamp(j, 2);
-    if (has1) {
-      if (k + 1 < kend) load(1, cur, k + 1, u + 1);
-      else load(1, nxt, kbn, u + 1);
-    }
+    const Item& t1 = k + 1 < kend ? cur : nxt;
+    const int k1n = k + 1 < kend ? k + 1 : kbn;
+    if (has1) load(1, t1, k1n, u + 1);
     lds_done();
     bar();
     if (k == k0c) stamp(j, 3);
@@ -596,15 +651,15 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     if (q1n + e1 == 2) wait_vmc<2>();
     else wait_le(q1n + e1);
     q2prev = 0;
+    const bool same2 = k + 2 < kend;
+    const int k2 = same2 ? k + 2 : kbn + (k + 2 - kend);
+    const Item& t2 = same2 ? cur : nxt;
     if (has2) {
-      const bool same = k + 2 < kend;
-      const int k2 = same ? k + 2 : kbn + (k + 2 - kend);
-      const Item& t2 = same ? cur : nxt;
       load(0, t2, k2, u + 2);
       load(2, t2, k2, u + 2);
       load(3, t2, k2, u + 2);
       q2prev = 6;
-      if ((TAIL ? !same && k + 2 == kend : k2 == 0) && has_bias) {  // the next segment's first K-tile
+      if ((TAIL ? !same2 && k + 2 == kend : k2 == 0) && has_bias) {  // the next segment's first K-tile
         bias_dma(t2, j + 1);
         q2prev = 7;
       }
@@ -721,7 +776,7 @@ int gemm8q_group(int ntm, int ntn) {
 
 int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int64_t lda, const void* B, int64_t ldb,
                   int M, int N, int K, int splits, const Epi& e, float* slab, hipStream_t st, float* dsum,
-                  void* ws, size_t ws_bytes, int* tail_r0, int* tail_splits) {
+                  void* ws, size_t ws_bytes, int* tail_r0, int* tail_splits, float* lse_part, int lse_v) {
   CAPK_CHECK_ARG((a_kmajor ? (int64_t)M * lda : (int64_t)K * lda) * 2 < (1ll << 31) &&
                      (b_kmajor ? (int64_t)N * ldb : (int64_t)K * ldb) * 2 < (1ll << 31),
                  "capk_gemm(bf16, 256x256): operand larger than 2 GiB");
@@ -758,11 +813,11 @@ int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int
                  "capk_gemm(bf16, 256x256): output or side operand larger than 2 GiB");
   const int items = cdiv(M, 256) * cdiv(N, 256);
   CAPK_CHECK_ARG(items > 256, "capk_gemm(gemm8q): persistent kernel for grids of more than 256 items");
-  // the split-K tail round (not the DSUM form; bf16 outputs): the caller reduces the slabs
+  // the split-K tail round (not the DSUM form): the caller reduces the slabs
   if (tail_r0) *tail_r0 = -1;
   {
     int r0, S;
-    if (tail_r0 && ws && !dsum && !out_f32 && gemm8q_tail_plan(M, N, K, &r0, &S) &&
+    if (tail_r0 && ws && !dsum && !lse_part && gemm8q_tail_plan(M, N, K, &r0, &S) &&
         ws_bytes >= (size_t)S * (size_t)(M - r0 * 256) * N * sizeof(float)) {
       p.tail_ws = (float*)ws;
       p.tail_r0 = r0;
@@ -782,7 +837,7 @@ int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int
   const dim3 grid(256), block(512);
 #define L8(AK, BKM, OT, ACTK, DVK, SKK, DS)                                                                        \
   do {                                                                                                          \
-    constexpr bool TAILV = std::is_same<OT, bf16>::value && !DS;                                                \
+    constexpr bool TAILV = !DS;                                                                                 \
     if (TAILV && p.tail_ws)                                                                                     \
       hipLaunchKernelGGL((gemm8q_kernel<AK, BKM, OT, ACTK, DVK, SKK, DS, TAILV>), grid, block, 0, st, A, lda, B, \
                          ldb, M, N, K, 1, p);                                                                   \
@@ -800,7 +855,14 @@ int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int
 #define L8ACT(ACTK)                                        \
   if (dv) L8(true, true, bf16, ACTK, true, SIDE_NONE, false); \
   else L8(true, true, bf16, ACTK, false, SIDE_NONE, false);
-  if (dsum) {  // dX with the backward-activation multiply + column sums (capk_gemm_dx_act_colsum)
+  if (lse_part) {  // the LM head with the shifted CE's softmax partials (capk_linear_lse)
+    CAPK_CHECK_ARG(a_kmajor && b_kmajor && !out_f32 && sk == SIDE_NONE && !fwd_act && !dsum,
+                   "capk_gemm(gemm8q): softmax partials only on a plain K-major bf16 product");
+    p.lse_part = lse_part;
+    p.lse_v = lse_v;
+    hipLaunchKernelGGL((gemm8q_kernel<true, true, bf16, 0, false, SIDE_NONE, false, false, true>), grid, block, 0, st,
+                       A, lda, B, ldb, M, N, K, 1, p);
+  } else if (dsum) {  // dX with the backward-activation multiply + column sums (capk_gemm_dx_act_colsum)
     CAPK_CHECK_ARG(a_kmajor && !b_kmajor && !out_f32 && sk == SIDE_AUX,
                    "capk_gemm(gemm8q): column sums only on the dX x act' product");
     p.dsum = dsum;

@@ -340,13 +340,17 @@ bool gemm8q_supports(const Epi& e, bool out_f32);
 int launch_colsum_finish(int parts, int N, const float* part, float* out, int accumulate, hipStream_t st);
 // dsum != nullptr: the dX x act' product also writes per-(tile row, wave row) column-sum
 // partials [2 * cdiv(M, 256)][N] fp32 there (capk_gemm_dx_act_colsum)
+// lse_part != nullptr (plain K-major bf16 products; no tail round): also the softmax partials of
+// the stored C over columns < lse_v, [cdiv(N, 256) * 4][M] (max, sum exp) pairs in the log2
+// domain (capk_linear_lse)
 // tail_r0 != nullptr and ws of gemm8q_tail_workspace() bytes: the split-K tail round when
 // gemm8q_tail_plan() picks one -- then *tail_r0 >= 0 and the caller must reduce the fp32
 // slabs ws[*tail_splits][M - 256 *tail_r0][N] into rows [256 *tail_r0, M) with the epilogue
 // (splitk_reduce_kernel); otherwise *tail_r0 = -1 and the launch wrote every row
 int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int64_t lda, const void* B, int64_t ldb,
                   int M, int N, int K, int splits, const Epi& e, float* slab, hipStream_t st, float* dsum = nullptr,
-                  void* ws = nullptr, size_t ws_bytes = 0, int* tail_r0 = nullptr, int* tail_splits = nullptr);
+                  void* ws = nullptr, size_t ws_bytes = 0, int* tail_r0 = nullptr, int* tail_splits = nullptr,
+                  float* lse_part = nullptr, int lse_v = 0);
 bool gemm8q_tail_plan(int M, int N, int K, int* r0, int* splits);
 size_t gemm8q_tail_workspace(int M, int N, int K);
 

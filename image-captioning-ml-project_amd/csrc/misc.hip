@@ -212,6 +212,103 @@ __global__ void ce_finish_kernel(int rows, const float* __restrict__ row_loss, c
   }
 }
 
+// ------------------------------------- shifted CE from the LM head's partials --------
+// capk_linear_lse leaves per row P = 4 cdiv(Vp, 256) pairs (max, sum 2^(t - max)) of
+// t = log2(e) * logit over disjoint column ranges.  Forward: four waves per 64 rows, each wave
+// merging a quarter of the partials (lane = row: coalesced 8-B reads), combined through LDS
+// into lse (natural log) and the row loss lse - logit[target].  Backward: one streaming pass,
+// dlogits = (2^(t - lse log2 e) - [col == target]) * grad_scale / count with the column sums of
+// the stored gradient (the LM-head bias gradient) as per-row-group partials.
+__global__ __launch_bounds__(256) void ce_lse_merge_kernel(int B, int T_, int M, int P, const float2* __restrict__ part,
+                                                           const bf16* __restrict__ logits, int64_t ld,
+                                                           const int64_t* __restrict__ targets, int ignore_index,
+                                                           float* __restrict__ lse_out, float* __restrict__ row_loss) {
+  __shared__ float red[2][4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int row = blockIdx.x * 64 + lane;
+  const int p0 = w * P / 4, p1 = (w + 1) * P / 4;
+  float m = -INFINITY, sum = 0.f;
+  if (row < M) {
+#pragma unroll 4
+    for (int p = p0; p < p1; ++p) {
+      const float2 q = part[(int64_t)p * M + row];
+      if (q.x == -INFINITY) continue;  // a wave whose columns were all padding
+      const float mn = fmaxf(m, q.x);
+      sum = sum * __builtin_amdgcn_exp2f(m - mn) + q.y * __builtin_amdgcn_exp2f(q.x - mn);
+      m = mn;
+    }
+  }
+  red[0][w][lane] = m;
+  red[1][w][lane] = sum;
+  __syncthreads();
+  if (w == 0 && row < M) {
+    float mm = -INFINITY, ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float mi = red[0][i][lane], si = red[1][i][lane];
+      if (mi == -INFINITY) continue;
+      const float mn = fmaxf(mm, mi);
+      ss = ss * __builtin_amdgcn_exp2f(mm - mn) + si * __builtin_amdgcn_exp2f(mi - mn);
+      mm = mn;
+    }
+    const float lse = (mm + __log2f(ss)) * 0.6931471805599453f;
+    lse_out[row] = lse;
+    const int b = row / T_, t = row % T_;
+    const int64_t tgt = (t < T_ - 1) ? targets[(int64_t)b * T_ + t + 1] : (int64_t)ignore_index;
+    row_loss[row] = tgt != ignore_index ? lse - (float)logits[(int64_t)row * ld + tgt] : 0.f;
+  }
+}
+
+constexpr int CEB_ROWS = 128;  // rows per block of the backward pass (one column-sum partial row each)
+template <typename T>
+__global__ __launch_bounds__(256) void ce_lse_bwd_kernel(int B, int T_, int V, int64_t ld, const T* __restrict__ logits,
+                                                         const int64_t* __restrict__ targets, int ignore_index,
+                                                         const float* __restrict__ lse, const float* __restrict__ cnt,
+                                                         const float* __restrict__ grad_scale, T* __restrict__ dlogits,
+                                                         float* __restrict__ dbias_part) {
+  __shared__ float lse_s[CEB_ROWS];
+  __shared__ int tgt_s[CEB_ROWS];
+  const int M = B * T_;
+  const int r0 = blockIdx.y * CEB_ROWS, nr = min(CEB_ROWS, M - r0);
+  for (int i = threadIdx.x; i < nr; i += blockDim.x) {
+    const int row = r0 + i, b = row / T_, t = row % T_;
+    const int64_t tgt = (t < T_ - 1) ? targets[(int64_t)b * T_ + t + 1] : (int64_t)ignore_index;
+    tgt_s[i] = tgt != ignore_index ? (int)tgt : -1;  // -1: not counted (the whole row's gradient is 0)
+    lse_s[i] = lse[row] * 1.4426950408889634f;
+  }
+  __syncthreads();
+  const float scale = (grad_scale ? grad_scale[0] : 1.f) / cnt[0];
+  const int c8 = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (c8 >= ld) return;
+  float cs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < nr; ++i) {
+    const int row = r0 + i, tg = tgt_s[i];
+    float g[8];
+    if (tg < 0) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] = 0.f;
+    } else {
+      float l[8];
+      Vec8<T>::load(logits + (int64_t)row * ld + c8, l);
+      const float ls = lse_s[i];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int col = c8 + k;
+        const float pr = __builtin_amdgcn_exp2f(fmaf(l[k], 1.4426950408889634f, -ls));
+        g[k] = col < V ? (pr - (col == tg ? 1.f : 0.f)) * scale : 0.f;
+      }
+    }
+    Vec8<T>::store(dlogits + (int64_t)row * ld + c8, g);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cs[k] += to_f32(from_f32<T>(g[k]));  // the stored (rounded) values
+  }
+  if (dbias_part) {
+    float* dst = dbias_part + (int64_t)blockIdx.y * ld + c8;
+    *(f32x4*)dst = (f32x4){cs[0], cs[1], cs[2], cs[3]};
+    *(f32x4*)(dst + 4) = (f32x4){cs[4], cs[5], cs[6], cs[7]};
+  }
+}
+
 // ------------------------------------------------------------ colsum --------
 constexpr int CS_ROWS_PER_SPLIT = 256;
 template <typename T>
@@ -614,6 +711,50 @@ static int shifted_ce_impl(const float* row_weight, int dtype, int B, int T, int
     hipLaunchKernelGGL(ce_finish_kernel, dim3(1), dim3(1024), 0, st, B * T, row_loss, cnt, loss_out);
     CAPK_LAUNCH_CHECK("ce_finish_kernel");
   }
+  return CAPK_OK;
+}
+
+extern "C" size_t capk_ce_lse_workspace(int B, int T, int64_t ld) {
+  const int M = B * T;
+  return (size_t)(4 + M) * sizeof(float) + (size_t)cdiv(M, CEB_ROWS) * ld * sizeof(float);
+}
+
+extern "C" int capk_ce_lse_fwd(int B, int T, int V, int64_t ld, const void* logits, const int64_t* targets,
+                               int ignore_index, const float* part, int nparts, float* lse_out, float* loss_out,
+                               void* ws, size_t ws_bytes, void* stream) {
+  CAPK_CHECK_ARG(B > 0 && T > 1 && V > 0 && ld >= V && logits && targets && part && nparts > 0 && lse_out && loss_out,
+                 "capk_ce_lse_fwd: bad arguments");
+  CAPK_CHECK_ARG(ws && ws_bytes >= capk_ce_lse_workspace(B, T, ld), "capk_ce_lse_fwd: workspace too small");
+  const int M = B * T;
+  float* cnt = (float*)ws;
+  float* row_loss = cnt + 4;
+  hipStream_t st = S(stream);
+  hipLaunchKernelGGL(ce_count_kernel, dim3(1), dim3(1024), 0, st, B, T, targets, ignore_index, cnt);
+  CAPK_LAUNCH_CHECK("ce_count_kernel");
+  hipLaunchKernelGGL(ce_lse_merge_kernel, dim3(cdiv(M, 64)), dim3(256), 0, st, B, T, M, nparts, (const float2*)part,
+                     (const bf16*)logits, ld, targets, ignore_index, lse_out, row_loss);
+  CAPK_LAUNCH_CHECK("ce_lse_merge_kernel");
+  hipLaunchKernelGGL(ce_finish_kernel, dim3(1), dim3(1024), 0, st, M, row_loss, cnt, loss_out);
+  CAPK_LAUNCH_CHECK("ce_finish_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_ce_lse_bwd(int dtype, int B, int T, int V, int64_t ld, const void* logits, const int64_t* targets,
+                               int ignore_index, const float* lse, const float* cnt, const float* grad_scale,
+                               void* dlogits, float* dbias, void* ws, size_t ws_bytes, void* stream) {
+  CAPK_CHECK_ARG(B > 0 && T > 1 && V > 0 && ld >= V && ld % 8 == 0 && logits && targets && lse && cnt && dlogits,
+                 "capk_ce_lse_bwd: bad arguments");
+  CAPK_CHECK_ARG(((uintptr_t)logits % 16 == 0) && ((uintptr_t)dlogits % 16 == 0), "capk_ce_lse_bwd: alignment");
+  CAPK_CHECK_ARG(!dbias || (ws && ws_bytes >= capk_ce_lse_workspace(B, T, ld)), "capk_ce_lse_bwd: workspace too small");
+  const int M = B * T, groups = cdiv(M, CEB_ROWS);
+  float* dpart = dbias ? (float*)ws + 4 + M : nullptr;
+  hipStream_t st = S(stream);
+  const dim3 grid(cdiv((int)(ld / 8), 256), groups);
+#define L(T_, _) hipLaunchKernelGGL(ce_lse_bwd_kernel<T_>, grid, dim3(256), 0, st, B, T, V, ld, (const T_*)logits, targets, ignore_index, lse, cnt, grad_scale, (T_*)dlogits, dpart)
+  DT_DISPATCH(dtype, L, 0)
+#undef L
+  CAPK_LAUNCH_CHECK("ce_lse_bwd_kernel");
+  if (dbias) return launch_colsum_finish(groups, (int)ld, dpart, dbias, 0, st);
   return CAPK_OK;
 }
 

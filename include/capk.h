@@ -287,6 +287,27 @@ int capk_shifted_ce_weighted(int dtype, int B, int T, int V, int64_t ld, const v
                              const int64_t* targets, int ignore_index, const float* row_weight,
                              const float* grad_scale, float* loss_out, void* dlogits, void* ws, size_t ws_bytes,
                              void* stream);
+/* The shifted cross entropy with its forward folded into the LM head (config-3 training, bf16):
+ * capk_linear_lse computes C = x W^T + b (src/models/decoders.py:431, output_layer) and, from
+ * the epilogue registers, softmax partials part[P = 4 cdiv(N, 256)][M] of (max, sum 2^(t - max))
+ * over t = log2(e) * bf16(C[row, n]), n < V (capk_linear_lse_part_bytes); *done = 0 when the
+ * shape does not take the persistent kernel (C is then plain capk_gemm output and the caller
+ * uses capk_shifted_ce).  capk_ce_lse_fwd merges the partials: lse_out[row] (natural log) and
+ * loss_out = (mean, count) as capk_shifted_ce.  capk_ce_lse_bwd writes d(loss)/d(logits) *
+ * (*grad_scale) from the logits and lse in one pass (count: DEVICE pointer, loss_out + 1), and,
+ * if dbias != NULL, the column sums of that gradient over its ld columns (the LM-head bias
+ * gradient, written, not accumulated). */
+size_t capk_linear_lse_part_bytes(int M, int N);
+int capk_linear_lse(int M, int N, int K, const void* x, int64_t ldx, const void* w, int64_t ldw,
+                    const float* bias, void* C, int64_t ldc, int V, float* part, size_t part_bytes,
+                    int* done, void* ws, size_t ws_bytes, void* stream);
+size_t capk_ce_lse_workspace(int B, int T, int64_t ld);
+int capk_ce_lse_fwd(int B, int T, int V, int64_t ld, const void* logits, const int64_t* targets,
+                    int ignore_index, const float* part, int nparts, float* lse_out, float* loss_out,
+                    void* ws, size_t ws_bytes, void* stream);
+int capk_ce_lse_bwd(int dtype, int B, int T, int V, int64_t ld, const void* logits, const int64_t* targets,
+                    int ignore_index, const float* lse, const float* cnt, const float* grad_scale,
+                    void* dlogits, float* dbias, void* ws, size_t ws_bytes, void* stream);
 /* hipMemsetAsync(ptr, 0, bytes) on the stream (gradient buffers that are scatter-added). */
 int capk_zero(void* ptr, size_t bytes, void* stream);
 

@@ -41,6 +41,27 @@ if [[ ,$S, == *,benchab,* ]]; then  # config-3 bench under two environments, ABA
     echo "B$i $(grep -o '"value": [0-9.]*' $OUT/benchab_B$i.log | head -1)"
   done
 fi
+if [[ ,$S, == *,libtest,* ]]; then  # GEMM tests on every library of LIBS (diagnostic / experimental builds)
+  for L in ${LIBS}; do
+    CAPK_LIB_PATH=$PWD/image-captioning-ml-project_amd/capk/$L run libtest_$L 300 $PYT tests/test_gpu_gemm.py
+  done
+fi
+if [[ ,$S, == *,libab,* ]]; then  # tools/gemm_bench.py per library, libraries alternated, 2 rounds
+  for r in 1 2; do
+    for L in libcapk.so ${LIBS}; do
+      CAPK_LIB_PATH=$PWD/image-captioning-ml-project_amd/capk/$L GEMM_GRAPH=1 run libab_${L}_$r 200 python -u tools/gemm_bench.py
+    done
+  done
+  for L in libcapk.so ${LIBS}; do echo "== $L"; grep -h TFLOP $OUT/libab_${L}_*.log | sort | awk '{print}'; done > $OUT/libab_table.txt
+fi
+if [[ ,$S, == *,libbench,* ]]; then  # config-3 bench per library, alternated, 2 rounds
+  for r in 1 2; do
+    for L in libcapk.so ${LIBS}; do
+      CAPK_LIB_PATH=$PWD/image-captioning-ml-project_amd/capk/$L $B3 > $OUT/libbench_${L}_$r.log 2>&1 || { echo "$L failed"; tail -5 $OUT/libbench_${L}_$r.log; exit 1; }
+      echo "$L $r $(grep -o '"value": [0-9.]*' $OUT/libbench_${L}_$r.log | head -1)"
+    done
+  done
+fi
 [[ ,$S, == *,bench3,* ]] && run bench_config3 480 python bench.py --steps 10 --warmup 3
 [[ ,$S, == *,bench3q,* ]] && run bench_config3q 300 $B3
 [[ ,$S, == *,bench5,* ]] && run bench_config5 480 python bench.py --workload config5 --steps 5 --warmup 2

@@ -279,6 +279,13 @@ def test_grouped_raster_exact(group, tail):
         C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         ops.gemm(a, True, w, True, M, N, K, C, lda=K, ldb=K, ldc=N, bias=bias, residual=res, ldr=N)
         assert torch.equal(C.float(), (ref + bias + res.float()).bfloat16().float())
+        # fp32 outputs (the LM-head weight gradient's form: both operands MN-major), with the
+        # split-K tail round reduced by the fp32 reduce
+        C32 = torch.empty(M, N, device="cuda", dtype=torch.float32)
+        at, wt_ = a.t().contiguous(), w.t().contiguous()
+        ops.gemm(at, False, wt_, False, M, N, K, C32, lda=at.stride(0), ldb=wt_.stride(0), ldc=N)
+        assert L.capk_gemm_last_config() == 6
+        assert torch.equal(C32, ref)
         # DSUM: dX = dY W (W [K', N'] N-major) times aux, plus the column sums (fixed order)
         dy = torch.randint(-2, 3, (M, K), device="cuda", generator=g).bfloat16()
         wt = torch.randint(-2, 3, (K, N), device="cuda", generator=g).bfloat16()

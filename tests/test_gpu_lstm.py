@@ -133,7 +133,7 @@ def _full_lstm(precision, kind="soft", heads=1, seed=21, embedding_dim=None):
     import capk
     from capk import config as C
     from capk.models.decoders import build_decoder
-    from capk.models.lstm import LSTMDecoder
+    from capk.models.decoders import LSTMDecoder
     torch.manual_seed(seed)
     V, pad = 50257, 50256
     dcfg = C.DecoderConfig(decoder_type="lstm", hidden_dim=768, num_layers=6, num_heads=heads)

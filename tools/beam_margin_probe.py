@@ -1,0 +1,35 @@
+"""Stable coverage of the bf16-vs-fp32 beam-5 precision check (tests/test_gpu_beam.py
+_bf16_vs_fp32_margins) for several peaked-LM-head settings of the config-3 model, 256 images.
+PROBE_SETTINGS="n_hot:gain:eos_hot:round_bf16;..." overrides the list."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "image-captioning-ml-project_amd"), os.path.join(ROOT, "tests")):
+    sys.path.insert(0, p)
+import torch  # noqa: E402
+
+import test_gpu_beam as tb  # noqa: E402
+
+DEFAULT = "64:40:0:0;64:40:0:1;16:40:0:1;16:80:1:1;8:80:1:1;4:120:1:1"
+
+
+def main():
+    B = int(os.environ.get("PROBE_B", "256"))
+    images = torch.randn(B, 3, 224, 224, generator=torch.Generator().manual_seed(3)).cuda()
+    for item in os.environ.get("PROBE_SETTINGS", DEFAULT).split(";"):
+        n_hot, gain, eos_hot, rb = item.split(":")
+        kw = dict(n_hot=int(n_hot), gain=float(gain), eos_hot=eos_hot == "1", round_bf16=rb == "1")
+        m32, cfg = tb._config3_peaked("fp32", **kw)
+        m16, _ = tb._config3_peaked("bf16", **kw)
+        same, stable, ids16, err = tb._bf16_vs_fp32_margins(m32, m16, cfg, images)
+        lens = (ids16 != cfg.model.pad_token_id).sum(1).float()
+        print(f"{kw}: identical {float(same.float().mean()):.3f}  stable {float(stable.float().mean()):.3f}  "
+              f"stable&different {int((stable & ~same).sum())}  median err {float(err.median()):.4f}  "
+              f"mean output length {float(lens.mean()):.1f}", flush=True)
+        del m32, m16
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
