@@ -77,6 +77,7 @@ SIGNATURES = {
     "capk_shifted_ce_workspace": (_sz, [_i, _i]),
     "capk_shifted_ce": (_i, [_i, _i, _i, _i, _i64, _c_p, _c_p, _i, _c_p, _c_p, _c_p, _c_p, _sz, _c_p]),
     "capk_shifted_ce_weighted": (_i, [_i, _i, _i, _i, _i64, _c_p, _c_p, _i, _c_p, _c_p, _c_p, _c_p, _c_p, _sz, _c_p]),
+    "capk_zero_gap_rows": (_i, [_c_p, _i64, _i64, _i, _i, _i, _i, _c_p]),
     "capk_linear_lse_part_bytes": (_sz, [_i, _i]),
     "capk_linear_lse": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p, _c_p, _i64, _i, _c_p, _sz, _c_p, _c_p, _sz,
                              _c_p]),

@@ -237,7 +237,7 @@ class _DecoderFn(torch.autograd.Function):
             dqc = torch.empty(BT, D, dtype=dt, device=dev)
             dkv = torch.empty(M_ext, 2 * D, dtype=dt, device=dev)
             if rpb != S:
-                ops.zero_(dkv)  # gap rows (e.g. ViT CLS rows) get no K/V gradient
+                ops.zero_gap_rows(dkv, B, rpb, S)  # gap rows (e.g. ViT CLS rows) get no K/V gradient
             ops.attention_bwd(heads(qc, 0, B, T), HeadView(kv, 0, rpb * 2 * D, 2 * D),
                               HeadView(kv, D, rpb * 2 * D, 2 * D), heads(c, 0, B, T), heads(dc, 0, B, T), lse2,
                               heads(dqc, 0, B, T), HeadView(dkv, 0, rpb * 2 * D, 2 * D),

@@ -579,6 +579,13 @@ def dropout_mask(n, p, seed, offset=0, device="cuda"):
     return out
 
 
+def zero_gap_rows(t, B, rpb, S):
+    """Zero rows b * rpb + j (S <= j < rpb) of a contiguous 2-D buffer (capk_zero_gap_rows)."""
+    check(lib().capk_zero_gap_rows(_p(t), t.stride(0) * t.element_size(), t.shape[1] * t.element_size(), int(B),
+                                   int(rpb), int(S), t.shape[0], _stream()), "capk_zero_gap_rows")
+    return t
+
+
 def zero_(t):
     check(lib().capk_zero(_p(t), t.numel() * t.element_size(), _stream()), "capk_zero")
     return t

@@ -285,6 +285,10 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
         for (int j = 0; j < 2; ++j) c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[s][j], fa[s][i], c[i][j], 0, 0, 0);
   };
   auto fence = [] { __builtin_amdgcn_sched_barrier(0); };
+  // MFMA clusters at wave priority 1 (the lagging group at priority 1 throughout, or no
+  // priority changes at all, measured the same: profiles/round5/gemm_prio_ab.txt)
+  auto prio_mfma = [] { __builtin_amdgcn_s_setprio(1); };
+  auto prio_load = [] { __builtin_amdgcn_s_setprio(0); };
   auto bar = [&] {
     fence();
     raw_barrier();
@@ -640,10 +644,10 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     lds_done();
     bar();
     if (k == k0c) stamp(j, 3);
-    __builtin_amdgcn_s_setprio(1);
+    prio_mfma();
     mma(fa, fb0, acc[0][0]);
     mma(fa, fb1, acc[0][1]);
-    __builtin_amdgcn_s_setprio(0);
+    prio_load();
     bar();
     // Q2: (1,1), (1,0).  L: read A1 (u); wait A0 B0 B1 (+bias) (u+1); issue A0 B0 B1 (+bias) (u+2)
     readA(fa, u, 1);
@@ -666,10 +670,10 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     }
     lds_done();
     bar();
-    __builtin_amdgcn_s_setprio(1);
+    prio_mfma();
     mma(fa, fb1, acc[1][1]);
     mma(fa, fb0, acc[1][0]);
-    __builtin_amdgcn_s_setprio(0);
+    prio_load();
     bar();
     if (++k == kend) {  // the segment's last K-tile: epilogue, stores left in flight
       stamp(j, 0);

@@ -309,6 +309,22 @@ __global__ __launch_bounds__(256) void ce_lse_bwd_kernel(int B, int T_, int V, i
   }
 }
 
+// Zero the gap rows of a batch of strided row blocks: rows b * rpb + j for S <= j < rpb (and
+// row < rows), row_bytes from each row start -- the rows of a [B * rpb - 1, C] gradient that a
+// strided view skips (the decoder's cross-attention K / V gradient over the ViT sequence: the
+// CLS rows), instead of clearing the whole buffer.
+__global__ __launch_bounds__(256) void zero_gap_rows_kernel(char* __restrict__ base, int64_t ld_bytes, int chunks,
+                                                            int B, int rpb, int S, int rows) {
+  const int64_t total = (int64_t)B * (rpb - S) * chunks;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % chunks);
+    const int64_t g = i / chunks;
+    const int b = (int)(g / (rpb - S)), j = S + (int)(g % (rpb - S));
+    const int64_t row = (int64_t)b * rpb + j;
+    if (row < rows) *(f32x4*)(base + row * ld_bytes + (int64_t)c * 16) = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+}
+
 // ------------------------------------------------------------ colsum --------
 constexpr int CS_ROWS_PER_SPLIT = 256;
 template <typename T>
@@ -711,6 +727,20 @@ static int shifted_ce_impl(const float* row_weight, int dtype, int B, int T, int
     hipLaunchKernelGGL(ce_finish_kernel, dim3(1), dim3(1024), 0, st, B * T, row_loss, cnt, loss_out);
     CAPK_LAUNCH_CHECK("ce_finish_kernel");
   }
+  return CAPK_OK;
+}
+
+extern "C" int capk_zero_gap_rows(void* base, int64_t ld_bytes, int64_t row_bytes, int B, int rpb, int nk, int rows,
+                                  void* stream) {
+  CAPK_CHECK_ARG(base && B > 0 && nk > 0 && rpb >= nk && rows > 0 && row_bytes > 0 && row_bytes % 16 == 0 &&
+                     ld_bytes % 16 == 0 && (uintptr_t)base % 16 == 0 && row_bytes <= ld_bytes,
+                 "capk_zero_gap_rows: bad arguments");
+  if (rpb == nk) return CAPK_OK;
+  const int chunks = (int)(row_bytes / 16);
+  const int64_t total = (int64_t)B * (rpb - nk) * chunks;
+  hipLaunchKernelGGL(zero_gap_rows_kernel, dim3(grid_for(total)), dim3(256), 0, S(stream), (char*)base, ld_bytes, chunks,
+                     B, rpb, nk, rows);
+  CAPK_LAUNCH_CHECK("zero_gap_rows_kernel");
   return CAPK_OK;
 }
 

@@ -308,6 +308,11 @@ int capk_ce_lse_fwd(int B, int T, int V, int64_t ld, const void* logits, const i
 int capk_ce_lse_bwd(int dtype, int B, int T, int V, int64_t ld, const void* logits, const int64_t* targets,
                     int ignore_index, const float* lse, const float* cnt, const float* grad_scale,
                     void* dlogits, float* dbias, void* ws, size_t ws_bytes, void* stream);
+/* Zero rows b * rpb + j (S <= j < rpb, row < rows; row_bytes from each row start, rows ld_bytes
+ * apart) -- the gap rows of a strided per-image view (the cross-attention K / V gradient of
+ * src/models/decoders.py:421-428 over the ViT sequence minus its CLS rows). */
+int capk_zero_gap_rows(void* base, int64_t ld_bytes, int64_t row_bytes, int B, int rpb, int S, int rows,
+                       void* stream);
 /* hipMemsetAsync(ptr, 0, bytes) on the stream (gradient buffers that are scatter-added). */
 int capk_zero(void* ptr, size_t bytes, void* stream);
 

@@ -62,6 +62,8 @@ if [[ ,$S, == *,libbench,* ]]; then  # config-3 bench per library, alternated, 2
     done
   done
 fi
+[[ ,$S, == *,hiptrace,* ]] && run hiptrace 300 rocprofv3 --hip-trace --kernel-trace --output-format csv -d $OUT/hiptrace -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --beam-batch 0
+[[ ,$S, == *,profbeam,* ]] && run profbeam 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profbeam -o run -- python3 tools/beam_bench.py --reps 2
 [[ ,$S, == *,bench3,* ]] && run bench_config3 480 python bench.py --steps 10 --warmup 3
 [[ ,$S, == *,bench3q,* ]] && run bench_config3q 300 $B3
 [[ ,$S, == *,bench5,* ]] && run bench_config5 480 python bench.py --workload config5 --steps 5 --warmup 2

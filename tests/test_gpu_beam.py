@@ -245,7 +245,8 @@ def test_transformer_beam5_config3_fp32_vs_oracle():
     torch.testing.assert_close(info["sequences_scores"].cpu(), ref["sequences_scores"], rtol=1e-4, atol=1e-4)
 
 
-def _config3_peaked(precision, seed=42, n_hot=64, gain=40.0, eos_hot=False, round_bf16=False):
+def _config3_peaked(precision, seed=42, n_hot=64, gain=40.0, eos_hot=False, round_bf16=False, bias_step=0.0,
+                    cold_bias=0.0):
     """The config-3 model (test_gpu_model._full_model) with a peaked LM head: the output rows of
     n_hot tokens (fixed, seed-drawn; with eos_hot the EOS token is one of them) scaled by `gain`,
     so that, like a trained captioner's, the next-token distribution concentrates on a few tokens
@@ -253,7 +254,11 @@ def _config3_peaked(precision, seed=42, n_hot=64, gain=40.0, eos_hot=False, roun
     beam order is decided by differences below bf16 resolution.  round_bf16: every float
     parameter rounded to a bf16-representable value first, so that the fp32 and bf16 models
     compute with identical weights (only the activations' precision differs).  Same weights for
-    every precision."""
+    every precision.  bias_step: the i-th hot token's output bias raised by i * bias_step (exact
+    in both precisions: the bias is added in fp32), so candidate scores are spread by
+    image-independent gaps on top of the image-dependent logits.  cold_bias: the output bias of
+    every other token (e.g. -20: the distribution lives on the hot tokens while their logits stay
+    small, so the bf16 logits' rounding -- an ulp of 2^-8 |logit| -- stays small too)."""
     import capk
     from capk import config as C
     from capk.models import captioning_model as cm
@@ -269,6 +274,12 @@ def _config3_peaked(precision, seed=42, n_hot=64, gain=40.0, eos_hot=False, roun
         hot[-1] = cfg.model.eos_token_id
     with torch.no_grad():
         model.decoder.output_layer.weight[hot] *= gain
+        if bias_step:
+            model.decoder.output_layer.bias[hot] += bias_step * torch.arange(n_hot, dtype=torch.float32)
+        if cold_bias:
+            cold = torch.ones(cfg.model.vocab_size, dtype=torch.bool)
+            cold[hot] = False
+            model.decoder.output_layer.bias[cold] = cold_bias
         if round_bf16:
             for prm in model.parameters():
                 prm.copy_(prm.bfloat16().float())

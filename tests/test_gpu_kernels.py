@@ -734,3 +734,22 @@ def test_product_ln_slabs_bit_identical(M, K, N, conv):
     ref = torch.nn.functional.layer_norm((x.float() @ (w.float() if conv else w.float().t())) + b + res.float(),
                                          (N,), lw, lb, 1e-5)
     assert float((y1.float() - ref).norm() / ref.norm()) < 2e-2
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+def test_zero_gap_rows():
+    """capk_zero_gap_rows clears exactly rows b * rpb + j (S <= j < rpb) of a strided per-image
+    buffer -- the decoder's cross-attention K / V gradient over the ViT sequence minus its CLS
+    rows (M_ext = (B - 1) rpb + S rows, so the last image has no gap row) -- and nothing else."""
+    from capk import ops
+    B, rpb, S, C = 7, 197, 196, 1536
+    M = (B - 1) * rpb + S
+    x = torch.randn(M, C, device="cuda").bfloat16()
+    ref = x.clone()
+    for b in range(B):
+        for j in range(S, rpb):
+            r = b * rpb + j
+            if r < M:
+                ref[r] = 0
+    ops.zero_gap_rows(x, B, rpb, S)
+    assert torch.equal(x, ref)
