@@ -170,15 +170,25 @@ __global__ __launch_bounds__(ROWS_THREADS) void beam_rows_kernel(const T* __rest
   };
   const int V8 = V & ~7;
   bool first = true;
+  // the next chunk's 16-B load is issued before this chunk is filtered (one load in flight
+  // behind the filter's ballots and LDS appends)
+  float vn[8];
+  auto load_chunk = [&](int c, float (&d)[8]) {
+    const int i = c + lane * 8;
+    if (i < V8) Vec8<T>::load(x + i, d);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = -INFINITY;
+    }
+  };
+  if (w * 512 < V8) load_chunk(w * 512, vn);
   for (int c0 = w * 512; c0 < V8; c0 += 4 * 512) {
     const int i = c0 + lane * 8;
     const bool valid = i < V8;
     float v[8];
-    if (valid) Vec8<T>::load(x + i, v);
-    else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = -INFINITY;
-    }
+    for (int j = 0; j < 8; ++j) v[j] = vn[j];
+    if (c0 + 4 * 512 < V8) load_chunk(c0 + 4 * 512, vn);
     float cm = v[0];
 #pragma unroll
     for (int j = 1; j < 8; ++j) cm = fmaxf(cm, v[j]);
@@ -199,8 +209,17 @@ __global__ __launch_bounds__(ROWS_THREADS) void beam_rows_kernel(const T* __rest
       const uint64_t ball = __ballot(km != 0 && rank == K2 - 1);
       thr = ball ? readlane_u64(km, __builtin_ctzll(ball)) : 0;
     }
+    // only a chunk with some key >= the threshold can append: one ballot decides for all 8
+    // (offer() raises the threshold only when it appends, so skipping is exact)
+    uint64_t kmax = 0;
+    if (valid) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) offer(valid ? ckey(v[j], i + j) : 0);
+      for (int j = 0; j < 8; ++j) { const uint64_t kk = ckey(v[j], i + j); kmax = kk > kmax ? kk : kmax; }
+    }
+    if (__ballot(kmax != 0 && kmax >= thr)) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) offer(valid ? ckey(v[j], i + j) : 0);
+    }
   }
   for (int t0 = V8 + w * 64; t0 < V; t0 += 256) {  // tail (< 8 elements, one wave-uniform pass)
     const int i = t0 + lane;

@@ -35,9 +35,9 @@ if [[ ,$S, == *,fetch,* ]]; then  # FETCH_SIZE per GEMM shape under each raster 
 fi
 if [[ ,$S, == *,benchab,* ]]; then  # config-3 bench under two environments, ABAB (same box)
   for i in 1 2; do
-    env ${ENV_A:-CAPK_GEMM_GROUP=0} $B3 > $OUT/benchab_A$i.log 2>&1 || { echo "A$i failed"; tail -5 $OUT/benchab_A$i.log; exit 1; }
+    env ${ENV_A:-CAPK_GEMM_GROUP=0} timeout -k 10 300 $B3 > $OUT/benchab_A$i.log 2>&1 || { echo "A$i failed"; tail -5 $OUT/benchab_A$i.log; exit 1; }
     echo "A$i $(grep -o '"value": [0-9.]*' $OUT/benchab_A$i.log | head -1)"
-    env ${ENV_B:-CAPK_GEMM_GROUP=-1} $B3 > $OUT/benchab_B$i.log 2>&1 || { echo "B$i failed"; tail -5 $OUT/benchab_B$i.log; exit 1; }
+    env ${ENV_B:-CAPK_GEMM_GROUP=-1} timeout -k 10 300 $B3 > $OUT/benchab_B$i.log 2>&1 || { echo "B$i failed"; tail -5 $OUT/benchab_B$i.log; exit 1; }
     echo "B$i $(grep -o '"value": [0-9.]*' $OUT/benchab_B$i.log | head -1)"
   done
 fi
@@ -64,6 +64,14 @@ if [[ ,$S, == *,libbench,* ]]; then  # config-3 bench per library, alternated, 2
 fi
 [[ ,$S, == *,hiptrace,* ]] && run hiptrace 300 rocprofv3 --hip-trace --kernel-trace --output-format csv -d $OUT/hiptrace -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --beam-batch 0
 [[ ,$S, == *,profbeam,* ]] && run profbeam 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profbeam -o run -- python3 tools/beam_bench.py --reps 2
+if [[ ,$S, == *,beamab,* ]]; then  # beam-5 (tools/beam_bench.py) under two environments, ABAB (same box)
+  for i in 1 2; do
+    env ${ENV_A:-CAPK_RING_GROUP=0} timeout -k 10 240 python tools/beam_bench.py --reps 3 > $OUT/beamab_A$i.log 2>&1 || { echo "beam A$i failed"; tail -5 $OUT/beamab_A$i.log; exit 1; }
+    echo "A$i $(grep -h 'captions/s' $OUT/beamab_A$i.log)"
+    env ${ENV_B:-CAPK_RING_GROUP=-1} timeout -k 10 240 python tools/beam_bench.py --reps 3 > $OUT/beamab_B$i.log 2>&1 || { echo "beam B$i failed"; tail -5 $OUT/beamab_B$i.log; exit 1; }
+    echo "B$i $(grep -h 'captions/s' $OUT/beamab_B$i.log)"
+  done
+fi
 [[ ,$S, == *,bench3,* ]] && run bench_config3 480 python bench.py --steps 10 --warmup 3
 [[ ,$S, == *,bench3q,* ]] && run bench_config3q 300 $B3
 [[ ,$S, == *,bench5,* ]] && run bench_config5 480 python bench.py --workload config5 --steps 5 --warmup 2

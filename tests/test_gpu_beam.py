@@ -246,7 +246,7 @@ def test_transformer_beam5_config3_fp32_vs_oracle():
 
 
 def _config3_peaked(precision, seed=42, n_hot=64, gain=40.0, eos_hot=False, round_bf16=False, bias_step=0.0,
-                    cold_bias=0.0):
+                    cold_bias=0.0, bias_spread=0.0):
     """The config-3 model (test_gpu_model._full_model) with a peaked LM head: the output rows of
     n_hot tokens (fixed, seed-drawn; with eos_hot the EOS token is one of them) scaled by `gain`,
     so that, like a trained captioner's, the next-token distribution concentrates on a few tokens
@@ -258,7 +258,10 @@ def _config3_peaked(precision, seed=42, n_hot=64, gain=40.0, eos_hot=False, roun
     in both precisions: the bias is added in fp32), so candidate scores are spread by
     image-independent gaps on top of the image-dependent logits.  cold_bias: the output bias of
     every other token (e.g. -20: the distribution lives on the hot tokens while their logits stay
-    small, so the bf16 logits' rounding -- an ulp of 2^-8 |logit| -- stays small too)."""
+    small, so the bf16 logits' rounding -- an ulp of 2^-8 |logit| -- stays small too).  bias_spread:
+    the hot tokens' biases drawn uniformly from [0, bias_spread) (seeded; generic values, so sums
+    along different hypotheses do not tie): a confident head whose candidate gaps are set mostly
+    by exact fp32 biases, the image-dependent logits (gain) deciding between close ones."""
     import capk
     from capk import config as C
     from capk.models import captioning_model as cm
@@ -276,6 +279,8 @@ def _config3_peaked(precision, seed=42, n_hot=64, gain=40.0, eos_hot=False, roun
         model.decoder.output_layer.weight[hot] *= gain
         if bias_step:
             model.decoder.output_layer.bias[hot] += bias_step * torch.arange(n_hot, dtype=torch.float32)
+        if bias_spread:
+            model.decoder.output_layer.bias[hot] = torch.rand(n_hot, generator=torch.Generator().manual_seed(seed + 1)) * bias_spread
         if cold_bias:
             cold = torch.ones(cfg.model.vocab_size, dtype=torch.bool)
             cold[hot] = False
@@ -318,7 +323,8 @@ def _bf16_vs_fp32_margins(m32, m16, cfg, images, k=5, L=20):
         init = torch.full((B, k), -1e9, device="cuda")
         init[:, 0] = 0.0
         st = {"S32": init.clone(), "S16": init.clone(), "err": torch.zeros(B, device="cuda"),
-              "stable": torch.ones(B, dtype=torch.bool, device="cuda"), "lp32": None, "lp16": None}
+              "stable": torch.ones(B, dtype=torch.bool, device="cuda"), "lp32": None, "lp16": None,
+              "steps": 0, "steps_ok": 0}
 
         def step(cur_len, ids, reorder):
             if reorder is not None:  # running scores of the new rows: parent's score + chosen token's log-prob
@@ -332,18 +338,30 @@ def _bf16_vs_fp32_margins(m32, m16, cfg, images, k=5, L=20):
             c32 = (st["S32"][:, :, None] + st["lp32"].view(B, k, V)).view(B, k * V)
             c16 = (st["S16"][:, :, None] + st["lp16"].view(B, k, V)).view(B, k * V)
             val, idx = c32.topk(2 * k + 1, -1)
-            err = (c16.gather(1, idx) - val).abs().amax(1)
-            st["err"] = torch.maximum(st["err"], err)
-            gaps = val[:, :-1] - val[:, 1:]
+            e = c16.gather(1, idx) - val  # [B, 2k+1] bf16 - fp32 error of each top candidate
+            st["err"] = torch.maximum(st["err"], e.abs().amax(1))
+            # a pair (i, j) of top candidates keeps its order in bf16 when its fp32 gap exceeds the
+            # difference of the two errors (candidates from related beams share their prefix's
+            # error); margin 2x.  Pairs that matter: across the k / k+1 boundary (the running set),
+            # every pair when an EOS or the length limit is in play (the finished set is ranked too)
+            gap = val[:, :, None] - val[:, None, :]
+            ok = gap > 2 * (e[:, :, None] - e[:, None, :]).abs()
+            ii = torch.arange(2 * k + 1, device="cuda")
+            upper = ii[:, None] < ii[None, :]
+            boundary = upper & (ii[:, None] < k) & (ii[None, :] >= k)
             hit = ((idx % V) == eos).any(1) | (cur_len + 1 >= L)
-            need = torch.where(hit, gaps.amin(1), gaps[:, k - 1])
-            st["stable"] &= need > 2 * err
+            need_pairs = torch.where(hit[:, None, None], upper[None], boundary[None])
+            step_ok = (ok | ~need_pairs).all(2).all(1)
+            st["stable"] &= step_ok
+            st["steps"] += 1
+            st["steps_ok"] += int(step_ok.sum())
             return lg32
 
         out = beam_search(step, B, k, L, prompt, eos, pad_token_id=pad, vocab_size=V)
     sc = out["all_scores"]
     stable = st["stable"] & ((sc[:, 0] - sc[:, 1]) > 2 * st["err"])
     same = (_padded(out["sequences"], L, pad) == _padded(ids16, L, pad)).all(1)
+    _bf16_vs_fp32_margins.step_cov = st["steps_ok"] / max(1, st["steps"] * B)
     return same, stable, ids16, st["err"]
 
 

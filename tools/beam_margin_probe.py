@@ -1,6 +1,6 @@
 """Stable coverage of the bf16-vs-fp32 beam-5 precision check (tests/test_gpu_beam.py
 _bf16_vs_fp32_margins) for several peaked-LM-head settings of the config-3 model, 256 images.
-PROBE_SETTINGS="n_hot:gain:eos_hot:round_bf16:bias_step:cold_bias;..." overrides the list."""
+PROBE_SETTINGS="n_hot:gain:eos_hot:round_bf16:bias_step:cold_bias:bias_spread;..." overrides the list."""
 import os
 import sys
 
@@ -11,21 +11,22 @@ import torch  # noqa: E402
 
 import test_gpu_beam as tb  # noqa: E402
 
-DEFAULT = "4:1:0:1:0:-20;4:2:0:1:0:-20;6:1.5:0:1:0:-20;8:1:0:1:0:-20;4:2:1:1:0:-20;3:2:0:1:0:-20;4:4:0:1:0:-20"
+DEFAULT = "16:0.5:0:1:0:-20:8;16:1:0:1:0:-20:8;32:1:0:1:0:-20:16;8:0.5:0:1:0:-20:4;16:2:0:1:0:-20:16;16:1:1:1:0:-20:8"
 
 
 def main():
     B = int(os.environ.get("PROBE_B", "256"))
     images = torch.randn(B, 3, 224, 224, generator=torch.Generator().manual_seed(3)).cuda()
     for item in os.environ.get("PROBE_SETTINGS", DEFAULT).split(";"):
-        n_hot, gain, eos_hot, rb, bstep, cold = item.split(":")
+        n_hot, gain, eos_hot, rb, bstep, cold, spread = item.split(":")
         kw = dict(n_hot=int(n_hot), gain=float(gain), eos_hot=eos_hot == "1", round_bf16=rb == "1",
-                  bias_step=float(bstep), cold_bias=float(cold))
+                  bias_step=float(bstep), cold_bias=float(cold), bias_spread=float(spread))
         m32, cfg = tb._config3_peaked("fp32", **kw)
         m16, _ = tb._config3_peaked("bf16", **kw)
         same, stable, ids16, err = tb._bf16_vs_fp32_margins(m32, m16, cfg, images)
         lens = (ids16 != cfg.model.pad_token_id).sum(1).float()
         print(f"{kw}: identical {float(same.float().mean()):.3f}  stable {float(stable.float().mean()):.3f}  "
+              f"stable steps {tb._bf16_vs_fp32_margins.step_cov:.3f}  "
               f"stable&different {int((stable & ~same).sum())}  median err {float(err.median()):.4f}  "
               f"mean output length {float(lens.mean()):.1f}  distinct best sequences {len(set(map(tuple, ids16.tolist())))}",
               flush=True)

@@ -29,6 +29,28 @@ import gemm_bench  # noqa: E402
 DEFAULT = "qkv:50432:2304:768:fwd,fc1_plain:50432:3072:768:fwd,fc1g:50432:3072:768:fwd_gelu_deriv,o_res:50432:768:768:fwd_res,dx768:50432:768:768:dx,dx3072:50432:768:3072:dx,fc2dxg:50432:3072:768:dx_gelu_deriv"
 
 
+def check_stamps(t, M, N, name):
+    """Reject a trace with unwritten or stale slots (round 4's t17 run printed 9e16 us spans and
+    the same item count for every shape): every WG must carry the item count its grid position
+    gives (within one: the split-K tail round moves items), each stamped item all four stamps in the
+    order T2 <= T3 <= T0 <= T1, consecutive items in order, and nothing past the item count."""
+    items = ((M + 255) // 256) * ((N + 255) // 256)
+    for w in range(256):
+        first = (w & 7) * 32 + (w >> 3)
+        expect = (items - first + 255) // 256 if first < items else 0
+        for g in range(2):
+            st = t[w, g]
+            n = int((st[:, 0] > 0).sum())
+            if not (max(0, expect - 1) <= n <= expect + 1) or (st[n:] != 0).any():
+                raise SystemExit(f"{name}: WG {w} group {g}: {n} stamped items, expected {expect} -- stale trace")
+            for j in range(n):
+                a = st[j]
+                if (a <= 0).any() or not (a[2] <= a[3] <= a[0] <= a[1]):
+                    raise SystemExit(f"{name}: WG {w} group {g} item {j}: stamps {a.tolist()} unwritten / out of order")
+                if j + 1 < n and st[j + 1, 2] < a[1]:
+                    raise SystemExit(f"{name}: WG {w} group {g}: item {j + 1} starts before item {j} ends")
+
+
 def main():
     spec = sys.argv[1] if len(sys.argv) > 1 else DEFAULT
     lib = _lib.load()
@@ -36,11 +58,13 @@ def main():
     fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     buf = np.zeros((256, 2, 64, 4), dtype=np.uint64)
     for item in spec.split(","):
+        buf[:] = 0
         name, M, N, K, kind = item.split(":")
         gemm_bench.run(name, int(M), int(N), int(K), kind, iters=3)
         torch.cuda.synchronize()
         assert fn(buf.ctypes.data, buf.nbytes) == 0
         t = buf.astype(np.int64)
+        check_stamps(t, int(M), int(N), name)
         lead = t[:, 0]  # [WG, item, stamp]
         main_, epi, wait, sync = [], [], [], []
         for w in range(256):
