@@ -628,16 +628,28 @@ extern "C" int capk_linear_lse(int M, int N, int K, const void* x, int64_t ldx, 
 // consumers (the cell kernels, lstm.hip) sum the slabs themselves -- one launch per step and
 // layer in place of two GEMMs and two split-K reduces.  128x128 ring tiles; splits so that
 // about one round of WGs runs, every split >= CAPK_PAIR_MINKT (4) K-tiles.
-// A single product (no seam: the decode steps' GEMM -> LayerNorm pairs) takes capk_gemm's
-// own split count for the 128x128 ring, so the slabs -- and the sums of their consumers --
-// are bit-identical to capk_gemm + splitk_reduce.
+// A single product (no seam: the decode steps' GEMM -> LayerNorm pairs) has no reduce launch
+// to amortise -- its consumer sums the slabs -- so it splits until about two WGs per CU run
+// (each split >= 4 K-tiles): the decode steps' K = 768 out-projections at 1280 rows go from 60
+// one-split tiles (12 K-tiles each, latency-bound) to 3 splits.  CAPK_SLAB_SPLITS=0 keeps
+// capk_gemm's own count, whose slabs are bit-identical to capk_gemm + splitk_reduce.
 static int pair_splits(int M, int N, int K, bool seam) {
   static const int min_kt = [] {
     const char* v = getenv("CAPK_PAIR_MINKT");
     return v ? std::max(1, atoi(v)) : 4;
   }();
+  static const bool slab_policy = [] {
+    const char* v = getenv("CAPK_SLAB_SPLITS");
+    return !(v && v[0] == '0');
+  }();
   const int tiles = cdiv(M, 128) * cdiv(N, BN), nk = cdiv(K, 64);
-  const int s = seam ? std::max(1, std::min(256 / tiles, nk / min_kt)) : choose_splits(1, M, N, K);
+  int s;
+  if (seam) s = std::max(1, std::min(256 / tiles, nk / min_kt));
+  else {
+    s = choose_splits(1, M, N, K);
+    if (slab_policy) s = std::max(s, std::min(512 / tiles, nk / min_kt));
+  }
+  s = std::max(1, s);
   return cdiv(nk, cdiv(nk, s));  // effective count: every split owns >= 1 K-tile
 }
 

@@ -345,13 +345,23 @@ def _bf16_vs_fp32_margins(m32, m16, cfg, images, k=5, L=20):
             # error); margin 2x.  Pairs that matter: across the k / k+1 boundary (the running set),
             # every pair when an EOS or the length limit is in play (the finished set is ranked too)
             gap = val[:, :, None] - val[:, None, :]
-            ok = gap > 2 * (e[:, :, None] - e[:, None, :]).abs()
-            ii = torch.arange(2 * k + 1, device="cuda")
-            upper = ii[:, None] < ii[None, :]
-            boundary = upper & (ii[:, None] < k) & (ii[None, :] >= k)
-            hit = ((idx % V) == eos).any(1) | (cur_len + 1 >= L)
-            need_pairs = torch.where(hit[:, None, None], upper[None], boundary[None])
-            step_ok = (ok | ~need_pairs).all(2).all(1)
+            ok = gap > 2 * (e[:, :, None] - e[:, None, :]).abs()  # [B, i, j]: i above j keeps its place
+            n = 2 * k + 1
+            non_eos = (idx % V) != eos
+            # (a) the running set: the first k non-EOS candidates against every later non-EOS one
+            nrank = torch.cumsum(non_eos.int(), 1)  # 1-based rank among the non-EOS candidates
+            in_run = non_eos & (nrank <= k)
+            out_run = non_eos & (nrank > k)
+            need = in_run[:, :, None] & out_run[:, None, :]
+            # (b) membership of the 2k kept candidates when an EOS is among the 2k + 1 best (a
+            # finished hypothesis may be the final best: HF keeps it by its length-normalised score)
+            top = torch.arange(n, device="cuda") < 2 * k
+            eos_in = (~non_eos).any(1)
+            need |= (eos_in[:, None, None] & top[None, :, None] & ~top[None, None, :])
+            # the last step sends every kept candidate to the finished set: only the final best's
+            # margin (below) decides the output
+            last = cur_len + 1 >= L
+            step_ok = (ok | ~need).all(2).all(1) | last
             st["stable"] &= step_ok
             st["steps"] += 1
             st["steps_ok"] += int(step_ok.sum())
@@ -359,7 +369,13 @@ def _bf16_vs_fp32_margins(m32, m16, cfg, images, k=5, L=20):
 
         out = beam_search(step, B, k, L, prompt, eos, pad_token_id=pad, vocab_size=V)
     sc = out["all_scores"]
-    stable = st["stable"] & ((sc[:, 0] - sc[:, 1]) > 2 * st["err"])
+    # finished scores are length-normalised (sum / generated length ** 1): their errors are at most
+    # the sum's error over the shorter generated length
+    gen = out["all_sequences"][:, :2, 1:]
+    is_end = gen == eos
+    first_end = torch.where(is_end.any(2), is_end.int().argmax(2) + 1, torch.full_like(is_end[..., 0], L - 1, dtype=torch.long))
+    min_len = first_end.min(1).values.clamp_min(1).float()
+    stable = st["stable"] & ((sc[:, 0] - sc[:, 1]) > 2 * st["err"] / min_len)
     same = (_padded(out["sequences"], L, pad) == _padded(ids16, L, pad)).all(1)
     _bf16_vs_fp32_margins.step_cov = st["steps_ok"] / max(1, st["steps"] * B)
     return same, stable, ids16, st["err"]

@@ -709,9 +709,12 @@ def test_gemm_timer_follows_the_stream(ops):
                                         (1280, 768, 768, False), (1280, 3072, 768, False), (40, 512, 512, False)])
 def test_product_ln_slabs_bit_identical(M, K, N, conv):
     """ops.product_ln (split-K slabs summed by capk_layernorm_fwd_slabs) against the separate
-    route (capk_gemm + bias + residual, then capk_layernorm_fwd): LayerNorm output and the
-    kept pre-LN sum bit-identical, for the GPT-2 Conv1D [in, out] and nn.Linear [out, in]
-    weights of the decode steps (split and unsplit shapes)."""
+    route (capk_gemm + bias + residual, then capk_layernorm_fwd), for the GPT-2 Conv1D [in, out]
+    and nn.Linear [out, in] weights of the decode steps: LayerNorm output and the kept pre-LN sum
+    bit-identical when both routes split K the same way (CAPK_SLAB_SPLITS=0, or shapes where the
+    slab policy keeps capk_gemm's count), else within fp32 summation-order rounding of it (the
+    slab route splits the short-K products further: no reduce launch to amortise); both vs an
+    fp32 torch reference within 2e-2."""
     from capk import ops
     g = torch.Generator(device="cuda").manual_seed(M + K)
     bf = torch.bfloat16
@@ -729,8 +732,15 @@ def test_product_ln_slabs_bit_identical(M, K, N, conv):
         y0, s0 = ops.product_ln(x, w, conv, b, res, lw, lb, 1e-5, keep=True)
     finally:
         ops.DECODE_SLABS = saved
-    assert torch.equal(s1, s0)
-    assert torch.equal(y1, y0)
+    import ctypes
+    sp = ctypes.c_int(0)
+    ops.lib().capk_gemm_slabs_workspace(M, N, K, ctypes.byref(sp))
+    if sp.value == 1:  # (then capk_gemm's own count is 1 as well: the slab policy only raises it)
+        assert torch.equal(s1, s0)
+        assert torch.equal(y1, y0)
+    else:
+        assert float((s1.float() - s0.float()).norm() / s0.float().norm()) < 1e-2
+        assert float((y1.float() - y0.float()).norm() / y0.float().norm()) < 1e-2
     ref = torch.nn.functional.layer_norm((x.float() @ (w.float() if conv else w.float().t())) + b + res.float(),
                                          (N,), lw, lb, 1e-5)
     assert float((y1.float() - ref).norm() / ref.norm()) < 2e-2
