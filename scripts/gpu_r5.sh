@@ -62,6 +62,13 @@ if [[ ,$S, == *,libbench,* ]]; then  # config-3 bench per library, alternated, 2
     done
   done
 fi
+if [[ ,$S, == *,traffic,* ]]; then  # GEMM bytes per launch for bench.py's roofline.traffic (-> profiles/round5/gemm_traffic.json)
+  TC="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --beam-batch 0"
+  run fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/fetch -o run -- $TC
+  run write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/write -o run -- $TC
+  python3 tools/pmc_traffic.py $OUT/fetch $OUT/write --out $OUT/gemm_traffic.json --cmd "$TC" > /dev/null && \
+    mkdir -p profiles/round5 && cp $OUT/gemm_traffic.json profiles/round5/gemm_traffic.json
+fi
 [[ ,$S, == *,hiptrace,* ]] && run hiptrace 300 rocprofv3 --hip-trace --kernel-trace --output-format csv -d $OUT/hiptrace -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --beam-batch 0
 [[ ,$S, == *,profbeam,* ]] && run profbeam 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profbeam -o run -- python3 tools/beam_bench.py --reps 2
 if [[ ,$S, == *,beamab,* ]]; then  # beam-5 (tools/beam_bench.py) under two environments, ABAB (same box)

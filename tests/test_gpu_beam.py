@@ -381,14 +381,19 @@ def _bf16_vs_fp32_margins(m32, m16, cfg, images, k=5, L=20):
     return same, stable, ids16, st["err"]
 
 
-# peaked-head settings of the bf16-vs-fp32 beam test (tools/beam_margin_probe.py measures the
-# stable coverage of each candidate setting on the GPU)
-BEAM_PEAK = dict(n_hot=64, gain=40.0, eos_hot=False, round_bf16=False)
-BEAM_MIN_STABLE = 0.25
+# peaked-head settings of the bf16-vs-fp32 beam test and the stable coverage each must reach
+# (tools/beam_margin_probe.py measured them on the GPU: profiles/round5/beam_margin_probe_7.txt).
+# A narrow head decides most images by wide margins but every image then takes the same caption;
+# a wider one gives 13 distinct captions over the batch with fewer images decided by margins.
+BEAM_PEAKS = [
+    (dict(n_hot=6, gain=2.0, eos_hot=False, round_bf16=True, cold_bias=-20.0, bias_spread=8.0), 0.40),
+    (dict(n_hot=8, gain=2.5, eos_hot=False, round_bf16=True, cold_bias=-20.0, bias_spread=8.0), 0.04),
+]
 
 
 @cuda
-def test_transformer_beam5_config3_bf16_vs_fp32():
+@pytest.mark.parametrize("peak,min_stable", BEAM_PEAKS, ids=["narrow", "wide"])
+def test_transformer_beam5_config3_bf16_vs_fp32(peak, min_stable):
     """The benchmarked path end to end: config-3 model (ViT-B/16 + 6L/8H decoder, V = 50 257),
     256 images, bf16 beam-5 through ``generate`` (graph-replayed KV-cached decode).
 
@@ -402,13 +407,13 @@ def test_transformer_beam5_config3_bf16_vs_fp32():
        bit-exactly to the CPU reference by test_transformer_beam5_config3_fp32_vs_oracle), every
        image whose search is decided by margins larger than the bf16 error at every step
        (_bf16_vs_fp32_margins) must return the identical best sequence, and such images must be
-       at least BEAM_MIN_STABLE of the batch.  Weights: random init with a peaked LM head
-       (_config3_peaked with BEAM_PEAK: the next-token distribution concentrates on a few
+       at least ``min_stable`` of the batch.  Weights: random init with a peaked LM head
+       (_config3_peaked with ``peak``: the next-token distribution concentrates on a few
        well-separated tokens, like a trained captioner's)."""
     from capk.beam import beam_search
     from capk.models.transformer import KVDecodeRunner
-    m32, cfg = _config3_peaked("fp32", **BEAM_PEAK)
-    m16, _ = _config3_peaked("bf16", **BEAM_PEAK)
+    m32, cfg = _config3_peaked("fp32", **peak)
+    m16, _ = _config3_peaked("bf16", **peak)
     B, k, L = 256, 5, 20
     V, eos, pad = cfg.model.vocab_size, cfg.model.eos_token_id, cfg.model.pad_token_id
     images = torch.randn(B, 3, 224, 224, generator=torch.Generator().manual_seed(3)).cuda()
@@ -446,6 +451,7 @@ def test_transformer_beam5_config3_bf16_vs_fp32():
     cov = float(stable.float().mean())
     print(f"bf16 beam-5 at config-3 size: {st1['n']} selections x {B} images checked; vs fp32: identical best "
           f"sequence {float(same.float().mean()):.3f}, stable {int(stable.sum())}/{B} = {cov:.3f} "
-          f"(identical {int((same & stable).sum())}), median max candidate error {float(err.median()):.4f}")
+          f"(identical {int((same & stable).sum())}), median max candidate error {float(err.median()):.4f}, "
+          f"distinct captions {len(set(map(tuple, ids16.tolist())))} (stable {len(set(map(tuple, ids16[stable].tolist())))})")
     assert bool(same[stable].all()), torch.nonzero(stable & ~same).flatten().tolist()
-    assert cov >= BEAM_MIN_STABLE, cov
+    assert cov >= min_stable, cov

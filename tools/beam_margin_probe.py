@@ -11,7 +11,7 @@ import torch  # noqa: E402
 
 import test_gpu_beam as tb  # noqa: E402
 
-DEFAULT = "16:2:0:1:0:-20:8;16:1.5:0:1:0:-20:8;8:2:0:1:0:-20:8;12:1:0:1:0:-20:6;8:1:0:1:0:-20:4;16:0.5:0:1:0:-20:8;64:40:0:0:0:0:0"
+DEFAULT = "8:3:0:1:0:-20:10;8:4:0:1:0:-20:12;12:3:0:1:0:-20:16;6:2:0:1:0:-20:8;8:2.5:0:1:0:-20:8;16:3:0:1:0:-20:24;8:2:0:1:0:-20:8"
 
 
 def main():
