@@ -47,7 +47,21 @@ struct AttnArgs {
   int64_t dbias_ld;
   float* rsum;
   int b_base;  // batch index of this launch's first image (a batch slice): dropout mask index
+  // XCD-chunked block order (xcd_bh): set by the host when the grid is B * H blocks, B * H % 8 == 0
+  int xcd_chunk;
 };
+
+// (batch, head) of this workgroup.  Workgroups are dispatched round-robin over the 8 XCDs
+// (block i runs on XCD i % 8), so with the plain order the H heads of one image run on H
+// different XCDs.  With hd = 96 a head's slice of a K / V row is 192 B and shares 128-B lines
+// with its neighbours, so every XCD fetched each line of the row through its own L2.  With
+// xcd_chunk, XCD x takes the contiguous logical blocks [x n / 8, (x + 1) n / 8) in order: the
+// heads of an image run back to back on one XCD and read the shared lines once.
+__device__ __forceinline__ int xcd_bh(const AttnArgs& a) {
+  const int i = blockIdx.x;
+  return a.xcd_chunk ? (i & 7) * (int)(gridDim.x >> 3) + (i >> 3) : i;
+}
+
 
 // the K / V batch row holding key j of batch row b
 __device__ __forceinline__ int64_t kv_row(const AttnArgs& a, int b, int j) {
@@ -1125,7 +1139,7 @@ __global__ __launch_bounds__(256) void attn_xdec_bf16(AttnArgs a) {
   static_assert(NQ * HDP * 4 <= KPW * ST * 2, "the fp32 partial O of a wave fits its V image");
   __shared__ __attribute__((aligned(16))) bf16 vimg[NW][KPW * ST];
   __shared__ float mm[NW][NQ], ll[NW][NQ];
-  const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
+  const int bh = xcd_bh(a), b = bh / a.H, h = bh % a.H;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
   const int hoff = h * a.hd;
   const int k0 = w * KPW;  // the wave's first key
@@ -1276,7 +1290,7 @@ __global__ __launch_bounds__(256) void attn_xbwd_bf16(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 dsimg[NW][32 * DST];
   __shared__ float lse_s[32], del_s[32];
   static_assert(2 * NQ * HDP * 4 <= (int)sizeof(kimg), "two fp32 dQ partials fit the K images");
-  const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
+  const int bh = xcd_bh(a), b = bh / a.H, h = bh % a.H;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
   const int hoff = h * a.hd;
   const bf16* kbase = (const bf16*)a.k + (int64_t)b * a.k_bs + hoff;
@@ -1690,7 +1704,7 @@ __device__ __forceinline__ float grp_sum(float x) {  // sum over the lane's LPR-
 template <int LPR, int NQ, int MAXP>
 __global__ __launch_bounds__(512) void attn_decode2_bf16(AttnArgs a, int passes_per_wave) {
   constexpr int KPP = 64 / LPR;
-  const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
+  const int bh = xcd_bh(a), b = bh / a.H, h = bh % a.H;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, W = blockDim.x >> 6;
   const int g = lane / LPR, c = lane % LPR;
   const bool act = c * 8 < a.hd;
@@ -1823,9 +1837,16 @@ __global__ __launch_bounds__(512) void attn_decode2_bf16(AttnArgs a, int passes_
   }
 }
 
+// xcd_chunk for a grid of nblk (batch, head) workgroups (CAPK_ATTN_XCD=0: the plain order, for A/B)
+static int attn_xcd(int nblk) {
+  static const bool on = [] { const char* e = getenv("CAPK_ATTN_XCD"); return !(e && e[0] == '0'); }();
+  return on && nblk % 8 == 0 ? 1 : 0;
+}
+
 // launch the v2 decode kernel: LPR by head width, W waves so that each wave has <= MAXP passes
 template <int NQ>
-static int launch_decode2(const AttnArgs& a, hipStream_t st) {
+static int launch_decode2(AttnArgs a, hipStream_t st) {
+  a.xcd_chunk = attn_xcd(a.B * a.H);
   constexpr int MAXP = 8;
   const int lpr = a.hd <= 64 ? 8 : 16, kpp = 64 / lpr;
   const int npass = cdiv(a.Nk, kpp);
@@ -1914,6 +1935,7 @@ extern "C" int capk_attention_fwd(int dtype, int B, int H, int Nq, int Nk, int h
   if (xdec_on && !decode_v1 && Nq >= 2 && Nq <= 32 && Nk > 64 && Nk <= 256 && !causal &&
       (hd == 64 || hd == 96 || hd == 128)) {
     const dim3 g(B * H), blk(256);
+    a.xcd_chunk = attn_xcd(B * H);
     const int xm = (key_pad ? AM_MASK : 0) | (drop_p > 0.f ? AM_DROP : 0);
 #define XDQ(HD, M)                                                                  \
   if (Nq <= 16) hipLaunchKernelGGL((attn_xdec_bf16<HD, M, 1>), g, blk, 0, st, a);   \
@@ -2091,6 +2113,7 @@ static int attention_bwd_impl(int dtype, int B, int H, int Nq, int Nk, int hd, f
   static const bool xbwd_on = [] { const char* e = getenv("CAPK_XDEC"); return !(e && e[0] == '0'); }();
   if (xbwd_on && Nq >= 2 && Nq <= 32 && Nk > 64 && Nk <= 256 && !causal && (hd == 64 || hd == 96 || hd == 128)) {
     const dim3 g(B * H), blk(256);
+    a.xcd_chunk = attn_xcd(B * H);
     const int xm = (key_pad ? AM_MASK : 0) | (drop_p > 0.f ? AM_DROP : 0);
 #define XBQ(HD, M)                                                                  \
   if (Nq <= 16) hipLaunchKernelGGL((attn_xbwd_bf16<HD, M, 1>), g, blk, 0, st, a);   \

@@ -17,6 +17,11 @@ CASES = [("vit", 256, 12, 197, 197, 64, False), ("dec_self", 256, 8, 20, 20, 96,
          ("dstep_self", 1280, 8, 1, 20, 96, False), ("dstep_cross5", 256, 8, 5, 196, 96, False),
          ("dstep_gpt2_b4", 1024, 12, 1, 30, 64, False), ("dstep_gpt2_s", 256, 12, 1, 30, 64, False)]
 ONLY = os.environ.get("ATTN_ONLY")
+# ATTN_FLUSH=1: read a 1 GB scratch buffer before every timed call (events around each call),
+# so K / V come from HBM as in the model, where the other layers' K / V evict them from the
+# 256 MB Infinity Cache between two calls of one layer (a read, not a fill: evicting dirty
+# lines would add write-backs to the timed call)
+FLUSH = os.environ.get("ATTN_FLUSH") == "1"
 
 
 def main(iters=10):
@@ -41,12 +46,24 @@ def main(iters=10):
             fn()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(iters):
-                fn()
-            e1.record()
-            torch.cuda.synchronize()
-            ms = e0.elapsed_time(e1) / iters
+            if FLUSH:
+                scratch = torch.ones(128 << 20, dtype=torch.int64, device="cuda")
+                ms = 0.0
+                for _ in range(iters):
+                    scratch.max()
+                    e0.record()
+                    fn()
+                    e1.record()
+                    torch.cuda.synchronize()
+                    ms += e0.elapsed_time(e1) / iters
+                del scratch
+            else:
+                e0.record()
+                for _ in range(iters):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / iters
             fl = mult * B * H * Nq * Nk * hd / (2 if causal else 1)
             by = (2 * B * Nq * D + 2 * B * Nk * D) * 2 * (1 if tag == "fwd" else 2)  # Q, O, K, V (x2 bwd)
             print(f"{name:10s} {tag}: {ms * 1e3:8.1f} us  {fl / ms / 1e9:7.1f} TFLOP/s  ~{by / ms / 1e9:6.2f} TB/s", flush=True)
