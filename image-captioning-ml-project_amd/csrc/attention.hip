@@ -49,6 +49,8 @@ struct AttnArgs {
   int b_base;  // batch index of this launch's first image (a batch slice): dropout mask index
   // XCD-chunked block order (xcd_bh): set by the host when the grid is B * H blocks, B * H % 8 == 0
   int xcd_chunk;
+  // stage the swizzled 64-wide head images by LDS DMA (stage_dma_sw), bit 0 forward, 1 dQ, 2 dK/dV
+  int dma_stage;
 };
 
 // (batch, head) of this workgroup.  Workgroups are dispatched round-robin over the 8 XCDs
@@ -231,6 +233,25 @@ __device__ __forceinline__ void stage_images_rt(const StageSrc (&S)[NIMG], int h
   }
 }
 
+// Swizzled 64-wide head images (swz_off layout) staged by LDS DMA (global_load_lds, 16 B per
+// lane): 1-KiB pieces of 8 rows; lane l of a piece writes row 8p + l/8, chunk slot l%8, which
+// holds source chunk (l%8) ^ ((l/8) & 6) -- the swizzle moves to the source address, and no
+// VGPR, address select or LDS store is spent on the copy.  Rows n..NP-1 read row n - 1 (the
+// kernels mask or zero-weight them).  The caller waits vmcnt(0) and barriers before reading.
+template <int NIMG>
+__device__ __forceinline__ void stage_dma_sw(const StageSrc (&S)[NIMG], int wave, int nwaves, int lane) {
+  const int rl = lane >> 3, csrc = ((lane & 7) ^ (rl & 6)) * 8;
+#pragma unroll
+  for (int im = 0; im < NIMG; ++im) {
+    const int pieces = S[im].NP >> 3;
+    for (int p = wave; p < pieces; p += nwaves) {
+      const int r = min(p * 8 + rl, S[im].n - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(S[im].src + (int64_t)r * S[im].rs + csrc),
+                                       (__attribute__((address_space(3))) void*)(S[im].img + p * 512), 16, 0, 0);
+    }
+  }
+}
+
 template <int HDP>
 __device__ __forceinline__ void load_q_frags(const AttnArgs& a, const bf16* qsrc, int qt, int lane, bf16x8 (&qf)[HDP / 32]) {
   const int qi = qt * 16 + (lane & 15);
@@ -379,7 +400,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HDP == 64 ?
   {
     const StageSrc S[2] = {{Ks, (const bf16*)a.k + (int64_t)b * a.k_bs + hoff, a.k_rs, a.Nk, NKP},
                            {Vs, (const bf16*)a.v + (int64_t)b * a.v_bs + hoff, a.v_rs, a.Nk, NKP}};
-    stage_images_rt<HDP, 2, SW>(S, a.hd);
+    if (SW && a.hd == 64 && (a.dma_stage & 1)) {
+      stage_dma_sw<2>(S, wave, nwaves, lane);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      stage_images_rt<HDP, 2, SW>(S, a.hd);
+    }
   }
   __syncthreads();
 
@@ -592,7 +618,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
   {
     const StageSrc S[2] = {{Qs, (const bf16*)a.q + (int64_t)b * a.q_bs + hoff, a.q_rs, a.Nq, NQP},
                            {dOs, (const bf16*)a.dout + (int64_t)b * a.do_bs + hoff, a.do_rs, a.Nq, NQP}};
-    stage_images<HDP, 2, 512, SW>(S, a.hd);
+    if (SW && a.hd == 64 && (a.dma_stage & 4)) {  // rows Nq..NQP-1 repeat row Nq-1: P = dS = 0 there
+      stage_dma_sw<2>(S, wave, nwaves, lane);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      stage_images<HDP, 2, 512, SW>(S, a.hd);
+    }
   }
   if (threadIdx.x < NQP) lse_s[threadIdx.x] = lse_r;  // log2 domain
   float* ksum_s = del_s + NQP;  // BIAS: [NKP] sum_q dS[q, key]
@@ -749,7 +780,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HDP == 64 ?
   {
     const StageSrc S[2] = {{Ks, (const bf16*)a.k + (int64_t)b * a.k_bs + hoff, a.k_rs, a.Nk, NKP},
                            {Vs, (const bf16*)a.v + (int64_t)b * a.v_bs + hoff, a.v_rs, a.Nk, NKP}};
-    stage_images_rt<HDP, 2, SW>(S, a.hd);
+    if (SW && a.hd == 64 && (a.dma_stage & 2)) {
+      stage_dma_sw<2>(S, wave, nwaves, lane);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      stage_images_rt<HDP, 2, SW>(S, a.hd);
+    }
   }
   __syncthreads();
   const float sl2 = a.scale * kLog2e;
@@ -1886,6 +1922,11 @@ int launch_colsum_finish(int parts, int N, const float* part, float* out, int ac
 
 using namespace capk;
 
+static int attn_dma_env() {  // CAPK_ATTN_DMA: bit 0 forward, bit 1 dQ, bit 2 dK/dV kernel (default 7; A/B)
+  static const int v = [] { const char* e = getenv("CAPK_ATTN_DMA"); return e ? atoi(e) & 7 : 7; }();
+  return v;
+}
+
 extern "C" int capk_attention_fwd(int dtype, int B, int H, int Nq, int Nk, int hd, float scale, int causal,
                                   const void* q, int64_t q_bs, int64_t q_rs, const void* k, int64_t k_bs,
                                   int64_t k_rs, const void* v, int64_t v_bs, int64_t v_rs, const uint8_t* key_pad,
@@ -1898,6 +1939,7 @@ extern "C" int capk_attention_fwd(int dtype, int B, int H, int Nq, int Nk, int h
   a.q = q; a.k = k; a.v = v; a.q_bs = q_bs; a.q_rs = q_rs; a.k_bs = k_bs; a.k_rs = k_rs; a.v_bs = v_bs; a.v_rs = v_rs;
   a.key_pad = key_pad; a.out = o; a.out_bs = o_bs; a.out_rs = o_rs; a.lse = lse;
   a.drop = make_drop(drop_p, drop_seed);
+  a.dma_stage = attn_dma_env();
   hipStream_t st = S(stream);
   if (dtype == CAPK_F32) {
     dim3 grid(B * H, cdiv(Nq, 64));
@@ -2057,6 +2099,7 @@ static int attention_bwd_impl(int dtype, int B, int H, int Nq, int Nk, int hd, f
   a.lse_in = lse; a.dq = dq; a.dq_bs = dq_bs; a.dq_rs = dq_rs; a.dk = dk; a.dk_bs = dk_bs; a.dk_rs = dk_rs;
   a.dv = dv; a.dv_bs = dv_bs; a.dv_rs = dv_rs;
   a.drop = make_drop(drop_p, drop_seed);
+  a.dma_stage = attn_dma_env();
   hipStream_t st = S(stream);
   if (dtype == CAPK_F32) {
     {

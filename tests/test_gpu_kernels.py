@@ -64,6 +64,35 @@ def test_linear_backward_layouts(ops, dtype):
 
 
 @cuda
+@pytest.mark.parametrize("cfg", [1, 7, 8])
+@pytest.mark.parametrize("M,N,K", [(1280, 768, 768), (300, 256, 192), (517, 384, 3072), (70, 3072, 768)])
+def test_ring_configs_bf16(ops, cfg, M, N, K):
+    """The 128x128 ring tiles (1: 2-deep, 7: 4-deep, one WG per CU) and the 64x128 tile (8: two
+    waves), forced in turn on K-major products with ragged M / N: bias + GELU (kept pre-act) +
+    residual epilogue, and a plain product whose K split takes the slab reduce, vs the fp32
+    product of the same bf16 values."""
+    from capk._lib import ACT_GELU_ERF
+    L = ops.lib()
+    g = torch.Generator(device="cuda").manual_seed(9)
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device="cuda", generator=g)
+    r = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    try:
+        ops.check(L.capk_gemm_force_config(cfg), "force_config")
+        y = ops.linear(x, w, b, residual=r, act=ACT_GELU_ERF, preact=pre)
+        assert L.capk_gemm_last_config() == cfg
+        yp = ops.linear(x, w)
+    finally:
+        L.capk_gemm_force_config(-1)
+    ref_pre = x.float() @ w.float().t() + b
+    assert _rel(pre, ref_pre) < 1e-2
+    assert _rel(y, F.gelu(ref_pre) + r.float()) < 1e-2
+    assert _rel(yp, x.float() @ w.float().t()) < 1e-2
+
+
+@cuda
 def test_gemm_bf16_splitk_and_beta(ops):
     """dW-shaped GEMM with a long reduction (split-K slabs + reduce) and accumulate."""
     g = torch.Generator(device="cuda").manual_seed(2)
