@@ -738,6 +738,157 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
 }
 
+// Fused single-pass backward for 64-wide heads (the ViT layers, N = 197): one workgroup per
+// (image, head) with one wave per 16-key block (13 for N = 197, up to 16) holds Q, dO and K in
+// LDS (LDS-DMA), forms P and dS once per (query, key) and produces dK, dV and dQ.  The split
+// pair (attn_bwd_kv_bf16 + attn_bwd_q_bf16) formed P and dS twice and read every operand twice.
+//  * key waves: the attn_bwd_kv_bf16 loop over 32-query chunks (their K / V rows in registers,
+//    dV += dO^T P, dK += Q^T dS in registers), and each chunk's dS^T block goes to an LDS
+//    image [keys][32 queries] (double-buffered, one barrier per chunk);
+//  * after the barrier, waves 0-7 each form one 16 x 16 block of the chunk's dQ^T = K^T dS^T
+//    over all keys (transposed reads of the K image and of the dS^T image, the same key order
+//    on both sides) and store it -- every key has contributed, so no dQ accumulator survives
+//    the chunk.
+// Same expressions as the split pair (P, dS, delta, masks, dropout index).  Requires hd == 64,
+// NKP = Nk rounded to 16 <= 256, LDS (2 NQP + NKP) x 128 B + the dS^T images <= 160 KiB.
+template <int MODE>
+__global__ __launch_bounds__(1024) void attn_bwd_fused64(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int HDP = 64, DSST = 48;  // dS^T image row stride: 32 queries + 16 (conflict-free transposed reads)
+  const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int NQP = (a.Nq + 31) & ~31, NKP = (a.Nk + 15) & ~15, NKB = NKP / 16, NKC = (NKP + 31) / 32;
+  bf16* Qs = (bf16*)smem;      // [NQP][64], swz_off layout
+  bf16* dOs = Qs + NQP * 64;   // [NQP][64]
+  bf16* Ks = dOs + NQP * 64;   // [NKP][64]
+  bf16* dST = Ks + NKP * 64;   // [2][NKC * 32][DSST]
+  const int DSB = NKC * 32 * DSST;
+  float* lse_s = (float*)(dST + 2 * DSB);
+  float* del_s = lse_s + NQP;
+  const int hoff = h * HDP;
+  const bool kw = wave < NKB;  // a key wave: key block kb = wave
+  const int kb = wave, keyl = kb * 16 + i16;
+  const bf16* kbase = (const bf16*)a.k + (int64_t)b * a.k_bs + hoff;
+  const bf16* vbase = (const bf16*)a.v + (int64_t)b * a.v_bs + hoff;
+  // ---- prologue: the wave's K / V rows, lse, O rows for delta, and the Q / dO / K images by DMA
+  bf16x8 kf[2], vf[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int d = s * 32 + 8 * g;
+    const bool in = kw && keyl < a.Nk;
+    kf[s] = in ? ld8(kbase + (int64_t)keyl * a.k_rs + d) : zero8();
+    vf[s] = in ? ld8(vbase + (int64_t)keyl * a.v_rs + d) : zero8();
+  }
+  const float lse_r = threadIdx.x < a.Nq ? a.lse_in[((int64_t)b * a.H + h) * a.Nq + threadIdx.x] * kLog2e : 0.f;
+  bf16x8 ov[2];  // 8 lanes per query, 8 dims each: queries threadIdx.x / 8 (+ 128 per pass)
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int idx = threadIdx.x + it * (int)blockDim.x, q = idx >> 3, c = idx & 7;
+    ov[it] = q < a.Nq ? ld8((const bf16*)a.o + (int64_t)b * a.o_bs + (int64_t)q * a.o_rs + hoff + c * 8) : zero8();
+  }
+  {
+    const StageSrc S[3] = {{Qs, (const bf16*)a.q + (int64_t)b * a.q_bs + hoff, a.q_rs, a.Nq, NQP},
+                           {dOs, (const bf16*)a.dout + (int64_t)b * a.do_bs + hoff, a.do_rs, a.Nq, NQP},
+                           {Ks, kbase, a.k_rs, a.Nk, NKP}};
+    stage_dma_sw<3>(S, wave, nwaves, lane);
+  }
+  // dS^T rows past NKP are read by the last key chunk's transposed reads: zero, both buffers
+  for (int e = threadIdx.x; e < 2 * (NKC * 32 - NKP) * DSST; e += blockDim.x) {
+    const int bi = e / ((NKC * 32 - NKP) * DSST), rem = e - bi * (NKC * 32 - NKP) * DSST;
+    dST[bi * DSB + NKP * DSST + rem] = (bf16)0.f;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x < NQP) lse_s[threadIdx.x] = lse_r;  // log2 domain
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {  // delta = rowsum(dO * O), the attn_bwd_kv_bf16 order
+    const int idx = threadIdx.x + it * (int)blockDim.x, q = idx >> 3, c = idx & 7;
+    if (it * (int)blockDim.x >= NQP * 8) break;  // uniform over the block
+    float sum = 0.f;
+    if (q < NQP) {
+      const bf16x8 dv = *(const bf16x8*)(dOs + swz_off(q, c * 8));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) sum += (float)ov[it][i] * (float)dv[i];
+    }
+    sum += __shfl_xor(sum, 1, 64);
+    sum += __shfl_xor(sum, 2, 64);
+    sum += __shfl_xor(sum, 4, 64);
+    if (c == 0 && q < NQP) del_s[q] = sum;
+  }
+  __syncthreads();
+  const float sl2 = a.scale * kLog2e;
+  f32x4 dvt[4], dkt[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) dvt[db] = dkt[db] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < NQP / 32; ++t) {
+    bf16* dsi = dST + (t & 1) * DSB;
+    if (kw) {
+      f32x4 p[2], ds[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int qa = t * 32 + c * 16 + i16;
+        f32x4 s_acc = {0.f, 0.f, 0.f, 0.f}, dp_acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int qo = swz_off(qa, s * 32 + 8 * g);
+          s_acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(Qs + qo), kf[s], s_acc, 0, 0, 0);
+          dp_acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(dOs + qo), vf[s], dp_acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = t * 32 + c * 16 + g * 4 + r;
+          const bool ok = q < a.Nq && (fullk<MODE>(a, kb) || kok<MODE>(a, b, keyl, q));
+          const float pv = ok ? fexp2(s_acc[r] * sl2 - lse_s[q]) : 0.f;
+          const float mk = dropm<MODE>() && q < a.Nq ? pdrop(a, b, h, q, keyl) : 1.f;
+          p[c][r] = pv * mk;
+          ds[c][r] = pv * (dp_acc[r] * mk - del_s[q]);
+        }
+      }
+      const bf16x8 pb = pack8(p[0], p[1]), dsb = pack8(ds[0], ds[1]);
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const bf16x8 dot = tr_read8_sw(dOs, t * 32, db * 16, lane, true);
+        const bf16x8 qt = tr_read8_sw(Qs, t * 32, db * 16, lane, true);
+        dvt[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, pb, dvt[db], 0, 0, 0);
+        dkt[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, dsb, dkt[db], 0, 0, 0);
+      }
+      // this key row's dS for the chunk's queries c * 16 + 4g .. + 3 (the bf16 values dK used)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        bf16x4 w;
+        w[0] = dsb[4 * c + 0]; w[1] = dsb[4 * c + 1]; w[2] = dsb[4 * c + 2]; w[3] = dsb[4 * c + 3];
+        *(bf16x4*)(dsi + keyl * DSST + c * 16 + 4 * g) = w;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the chunk's dS^T image is complete
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (wave < 8) {  // dQ^T block (dims db * 16.., queries qb * 16..) of the chunk, over every key
+      const int qb = wave >> 2, db = wave & 3;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int kc = 0; kc < NKC; ++kc) {
+        const bool hi = kc * 32 + 16 < NKP;
+        const bf16x8 kt = tr_read8_sw(Ks, kc * 32, db * 16, lane, hi);
+        const bf16x8 dst = tr_read8(dsi, DSST, kc * 32, qb * 16, lane);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt, dst, acc, 0, 0, 0);
+      }
+      const int q = t * 32 + qb * 16 + i16;
+      if (q < a.Nq) store4((bf16*)a.dq + (int64_t)b * a.dq_bs + (int64_t)q * a.dq_rs + hoff + db * 16 + 4 * g, acc, a.scale);
+    }
+  }
+  if (kw && keyl < a.Nk) {
+    bf16* dkrow = (bf16*)a.dk + (int64_t)b * a.dk_bs + (int64_t)keyl * a.dk_rs + hoff;
+    bf16* dvrow = (bf16*)a.dv + (int64_t)b * a.dv_bs + (int64_t)keyl * a.dv_rs + hoff;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const int d0 = db * 16 + g * 4;
+      store4(dkrow + d0, dkt[db], a.scale);
+      store4(dvrow + d0, dvt[db], 1.f);
+    }
+  }
+}
+
 // dQ kernel; HDP 64: swizzled 16-row K/V images and <= 80 VGPRs (three workgroups per CU),
 // as the forward kernel.
 // BIAS: also the per-image column sums of dK and dV (AttnArgs::dbias_part), as
@@ -2079,6 +2230,7 @@ extern "C" int capk_attention_decode_rows(int dtype, int B, int H, int Nq, int N
 }
 
 static int g_bwd_slice = -1;  // capk_attention_set_bwd_slice (-1: CAPK_ATTN_BWD_SLICE)
+static int g_fused_bwd = -1;  // capk_attention_set_fused_bwd (-1: CAPK_ATTN_FUSED_BWD, default on)
 
 // bias_part != nullptr: the split kernels also write per-image dQ / dK / dV column sums
 // ([B][3*H*hd], AttnArgs::dbias_part) and *bias_fused is set; other routes leave it false.
@@ -2173,6 +2325,21 @@ static int attention_bwd_impl(int dtype, int B, int H, int Nq, int Nk, int hd, f
 #undef XBQ
     CAPK_LAUNCH_CHECK("attn_xbwd_bf16");
     return CAPK_OK;
+  }
+  // 64-wide heads without the bias sums: the fused single-pass kernel (attn_bwd_fused64)
+  static const bool fused_env = [] { const char* e = getenv("CAPK_ATTN_FUSED_BWD"); return !(e && e[0] == '0'); }();
+  if ((g_fused_bwd >= 0 ? g_fused_bwd == 1 : fused_env) && hd == 64 && !bias_part && Nq > 32 && Nk <= 256) {
+    const int nqp = (Nq + 31) & ~31, nkp = (Nk + 15) & ~15, nkc = (nkp + 31) / 32;
+    const size_t shm = (size_t)(2 * nqp + nkp) * 128 + (size_t)2 * nkc * 32 * 48 * 2 + (size_t)2 * nqp * 4;
+    if (shm <= 160 * 1024) {
+      const dim3 fg(B * H), fb(64 * std::max(8, nkp / 16));
+      switch (mode) {
+        case 0: return launch_dyn(attn_bwd_fused64<0>, fg, fb, shm, st, a, "attn_bwd_fused64");
+        case 1: return launch_dyn(attn_bwd_fused64<1>, fg, fb, shm, st, a, "attn_bwd_fused64");
+        case 2: return launch_dyn(attn_bwd_fused64<2>, fg, fb, shm, st, a, "attn_bwd_fused64");
+        default: return launch_dyn(attn_bwd_fused64<3>, fg, fb, shm, st, a, "attn_bwd_fused64");
+      }
+    }
   }
   {
     // split backward: dK/dV kernel, then dQ kernel (two head images in LDS each)
@@ -2277,6 +2444,12 @@ extern "C" int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int h
   return attention_bwd_impl(dtype, B, H, Nq, Nk, hd, scale, causal, q, q_bs, q_rs, k, k_bs, k_rs, v, v_bs, v_rs,
                             key_pad, o, o_bs, o_rs, dout, do_bs, do_rs, lse, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv,
                             dv_bs, dv_rs, drop_p, drop_seed, stream, nullptr, nullptr);
+}
+
+extern "C" int capk_attention_set_fused_bwd(int mode) {
+  CAPK_CHECK_ARG(mode >= -1 && mode <= 1, "capk_attention_set_fused_bwd: mode must be -1, 0 or 1");
+  g_fused_bwd = mode;
+  return CAPK_OK;
 }
 
 extern "C" int capk_attention_set_bwd_slice(int images) {

@@ -36,10 +36,7 @@ struct Seg2 {
   int k1, n1;
 };
 
-// PIPE (K-major operands, NST >= 4; the one-WG-per-CU decode grids): the fragments of K-tile
-// kt+1 are read from LDS while the MFMAs of K-tile kt run (two register sets, the loop unrolled
-// by two), so a wave alone on its SIMD no longer waits out the LDS latency at every K-tile.
-template <int BMX, int BKX, int NST, bool AK, bool BK, typename OutT, bool PAIR = false, bool PIPE = false>
+template <int BMX, int BKX, int NST, bool AK, bool BK, typename OutT, bool PAIR = false>
 __global__ __launch_bounds__(BMX / 32 * 64) void gemm_bf16_kernel(
     const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb, int M, int N, int K, int splits,
     Epi e, float* __restrict__ ws, Seg2 g2) {
@@ -92,59 +89,6 @@ __global__ __launch_bounds__(BMX / 32 * 64) void gemm_bf16_kernel(
 #pragma unroll
   for (int p = 0; p < NST - 1; ++p)
     if (p < nk) stage(p, p);
-  if constexpr (PIPE) {
-    static_assert(AK && BK && NST >= 4 && NST <= 5, "PIPE: K-major operands, 4- or 5-deep ring");
-    // wait until at most n stages are in flight (n < NST - 1, wave-uniform)
-    auto wait_stages = [&](int n) {
-      if (n >= 3) wait_vm<3 * C::VM_PER_STAGE>();
-      else if (n == 2) wait_vm<2 * C::VM_PER_STAGE>();
-      else if (n == 1) wait_vm<C::VM_PER_STAGE>();
-      else wait_vm<0>();
-    };
-    typedef bf16x8 Frags[BKX / 32][4];
-    Frags fa0, fb0, fa1, fb1;
-    auto rd = [&](int kt, Frags& fa, Frags& fb) {
-      const char* sc = smem + (kt % NST) * C::STAGE;
-#pragma unroll
-      for (int s = 0; s < BKX / 32; ++s) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fa[s][i] = read_frag<true, BMX, BKX>(sc, wm * 64 + i * 16, s, lane);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) fb[s][j] = read_frag<true, BN, BKX>(sc + C::A_BYTES, wn * 64 + j * 16, s, lane);
-      }
-    };
-    auto mm = [&](Frags& fa, Frags& fb) {
-#pragma unroll
-      for (int s = 0; s < BKX / 32; ++s)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s][i], fb[s][j], acc[i][j], 0, 0, 0);
-    };
-    // K-tile kt's fragments are in (fa, fb); read kt+1's into (ga, gb) under kt's MFMAs
-    auto step = [&](int kt, Frags& fa, Frags& fb, Frags& ga, Frags& gb) {
-      if (kt + 1 < nk) {
-        wait_stages(min(nk - 1, kt + NST - 2) - (kt + 1));  // tile kt+1 landed; later stages may stay in flight
-        __builtin_amdgcn_s_barrier();  // ... for every wave; every wave is done reading tile kt-1's slot
-        asm volatile("" ::: "memory");
-        if (kt + NST - 1 < nk) stage(kt + NST - 1, (kt + NST - 1) % NST);
-        rd(kt + 1, ga, gb);
-        __builtin_amdgcn_sched_barrier(0);  // the reads stay ahead of the MFMAs
-      }
-      mm(fa, fb);
-    };
-    if (nk > 0) {
-      wait_stages(min(nk, NST - 1) - 1);
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      rd(0, fa0, fb0);
-    }
-    for (int kt = 0; kt < nk; kt += 2) {
-      step(kt, fa0, fb0, fa1, fb1);
-      if (kt + 1 < nk) step(kt + 1, fa1, fb1, fa0, fb0);
-    }
-  } else {
   for (int kt = 0; kt < nk; ++kt) {
     if (kt + NST - 2 < nk) wait_vm<(NST - 2) * C::VM_PER_STAGE>();
     else wait_vm<0>();
@@ -152,26 +96,19 @@ __global__ __launch_bounds__(BMX / 32 * 64) void gemm_bf16_kernel(
     asm volatile("" ::: "memory");
     if (kt + NST - 1 < nk) stage(kt + NST - 1, (kt + NST - 1) % NST);
     const char* sc = smem + (kt % NST) * C::STAGE;
-    // every fragment of the K-tile is read before the first MFMA: with one wave per SIMD (the
-    // one-round decode grids) nothing else hides the LDS latency, and reading per 32-k half
-    // exposed it at every half (measured 0.66 us per 128x128x64 K-tile, 2.9x its MFMA time)
-    bf16x8 af[BKX / 32][4], bfr[BKX / 32][4];
 #pragma unroll
     for (int s = 0; s < BKX / 32; ++s) {
+      bf16x8 af[4], bfr[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[s][i] = read_frag<AK, BMX, BKX>(sc, wm * 64 + i * 16, s, lane);
+      for (int i = 0; i < 4; ++i) af[i] = read_frag<AK, BMX, BKX>(sc, wm * 64 + i * 16, s, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[s][j] = read_frag<BK, BN, BKX>(sc + C::A_BYTES, wn * 64 + j * 16, s, lane);
-    }
-    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the MFMAs (the scheduler sinks them)
-#pragma unroll
-    for (int s = 0; s < BKX / 32; ++s)
+      for (int j = 0; j < 4; ++j) bfr[j] = read_frag<BK, BN, BKX>(sc + C::A_BYTES, wn * 64 + j * 16, s, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[s][i], bfr[s][j], acc[i][j], 0, 0, 0);
-  }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
   }
   // (the last K-tile was waited with vmcnt(0): no operand load is outstanding here)
 
@@ -419,15 +356,6 @@ static bool deep_ring(int grid) {
   }();
   return on && grid <= 256;
 }
-// the deep ring's K-major products read K-tile kt+1's fragments under kt's MFMAs
-// (gemm_bf16_kernel PIPE; CAPK_GEMM_PIPE=1 -- off by default until measured)
-static bool pipe_on() {
-  static const bool on = [] {
-    const char* v = getenv("CAPK_GEMM_PIPE");
-    return v && v[0] == '1';
-  }();
-  return on;
-}
 static int choose_cfg(int M, int N, int K, int a_kmajor, int b_kmajor, int act) {
   int o = cfg_override();
   // K-major operands with K % 64 != 0 (e.g. Swin-T/S, C = 96): only the BK-32 rings apply
@@ -593,19 +521,13 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
 #define LAUNCH1(BMX, BKX, NST, AK, BKM, OT)                                                                     \
   hipLaunchKernelGGL((gemm_bf16_kernel<BMX, BKX, NST, AK, BKM, OT>), dim3(grid), dim3(BMX / 32 * 64), 0, st, \
                      (const bf16*)A, lda, (const bf16*)B, ldb, M, N, K, splits, e, slab, Seg2{})
-#define LAUNCH1P(AK, BKM, OT)                                                                                 \
-  hipLaunchKernelGGL((gemm_bf16_kernel<128, 64, 4, AK, BKM, OT, false, (AK) && (BKM)>), dim3(grid), dim3(256), 0, st, \
-                     (const bf16*)A, lda, (const bf16*)B, ldb, M, N, K, splits, e, slab, Seg2{})
 #define LAUNCH(AK, BKM, OT)                                    \
   do {                                                         \
     switch (cfg) {                                             \
       case 2: LAUNCH1(256, 64, 3, AK, BKM, OT); break;         \
       case 3: LAUNCH1(128, 32, 4, AK, BKM, OT); break;         \
       case 4: LAUNCH1(128, 32, 3, AK, BKM, OT); break;         \
-      case 7:                                                  \
-        if ((AK) && (BKM) && pipe_on()) LAUNCH1P(AK, BKM, OT); \
-        else LAUNCH1(128, 64, 4, AK, BKM, OT);                 \
-        break;                                                 \
+      case 7: LAUNCH1(128, 64, 4, AK, BKM, OT); break;         \
       case 8: LAUNCH1(64, 64, 2, AK, BKM, OT); break;          \
       default: LAUNCH1(128, 64, 2, AK, BKM, OT); break;        \
     }                                                          \
@@ -678,7 +600,6 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
   }
 #undef DISPATCH
 #undef LAUNCH
-#undef LAUNCH1P
 #undef LAUNCH1
   CAPK_LAUNCH_CHECK("gemm_bf16_kernel");
   if (splits > 1) {
@@ -790,16 +711,15 @@ extern "C" int capk_gemm_pair_slabs(int M, int N, int K, const void* A, int64_t 
   const int grid = cdiv(M, 128) * cdiv(N, BN) * splits;
   const bool deep = deep_ring(grid);
   g_last_cfg = deep ? 7 : 1;
-#define PAIR_LAUNCH(NST, BKM, PP)                                                                                    \
-  hipLaunchKernelGGL((gemm_bf16_kernel<128, 64, NST, true, BKM, bf16, true, PP>), dim3(grid), dim3(256), 0, S(stream), \
+#define PAIR_LAUNCH(NST, BKM)                                                                                    \
+  hipLaunchKernelGGL((gemm_bf16_kernel<128, 64, NST, true, BKM, bf16, true>), dim3(grid), dim3(256), 0, S(stream), \
                      (const bf16*)A, lda, (const bf16*)B, ldb, M, N, K, splits, e, ws, g2)
   if (deep) {
-    if (b_kmajor && pipe_on()) PAIR_LAUNCH(4, true, true);
-    else if (b_kmajor) PAIR_LAUNCH(4, true, false);
-    else PAIR_LAUNCH(4, false, false);
+    if (b_kmajor) PAIR_LAUNCH(4, true);
+    else PAIR_LAUNCH(4, false);
   } else {
-    if (b_kmajor) PAIR_LAUNCH(2, true, false);
-    else PAIR_LAUNCH(2, false, false);
+    if (b_kmajor) PAIR_LAUNCH(2, true);
+    else PAIR_LAUNCH(2, false);
   }
 #undef PAIR_LAUNCH
   CAPK_LAUNCH_CHECK("gemm_bf16_kernel(pair)");

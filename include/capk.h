@@ -220,6 +220,10 @@ int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int hd, float sc
  * CAPK_ATTN_BWD_SLICE environment value), so the dQ kernel re-reads a slice's operands while
  * they are still in the Infinity Cache.  Results are identical for every slice size. */
 int capk_attention_set_bwd_slice(int images);
+/* 64-wide heads with Nq > 32 (the ViT layers; not the bias-sum variant) take a fused
+ * single-pass backward: one workgroup per (image, head) forms P and dS once and writes dQ, dK
+ * and dV.  mode 1: on, 0: the split pair above, -1: back to CAPK_ATTN_FUSED_BWD (default on). */
+int capk_attention_set_fused_bwd(int mode);
 /* capk_attention_bwd plus the bias gradient of the fused QKV projection that produced q, k, v
  * (in_proj / c_attn / ViT query,key,value biases: autograd's sum of dQ, dK, dV over the tokens,
  * modeling_vit.py:205-216 through F.linear): dbias[3*H*hd] fp32 (+)= [colsum dQ | colsum dK |

@@ -18,7 +18,7 @@ run() {  # name seconds cmd...
 PYT="python -u -m pytest -x -q -rf --timeout 120 --timeout-method thread"
 B3="python bench.py --steps 10 --warmup 3 --no-cpu-baseline --beam-batch 0"
 S=${STEPS:-tests}
-[[ ,$S, == *,tsel,* ]] && run tsel 600 $PYT ${TESTS}
+[[ ,$S, == *,tsel,* ]] && run tsel 600 bash -c "$PYT ${TESTS}"
 [[ ,$S, == *,tests,* ]] && run tests 900 python -u -m pytest tests -m gpu -q -rf --timeout 240 --timeout-method thread
 [[ ,$S, == *,smoke,* ]] && run smoke 240 python -c "import __graft_entry__ as g; g.smoke()"
 [[ ,$S, == *,gemmab,* ]] && run gemmab ${GEMMAB_SECS:-400} python -u tools/gemm_ab.py

@@ -686,6 +686,70 @@ def test_attention_bwd_batch_slices_identical(ops):
 
 
 @cuda
+@pytest.mark.parametrize("case", ["vit", "pad_drop", "n100", "n256_gap"])
+def test_attention_fused_bwd_matches_split(ops, case):
+    """capk_attention_set_fused_bwd: the fused single-pass backward (one workgroup per (image,
+    head), P and dS formed once) against the split dK/dV + dQ pair on the same inputs -- ViT
+    shape, key padding + probability dropout, N = 100, N = 256 with a gap row between images.
+    dK and dV come from the same per-key-block loop (identical); dQ sums the same bf16 dS
+    blocks over the keys in the same order (rel. <= 5e-3), and both match fp32 autograd."""
+    from capk.ops import HeadView
+    L = ops.lib()
+    g = torch.Generator(device="cuda").manual_seed(47)
+    B, H, N, gap, p = {"vit": (12, 12, 197, 0, 0.0), "pad_drop": (9, 8, 197, 0, 0.1), "n100": (10, 4, 100, 0, 0.0),
+                       "n256_gap": (6, 4, 256, 1, 0.0)}[case]
+    hd = 64
+    D = H * hd
+    rows = (B - 1) * (N + gap) + N
+    qkv = torch.randn(rows, 3 * D, device="cuda", generator=g).bfloat16()
+    do = torch.randn(rows, D, device="cuda", generator=g).bfloat16()
+    o = torch.empty(rows, D, device="cuda", dtype=torch.bfloat16)
+    key_pad = None
+    if case == "pad_drop":
+        key_pad = torch.zeros(B, N, dtype=torch.bool, device="cuda")
+        key_pad[3, 150:] = True
+        key_pad[5, 7:12] = True
+    hv = lambda t, off, ld: HeadView(t, off, (N + gap) * ld, ld)
+    sc = 1.0 / math.sqrt(hd)
+    drop = (p, 4321) if p > 0 else ops.NO_DROP
+    lse, kp = ops.attention_fwd(hv(qkv, 0, 3 * D), hv(qkv, D, 3 * D), hv(qkv, 2 * D, 3 * D), hv(o, 0, D), B, H, N, N,
+                                hd, sc, key_pad=key_pad, drop=drop)
+    outs = []
+    try:
+        for mode in (0, 1):
+            ops.check(L.capk_attention_set_fused_bwd(mode), "set_fused_bwd")
+            d = torch.zeros_like(qkv)
+            ops.attention_bwd(hv(qkv, 0, 3 * D), hv(qkv, D, 3 * D), hv(qkv, 2 * D, 3 * D), hv(o, 0, D), hv(do, 0, D),
+                              lse, hv(d, 0, 3 * D), hv(d, D, 3 * D), hv(d, 2 * D, 3 * D), B, H, N, N, hd, sc,
+                              key_pad_u8=kp, drop=drop)
+            outs.append(d)
+    finally:
+        L.capk_attention_set_fused_bwd(-1)
+    split, fused = outs
+    assert bool(torch.isfinite(fused.float()).all())
+    assert torch.equal(fused[:, D:], split[:, D:])  # dK, dV
+    assert _rel(fused[:, :D], split[:, :D]) < 5e-3  # dQ
+    if gap:
+        gap_rows = torch.stack([fused[b * (N + gap) + N] for b in range(B - 1)])
+        assert float(gap_rows.abs().max()) == 0.0
+    if p == 0.0:  # vs fp32 autograd on the same bf16 values
+        def heads(col0):
+            t = torch.stack([qkv[b * (N + gap):b * (N + gap) + N, col0:col0 + D] for b in range(B)]).float()
+            return t.view(B, N, H, hd).transpose(1, 2).requires_grad_(True)
+        qr, kr, vr = heads(0), heads(D), heads(2 * D)
+        ref = _attn_ref(qr, kr, vr, sc, False, key_pad)
+        dor = torch.stack([do[b * (N + gap):b * (N + gap) + N] for b in range(B)]).float().view(B, N, H, hd).transpose(1, 2)
+        ref.backward(dor)
+
+        def got(col0):
+            return torch.stack([fused[b * (N + gap):b * (N + gap) + N, col0:col0 + D] for b in range(B)]).float().view(
+                B, N, H, hd).transpose(1, 2)
+        assert _rel(got(0), qr.grad) < 3e-2
+        assert _rel(got(D), kr.grad) < 3e-2
+        assert _rel(got(2 * D), vr.grad) < 3e-2
+
+
+@cuda
 def test_gemm_timer_follows_the_stream(ops):
     """bench.py's live GEMM timer (ops.GEMM_TIMER) records the GEMMs launched on the stream it
     was started on from any host thread -- those of a backward pass run on autograd's device
