@@ -144,7 +144,7 @@ __global__ __launch_bounds__(BMX / 32 * 64) void gemm_bf16_kernel(
         float v[8];
         Vec8<float>::load(stg + row * C::EPI_LD + ecol, v);
         if (ws) Vec8<float>::store(ws + ((int64_t)split * M + gm) * N + egn, v);
-        else epilogue8<OutT>(e, gm, egn, v, bias8, side[h][it], has_side);
+        else epilogue8<OutT>(e, gm, egn, v, e.bias ? bias8 : nullptr, has_side ? &side[h][it] : nullptr);
       }
     }
     lds_barrier();

@@ -344,7 +344,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(const void* __restrict__ A,
         float v[8];
         Vec8<float>::load(stg + row * EPI_LD + ecol, v);
         if (ws) Vec8<float>::store(ws + ((int64_t)split * M + gm) * N + egn, v);
-        else epilogue8<OutT>(e, gm, egn, v, bias8, side[qm * 2 + (it >> 2)][it & 3], has_side);
+        else epilogue8<OutT>(e, gm, egn, v, e.bias ? bias8 : nullptr, has_side ? &side[qm * 2 + (it >> 2)][it & 3] : nullptr);
       }
     }
     lds_barrier();

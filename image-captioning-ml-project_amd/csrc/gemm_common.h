@@ -34,14 +34,11 @@ template <> struct Raw8<float> {
   __device__ __forceinline__ float get(int i) const { return i < 4 ? a[i] : b[i - 4]; }
 };
 
-// bias8 / side: operands the caller loaded before its first store (use_* false: load here).
-// side is aux for a backward activation, else the residual.  The prefetched operands are
-// selected by flags, never by a null-or-array pointer: a pointer select between a private
-// array and null keeps the array in scratch memory (SROA cannot split it), which cost the
-// 128x128 ring 144 B and the 256x256 kernel 528-784 B of scratch per lane.
+// bias8 / side: operands the caller loaded before its first store (nullptr: load here).
+// side is aux for a backward activation, else the residual.
 template <typename OutT>
-__device__ __forceinline__ void epilogue8_core(const Epi& e, int m, int n, float (&v)[8], const float* bias8, bool use_bias8,
-                                               const Raw8<OutT>* side, bool use_side) {
+__device__ __forceinline__ void epilogue8(const Epi& e, int m, int n, float (&v)[8], const float* bias8 = nullptr,
+                                          const Raw8<OutT>* side = nullptr) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) v[i] *= e.alpha;
   if (e.beta != 0.f) {
@@ -52,7 +49,7 @@ __device__ __forceinline__ void epilogue8_core(const Epi& e, int m, int n, float
   }
   if (e.bias) {
     float b[8];
-    if (use_bias8) {
+    if (bias8) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) b[i] = bias8[i];
     } else {
@@ -63,7 +60,7 @@ __device__ __forceinline__ void epilogue8_core(const Epi& e, int m, int n, float
   }
   if (e.act & CAPK_ACT_BWD) {
     float a[8];
-    if (use_side) {
+    if (side) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) a[i] = side->get(i);
     } else {
@@ -97,7 +94,7 @@ __device__ __forceinline__ void epilogue8_core(const Epi& e, int m, int n, float
   }
   if (e.res) {
     float r[8];
-    if (use_side && !(e.act & CAPK_ACT_BWD)) {
+    if (side && !(e.act & CAPK_ACT_BWD)) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) r[i] = side->get(i);
     } else {
@@ -107,17 +104,6 @@ __device__ __forceinline__ void epilogue8_core(const Epi& e, int m, int n, float
     for (int i = 0; i < 8; ++i) v[i] += r[i];
   }
   Vec8<OutT>::store((OutT*)e.C + (int64_t)m * e.ldc + n, v);
-}
-// no prefetched operands
-template <typename OutT>
-__device__ __forceinline__ void epilogue8(const Epi& e, int m, int n, float (&v)[8]) {
-  epilogue8_core<OutT>(e, m, n, v, nullptr, false, nullptr, false);
-}
-// the thread's bias columns (loaded whenever e.bias) and one side segment (valid if use_side)
-template <typename OutT>
-__device__ __forceinline__ void epilogue8(const Epi& e, int m, int n, float (&v)[8], const float (&bias8)[8],
-                                          const Raw8<OutT>& side, bool use_side) {
-  epilogue8_core<OutT>(e, m, n, v, bias8, e.bias != nullptr, &side, use_side);
 }
 
 // Epilogue operand prefetch.  On gfx9 vmcnt counts stores as well as loads, in order,
