@@ -77,33 +77,53 @@ __global__ __launch_bounds__(256) void ln_fwd_slabs_kernel(int rows, int cols, c
   const int64_t ss = (int64_t)rows * cols;
   float v[MAXC][8];
   float s = 0.f;
+  // the slabs of both of the lane's chunks in groups of 4 splits, every load of a group issued
+  // before its first use (a per-split loop waited out one memory round trip per slab and chunk:
+  // 16 for the FC2 slabs of a decode step); summed in split order as before
+  float a[MAXC][8];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[c][i] = 0.f;
+  for (int k0 = 0; k0 < splits; k0 += 4) {
+    float t[MAXC][4][8];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = lane + c * 64;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (ch < nch && k0 + j < splits) Vec8<float>::load(ws + (k0 + j) * ss + (int64_t)row * cols + ch * 8, t[c][j]);
+    }
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = lane + c * 64;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (ch < nch && k0 + j < splits) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) a[c][i] += t[c][j][i];
+        }
+    }
+  }
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     const int ch = lane + c * 64;
     if (ch < nch) {
-      float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      const float* p = ws + (int64_t)row * cols + ch * 8;
-      for (int k = 0; k < splits; ++k, p += ss) {
-        float t[8];
-        Vec8<float>::load(p, t);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) a[i] += t[i];
-      }
       if (bias) {
         float bb[8];
         Vec8<float>::load(bias + ch * 8, bb);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) a[i] += bb[i];
+        for (int i = 0; i < 8; ++i) a[c][i] += bb[i];
       }
       if (res) {
         float r[8];
         Vec8<bf16>::load(res + (int64_t)row * ldr + ch * 8, r);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) a[i] += r[i];
+        for (int i = 0; i < 8; ++i) a[c][i] += r[i];
       }
       bf16x8 hx;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) hx[i] = (bf16)a[i];
+      for (int i = 0; i < 8; ++i) hx[i] = (bf16)a[c][i];
       if (x_out) *(bf16x8*)(x_out + (int64_t)row * ldxo + ch * 8) = hx;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
