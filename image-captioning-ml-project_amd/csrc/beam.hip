@@ -111,6 +111,25 @@ __device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2
 // (rank counting) when it could overflow.  All control flow on the filter is
 // wave-uniform (ballots), so there is no per-lane insertion divergence.
 static constexpr int WAVE_CAP = 128;
+static constexpr int RPD = 4;  // logits chunk loads in flight per wave
+
+template <typename T> struct RawRow8;
+template <> struct RawRow8<bf16> {
+  bf16x8 a;
+  __device__ __forceinline__ void load(const bf16* p) { a = *(const bf16x8*)p; }
+  __device__ __forceinline__ void cvt(float (&v)[8]) const {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)a[j];
+  }
+};
+template <> struct RawRow8<float> {
+  f32x4 a, b;
+  __device__ __forceinline__ void load(const float* p) { a = *(const f32x4*)p; b = *(const f32x4*)(p + 4); }
+  __device__ __forceinline__ void cvt(float (&v)[8]) const {
+    v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+    v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+  }
+};
 
 __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
   const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l), hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
@@ -152,7 +171,14 @@ __global__ __launch_bounds__(ROWS_THREADS) void beam_rows_kernel(const T* __rest
   __shared__ float sm[4], ss[4];
   uint64_t* wb = wbuf[w];
   float m = -INFINITY, s = 0.f;
+  // thr: the K2-th best (value, -index) key buffered so far; thr_f its value, a float
+  // pre-filter (v >= thr_f keeps every key >= thr; offer() applies the exact test)
   uint64_t thr = 0;
+  float thr_f = -INFINITY;
+  auto set_thr = [&](uint64_t t) {
+    thr = t;
+    thr_f = t ? funkey((uint32_t)(t >> 32)) : -INFINITY;
+  };
   int cnt = 0;
   auto offer = [&](uint64_t key) {  // wave-uniform call
     bool p = key != 0 && key >= thr;
@@ -160,7 +186,7 @@ __global__ __launch_bounds__(ROWS_THREADS) void beam_rows_kernel(const T* __rest
     if (!mask) return;
     if (cnt + 64 > WAVE_CAP) {
       cnt = wave_compact(wb, cnt, K2, lane);
-      if (cnt == K2) thr = wb[K2 - 1];
+      if (cnt == K2) set_thr(wb[K2 - 1]);
       p = key != 0 && key >= thr;
       mask = __ballot(p);
       if (!mask) return;
@@ -170,25 +196,17 @@ __global__ __launch_bounds__(ROWS_THREADS) void beam_rows_kernel(const T* __rest
   };
   const int V8 = V & ~7;
   bool first = true;
-  // the next chunk's 16-B load is issued before this chunk is filtered (one load in flight
-  // behind the filter's ballots and LDS appends)
-  float vn[8];
-  auto load_chunk = [&](int c, float (&d)[8]) {
-    const int i = c + lane * 8;
-    if (i < V8) Vec8<T>::load(x + i, d);
-    else {
+  // One 512-logit chunk (8 per lane at column i).  FULL: every lane in range (all chunks but
+  // a row's last), so the -inf masking and the validity exec mask are compiled out.  Keys are
+  // built only for the wave's first chunk (threshold seed) and for elements that pass the
+  // float pre-filter; each pass of the offer loop takes one such element per lane.
+  auto process = [&](auto full_tag, float (&v)[8], int i) {
+    constexpr bool FULL = decltype(full_tag)::value;
+    const bool valid = FULL || i < V8;
+    if (!FULL && !valid) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] = -INFINITY;
+      for (int j = 0; j < 8; ++j) v[j] = -INFINITY;
     }
-  };
-  if (w * 512 < V8) load_chunk(w * 512, vn);
-  for (int c0 = w * 512; c0 < V8; c0 += 4 * 512) {
-    const int i = c0 + lane * 8;
-    const bool valid = i < V8;
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = vn[j];
-    if (c0 + 4 * 512 < V8) load_chunk(c0 + 4 * 512, vn);
     float cm = v[0];
 #pragma unroll
     for (int j = 1; j < 8; ++j) cm = fmaxf(cm, v[j]);
@@ -199,26 +217,59 @@ __global__ __launch_bounds__(ROWS_THREADS) void beam_rows_kernel(const T* __rest
     }
     if (first) {  // threshold from the K2-th best lane maximum of the first chunk
       first = false;
-      uint64_t km = 0;
+      uint64_t kmax = 0;
       if (valid) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { const uint64_t kk = ckey(v[j], i + j); km = kk > km ? kk : km; }
+        for (int j = 0; j < 8; ++j) { const uint64_t kk = ckey(v[j], i + j); kmax = kk > kmax ? kk : kmax; }
       }
       int rank = 0;
-      for (int o = 0; o < 64; ++o) rank += readlane_u64(km, o) > km;
-      const uint64_t ball = __ballot(km != 0 && rank == K2 - 1);
-      thr = ball ? readlane_u64(km, __builtin_ctzll(ball)) : 0;
+      for (int o = 0; o < 64; ++o) rank += readlane_u64(kmax, o) > kmax;
+      const uint64_t ball = __ballot(kmax != 0 && rank == K2 - 1);
+      set_thr(ball ? readlane_u64(kmax, __builtin_ctzll(ball)) : 0);
     }
-    // only a chunk with some key >= the threshold can append: one ballot decides for all 8
-    // (offer() raises the threshold only when it appends, so skipping is exact)
-    uint64_t kmax = 0;
-    if (valid) {
+    // offer() raises the threshold only after a compaction, and a key it then drops is below
+    // K2 buffered keys, so filtering against the threshold of the moment is exact
+    if (__ballot(valid && cm >= thr_f)) {
+      uint32_t qm = 0;
+      if (valid) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { const uint64_t kk = ckey(v[j], i + j); kmax = kk > kmax ? kk : kmax; }
+        for (int j = 0; j < 8; ++j) qm |= v[j] >= thr_f ? (1u << j) : 0u;
+      }
+      while (__ballot(qm != 0)) {
+        const int jq = qm ? __builtin_ctz(qm) : 0;
+        float vq = v[0];
+#pragma unroll
+        for (int j = 1; j < 8; ++j) vq = j == jq ? v[j] : vq;
+        const uint64_t key = qm ? ckey(vq, i + jq) : 0;
+        qm &= qm - 1;
+        offer(key);
+      }
     }
-    if (__ballot(kmax != 0 && kmax >= thr)) {
+  };
+  // Chunk q of wave w covers [w*512 + q*2048, +512).  RPD chunk loads stay in flight per
+  // wave: raw 16-B registers, issued unconditionally (lanes past V8 read the row start and
+  // are masked after the load), so no exec-masked branch forces a wait right after the load.
+  const int c_first = __builtin_amdgcn_readfirstlane(w) * 512;  // wave-uniform (scalar loop control)
+  const int nq = c_first < V8 ? (V8 - c_first + 2047) / 2048 : 0;
+  RawRow8<T> buf[RPD];
+  auto issue = [&](int q, RawRow8<T>& d) {
+    const int i = c_first + q * 2048 + lane * 8;
+    d.load(x + (i < V8 ? i : 0));
+  };
+  // the chunk count is rounded up to a multiple of RPD: chunks past the row are all-invalid
+  // (their loads hit the row's first line), which keeps every load unconditional
 #pragma unroll
-      for (int j = 0; j < 8; ++j) offer(valid ? ckey(v[j], i + j) : 0);
+  for (int sl = 0; sl < RPD; ++sl) issue(sl, buf[sl]);
+  for (int q0 = 0; q0 < nq; q0 += RPD) {
+#pragma unroll
+    for (int sl = 0; sl < RPD; ++sl) {
+      const int q = q0 + sl;
+      const int c0 = c_first + q * 2048;
+      float v[8];
+      buf[sl].cvt(v);
+      issue(q + RPD, buf[sl]);
+      if (c0 + 512 <= V8) process(std::true_type{}, v, c0 + lane * 8);
+      else if (c0 < V8) process(std::false_type{}, v, c0 + lane * 8);
     }
   }
   for (int t0 = V8 + w * 64; t0 < V; t0 += 256) {  // tail (< 8 elements, one wave-uniform pass)

@@ -132,6 +132,52 @@ def test_device_beam_bf16_logits_runs():
     assert same >= 5 / 6
 
 
+def _filter_row(kind, V):
+    i = torch.arange(V, dtype=torch.float32)
+    if kind == "ascending":      # every chunk beats the running threshold: many compactions
+        return i / 64.0
+    if kind == "descending":
+        return -i / 64.0
+    if kind == "flat":           # all tied: the lowest indices win
+        return torch.zeros(V)
+    if kind == "sawtooth":       # the same 512-pattern in every chunk: ties across chunks
+        return (i % 512) / 8.0
+    if kind == "tail_spikes":    # winners in the last partial chunk and the < 8 tail
+        r = torch.full((V,), -30.0)
+        for j, p in enumerate([V - 1, V - 2, V - 9, max(V - 300, V // 3), V // 2, 3]):
+            r[p] = 5.0 - 0.5 * j
+        return r
+    g = torch.Generator().manual_seed(V)
+    return torch.randn(V, generator=g)
+
+
+@cuda
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("V", [61, 4099, 50257])
+@pytest.mark.parametrize("kind", ["ascending", "descending", "flat", "sawtooth", "tail_spikes", "randn"])
+def test_beam_rows_candidate_filter(kind, V, dtype):
+    """The per-row top-2k filter of beam_rows_kernel on adversarial rows: one search step
+    (max_length 2, so the k best continuations of beam 0 all finish) must pick exactly the k
+    tokens ranked by (value desc, index asc), with log_softmax scores."""
+    from capk.beam import beam_search
+    B, k = 2, 5
+    row = _filter_row(kind, V).to(dtype).float()
+    order = np.lexsort((np.arange(V), -row.numpy()))[:k]
+    want_lp = torch.log_softmax(row.double(), 0)[torch.from_numpy(order)].float()
+
+    def fn(seqs):
+        return row.expand(seqs.shape[0], V).clone()
+
+    prompt = torch.tensor([0, 1])
+    step = HostLogits(fn, prompt.repeat_interleave(k)[:, None], dtype=dtype, pad_cols=(8 - V % 8) % 8 + 8)  # ld % 8 == 0
+    out = beam_search(step, B, k, 2, prompt.cuda(), V + 5, pad_token_id=0, vocab_size=V)
+    for b in range(B):
+        got = out["all_sequences"][b, :, 1].cpu().numpy()
+        assert sorted(got.tolist()) == sorted(order.tolist()), (kind, V, b, got, order)
+        torch.testing.assert_close(out["all_scores"][b].cpu().sort().values, want_lp.sort().values, rtol=1e-5,
+                                   atol=1e-5)
+
+
 @cuda
 def test_gather_rows_kernel():
     from capk import ops
