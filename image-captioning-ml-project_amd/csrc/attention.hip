@@ -1321,8 +1321,9 @@ __global__ __launch_bounds__(256) void attn_decode_bf16(AttnArgs a) {
 //    kernels' pdrop index, so attn_bwd recomputes the same keep decisions.  No causal mask;
 //    key padding honoured.  lse (natural log) written for the backward.
 template <int HDP, int MODE, int NQT>
-__global__ __launch_bounds__(256) void attn_xdec_bf16(AttnArgs a) {
-  constexpr int NW = 4, KPW = 64, ST = HDP + 16, NCH = HDP / 8, NS = HDP / 32, ND = HDP / 16, NQ = 16 * NQT;
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HDP == 96 ? 3 : 1, 8))) void attn_xdec_bf16(
+    AttnArgs a) {
+  constexpr int NW = 4, KPW = 64, ST = HDP + (HDP == 96 ? 8 : 16), NCH = HDP / 8, NS = HDP / 32, ND = HDP / 16, NQ = 16 * NQT;
   static_assert(NQ * HDP * 4 <= KPW * ST * 2, "the fp32 partial O of a wave fits its V image");
   __shared__ __attribute__((aligned(16))) bf16 vimg[NW][KPW * ST];
   __shared__ float mm[NW][NQ], ll[NW][NQ];

@@ -338,6 +338,7 @@ __global__ __launch_bounds__(64) void beam_update_kernel(BeamState st, int k, in
   for (int e = lane; e < k * L; e += 64) { o_rseq[e] = st.rseq[sb * L + e]; o_seq[e] = st.seq[sb * L + e]; }
   for (int e = lane; e < k * Lb; e += 64) { o_rbi[e] = st.rbi[sb * Lb + e]; o_bi[e] = st.bi[sb * Lb + e]; }
   const int unsat_old = st.unsat[b];
+  const int fin_l = lane < k ? st.fin[sb + lane] : 1;
   // 1. candidates: k rows x K2, score = ((x - max) - logsum) + running (torch log_softmax + add)
   const int nc = k * K2;  // <= 128
   float cs[2];
@@ -357,14 +358,22 @@ __global__ __launch_bounds__(64) void beam_update_kernel(BeamState st, int k, in
       ck[h] = ckey(cs[h], rr * V + tok);
     }
   }
-  // rank-count over all candidates (keys unique: flat index unique)
+  // rank-count over all candidates (keys unique: flat index unique); the other lanes' keys
+  // are read with v_readlane (uniform lane index), not a permute round trip per candidate
+  int rk[2] = {0, 0};
+  for (int c2 = 0; c2 < (nc < 64 ? nc : 64); ++c2) {
+    const uint64_t o = readlane_u64(ck[0], c2);
+    rk[0] += (o > ck[0]) ? 1 : 0;
+    rk[1] += (o > ck[1]) ? 1 : 0;
+  }
+  for (int c2 = 64; c2 < nc; ++c2) {
+    const uint64_t o = readlane_u64(ck[1], c2 - 64);
+    rk[0] += (o > ck[0]) ? 1 : 0;
+    rk[1] += (o > ck[1]) ? 1 : 0;
+  }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    int rank = 0;
-    for (int c2 = 0; c2 < nc; ++c2) {
-      const uint64_t o = __shfl(ck[c2 >= 64 ? 1 : 0], c2 & 63, 64);
-      rank += (o > ck[h]) ? 1 : 0;
-    }
+    const int rank = rk[h];
     const int c = lane + 64 * h;
     if (c < nc && rank < K2) {
       const int flat = (int)(0xFFFFFFFFu - (uint32_t)ck[h]);
@@ -375,14 +384,13 @@ __global__ __launch_bounds__(64) void beam_update_kernel(BeamState st, int k, in
   }
   __syncthreads();
   // 2. stopping criteria per continuation; running log-probs with the -1e9 penalty
+  const int full = __ballot(fin_l == 0) == 0;  // all k finished slots of this image taken
   if (lane < K2) {
     const int hit = (t_tok[lane] == eos) || (cur_len + 1 >= L);
     t_hit[lane] = hit;
     t_trl[lane] = t_lp[lane] + (hit ? -1.0e9f : -0.0f);
     // finished-candidate score: lp / len^lp, + full, + !unsat, + !just_finished penalties (utils.py:3175-3190)
     float sc = t_lp[lane] / fin_div;
-    int full = 1;
-    for (int i = 0; i < k; ++i) full &= (st.fin[sb + i] != 0);
     sc += (full && early_true) ? -1.0e9f : -0.0f;
     sc += unsat_old ? -0.0f : -1.0e9f;
     const int jf = hit && (lane < k);
@@ -390,21 +398,18 @@ __global__ __launch_bounds__(64) void beam_update_kernel(BeamState st, int k, in
     m_score[k + lane] = sc;
     m_fin[k + lane] = jf;
   }
-  if (lane < k) { m_score[lane] = st.score[sb + lane]; m_fin[lane] = st.fin[sb + lane]; }
+  if (lane < k) { m_score[lane] = st.score[sb + lane]; m_fin[lane] = fin_l; }
   __syncthreads();
   // 3. top-k running (ties: lower position first) and top-k finished over the merged list
-  if (lane < K2) {
-    const uint64_t me = ckey(t_trl[lane], lane);
-    int rank = 0;
-    for (int j = 0; j < K2; ++j) rank += (ckey(t_trl[j], j) > me) ? 1 : 0;
-    if (rank < k) { nxt[rank] = lane; n_rscore[rank] = t_trl[lane]; }
-  }
-  const int nm = k + K2;
-  if (lane < nm) {
-    const uint64_t me = ckey(m_score[lane], lane);
-    int rank = 0;
-    for (int j = 0; j < nm; ++j) rank += (ckey(m_score[j], j) > me) ? 1 : 0;
-    if (rank < k) msel[rank] = lane;
+  {
+    const int nm = k + K2;
+    const uint64_t me_r = lane < K2 ? ckey(t_trl[lane], lane) : 0;
+    const uint64_t me_m = lane < nm ? ckey(m_score[lane], lane) : 0;
+    int rank_r = 0, rank_m = 0;
+    for (int j = 0; j < K2; ++j) rank_r += (readlane_u64(me_r, j) > me_r) ? 1 : 0;
+    for (int j = 0; j < nm; ++j) rank_m += (readlane_u64(me_m, j) > me_m) ? 1 : 0;
+    if (lane < K2 && rank_r < k) { nxt[rank_r] = lane; n_rscore[rank_r] = t_trl[lane]; }
+    if (lane < nm && rank_m < k) msel[rank_m] = lane;
   }
   __syncthreads();
   // 4. write the new running state
