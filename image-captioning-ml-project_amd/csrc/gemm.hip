@@ -151,6 +151,86 @@ __global__ __launch_bounds__(BMX / 32 * 64) void gemm_bf16_kernel(
   }
 }
 
+// 64x64 tile, four waves of 32x32 (cfg 9), K-major operands, no split-K: the one-round decode
+// products (M = k·B rows of a beam step).  A 128x128 tile gives each wave a 64x64 block, i.e.
+// 32 MFMA 16x16x32 per 64-deep K-tile on one SIMD (~0.43 us of the measured 0.66 us per
+// K-tile), and at <= 256 tiles only a quarter of the chip's SIMDs: here every wave issues 8
+// MFMAs per K-tile and a 1280 x 768 product runs 240 WGs x 4 waves.
+template <int NST, typename OutT>
+__global__ __launch_bounds__(256) void gemm_s64_kernel(const bf16* __restrict__ A, int64_t lda,
+                                                       const bf16* __restrict__ B, int64_t ldb, int M, int N, int K,
+                                                       Epi e) {
+  constexpr int T = 64, BKX = 64, TB = T * BKX * 2, STAGE = 2 * TB, EPI_LD = T + 4;
+  constexpr int SMEM = (NST * STAGE > T * EPI_LD * 4) ? NST * STAGE : T * EPI_LD * 4;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ntn = (N + T - 1) / T;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (wg / ntn) * T, n0 = (wg % ntn) * T;
+  const int nk = K / BKX;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0, 0x00020000);  // unused (K-major)
+  auto stage = [&](int kt, int slot) {
+    char* base = smem + slot * STAGE;
+    stage_tile<true, T, BKX, 2>(A, lda, M, m0, kt * BKX, base, wave * 2, lane, rs);
+    stage_tile<true, T, BKX, 2>(B, ldb, N, n0, kt * BKX, base + TB, wave * 2, lane, rs);
+  };
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int p = 0; p < NST - 1; ++p)
+    if (p < nk) stage(p, p);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + NST - 2 < nk) wait_vm<(NST - 2) * 4>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + NST - 1 < nk) stage(kt + NST - 1, (kt + NST - 1) % NST);
+    const char* sc = smem + (kt % NST) * STAGE;
+#pragma unroll
+    for (int s = 0; s < BKX / 32; ++s) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = read_frag<true, T, BKX>(sc, wm * 32 + i * 16, s, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j] = read_frag<true, T, BKX>(sc + TB, wn * 32 + j * 16, s, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  // epilogue: accumulators -> LDS (fp32 [64][68]) -> 8-wide rows, 8 threads per row
+  constexpr int ITS = T * T / 8 / 256;
+  const int ecol = (tid & 7) * 8, egn = n0 + ecol;
+  float bias8[8];
+  Raw8<OutT> side[1][ITS];
+  const bool has_side = prefetch_side<OutT, 1, ITS, 256, 8>(e, m0, egn, tid, bias8, side);
+  lds_barrier();
+  float* stg = (float*)smem;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        stg[(wm * 32 + i * 16 + (lane >> 4) * 4 + r) * EPI_LD + wn * 32 + j * 16 + (lane & 15)] = acc[i][j][r];
+  lds_barrier();
+#pragma unroll
+  for (int it = 0; it < ITS; ++it) {
+    const int row = (it * 256 + tid) >> 3;
+    const int gm = m0 + row;
+    if (gm < M && egn < N) {
+      float v[8];
+      Vec8<float>::load(stg + row * EPI_LD + ecol, v);
+      epilogue8<OutT>(e, gm, egn, v, e.bias ? bias8 : nullptr, has_side ? &side[0][it] : nullptr);
+    }
+  }
+}
+
 // Activation pass after the 256x256 kernel's plain product (the split activation route):
 // forward: C holds pre = acc + bias; writes act(pre) to C and pre or act'(pre)
 // (CAPK_ACT_DERIV) to `pre`.  Backward: C holds dY.W; multiplies by act'(aux) or by aux
@@ -335,12 +415,15 @@ static int cfg_override() {
 //   6: the same tile as a persistent kernel with a register-direct epilogue (gemm8q.hip)
 //   7: 128x128, BK 64, 4-deep ring (128 KiB, 1 WG/CU): grids of at most one WG per CU
 //   8: 64x128, BK 64, 2-deep ring, 2 waves (48 KiB, 3 WGs/CU): K-major operands only
+//   9: 64x64, BK 64, 3-deep ring, 4 waves of 32x32 (48 KiB, 3 WGs/CU): K-major operands,
+//      K % 64 == 0, no split-K (gemm_s64_kernel)
 static bool big_tile(int cfg) { return cfg == 5 || cfg == 6; }
 static int slots_of(int cfg) {  // resident WGs
-  return (cfg == 2 || cfg == 7 || big_tile(cfg)) ? 256 : (cfg == 4 || cfg == 8) ? 768 : 512;
+  return (cfg == 2 || cfg == 7 || big_tile(cfg)) ? 256 : (cfg == 4 || cfg == 8 || cfg == 9) ? 768 : 512;
 }
 static int tiles_of(int cfg, int M, int N) {
-  return cdiv(M, (cfg == 2 || big_tile(cfg)) ? 256 : cfg == 8 ? 64 : 128) * cdiv(N, big_tile(cfg) ? 256 : BN);
+  return cdiv(M, (cfg == 2 || big_tile(cfg)) ? 256 : (cfg == 8 || cfg == 9) ? 64 : 128) *
+         cdiv(N, big_tile(cfg) ? 256 : cfg == 9 ? 64 : BN);
 }
 // Measured per shape class (tools/gemm_bench.py, profiles/): the 3-WG/CU BK-32 ring wins when
 // the epilogue carries an activation (its stores overlap other WGs' main loops) and for the
@@ -363,8 +446,9 @@ static int choose_cfg(int M, int N, int K, int a_kmajor, int b_kmajor, int act) 
   if ((o == 2 || big_tile(o)) && M < 256) o = 1;
   if ((o == 3 || o == 4) && (a_kmajor || b_kmajor) && K % 32) o = 1;
   if (o == 7 && (int64_t)cdiv(M, 128) * cdiv(N, BN) > 256) o = 1;
-  if (o == 8 && !(a_kmajor && b_kmajor)) o = 1;  // the MN-major image swizzle assumes 128-row tiles
-  if (o >= 1 && o <= 8) return o;
+  if ((o == 8 || o == 9) && !(a_kmajor && b_kmajor)) o = 1;  // the MN-major image swizzle assumes 128-row tiles
+  if (o == 9 && K % 64) o = 1;
+  if (o >= 1 && o <= 9) return o;
   // Huge-M products with a short K (ResNet layer-1 convolutions at bs 128: M = 401 408 rows of
   // 56x56; the 1x1 expansion forward and backward-data and the 3x3 dcol have K = 64): with one
   // K-tile per item the 256x256 kernels are store-bound at one WG per CU and the 3-WG/CU BK-32
@@ -454,7 +538,7 @@ extern "C" size_t capk_gemm_workspace(int in_dtype, int out_dtype, int M, int N,
   if (in_dtype != CAPK_BF16) return 0;
   // upper bound over the configurations (the launch picks one of them)
   int s = 1;
-  for (int c = 1; c <= 8; ++c) s = std::max(s, choose_splits(c, M, N, K));
+  for (int c = 1; c <= 8; ++c) s = std::max(s, choose_splits(c, M, N, K));  // (cfg 9 never splits)
   const size_t slab = s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
   // persistent grids: the split-tail hand-off area (gemm8q.hip)
   return tiles_of(6, M, N) > 256 ? std::max(slab, gemm8q_tail_workspace(M, N, K)) : slab;
@@ -514,6 +598,16 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
       cfg = 5;
   }
   if (cfg == 1 && cfg_override() == 0 && deep_ring(tiles_of(1, M, N) * splits)) cfg = 7;
+  // one-round K-major products on the 64x64 four-wave tile (CAPK_GEMM_S64=0 keeps them on the
+  // 4-deep 128x128 ring, =1 only when the 64x64 grid is one round, for A/B)
+  static const int s64_mode = [] {
+    const char* v = getenv("CAPK_GEMM_S64");
+    return v ? atoi(v) : 2;
+  }();
+  if (cfg == 7 && cfg_override() == 0 && s64_mode && splits == 1 && a_kmajor && b_kmajor && K % 64 == 0 &&
+      (s64_mode == 2 || tiles_of(9, M, N) <= slots_of(9)))
+    cfg = 9;
+  if (cfg == 9) splits = 1;
   g_last_cfg = cfg;
   const int tiles = tiles_of(cfg, M, N);
   const int grid = tiles * splits;
@@ -593,6 +687,25 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
                          (const bf16*)aux, ldx, act, from_pre);
       CAPK_LAUNCH_CHECK("act_pass_kernel");
     }
+  } else if (cfg == 9) {
+    // grids past one round of the 3-deep ring (3 WGs/CU) take the 2-deep ring (32 KiB, 5 WGs/CU)
+    // (CAPK_GEMM_S64_NST2=0: always 3-deep, for A/B)
+    static const bool nst2_on = [] {
+      const char* v = getenv("CAPK_GEMM_S64_NST2");
+      return !(v && v[0] == '0');
+    }();
+#define S64(NS)                                                                                               \
+  do {                                                                                                        \
+    if (out_dtype == CAPK_BF16)                                                                               \
+      hipLaunchKernelGGL((gemm_s64_kernel<NS, bf16>), dim3(grid), dim3(256), 0, st, (const bf16*)A, lda,      \
+                         (const bf16*)B, ldb, M, N, K, e);                                                    \
+    else                                                                                                      \
+      hipLaunchKernelGGL((gemm_s64_kernel<NS, float>), dim3(grid), dim3(256), 0, st, (const bf16*)A, lda,     \
+                         (const bf16*)B, ldb, M, N, K, e);                                                    \
+  } while (0)
+    if (nst2_on && grid > slots_of(9)) S64(2);
+    else S64(3);
+#undef S64
   } else if (out_dtype == CAPK_BF16) {
     DISPATCH(bf16)
   } else {

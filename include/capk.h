@@ -75,11 +75,12 @@ size_t capk_gemm_workspace(int in_dtype, int out_dtype, int M, int N, int K);
 /* Tile configuration of the calling thread's last hand-written capk_gemm (gemm.hip
  * choose_cfg: 1-4 = 128-row tiles, 5 = the 256x256 phased kernel, 6 = the persistent
  * 256x256 kernel, 7 = the 4-deep 128x128 ring of one-WG-per-CU grids, 8 = the 64x128
- * two-wave tile). */
+ * two-wave tile, 9 = the 64x64 four-wave tile of one-round K-major products). */
 int capk_gemm_last_config(void);
-/* Test / benchmark control: force the tile configuration (cfg 1..8; 0 = automatic choice;
+/* Test / benchmark control: force the tile configuration (cfg 1..9; 0 = automatic choice;
  * -1 = CAPK_GEMM_CFG environment value) for every later capk_gemm call.  7 falls back to 1
- * on grids of more than 256 tiles, 8 to 1 unless both operands are K-major. */
+ * on grids of more than 256 tiles, 8 and 9 to 1 unless both operands are K-major (9 also
+ * needs K % 64 == 0 and never splits K). */
 int capk_gemm_force_config(int cfg);
 /* Split-K tail round of the persistent 256x256 kernel (grids of more than 256 items with a
  * partial last round and K >= 1536: the row blocks past the whole rounds run as 2+ K-splits

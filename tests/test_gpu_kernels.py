@@ -64,11 +64,11 @@ def test_linear_backward_layouts(ops, dtype):
 
 
 @cuda
-@pytest.mark.parametrize("cfg", [1, 7, 8])
+@pytest.mark.parametrize("cfg", [1, 7, 8, 9])
 @pytest.mark.parametrize("M,N,K", [(1280, 768, 768), (300, 256, 192), (517, 384, 3072), (70, 3072, 768)])
 def test_ring_configs_bf16(ops, cfg, M, N, K):
-    """The 128x128 ring tiles (1: 2-deep, 7: 4-deep, one WG per CU) and the 64x128 tile (8: two
-    waves), forced in turn on K-major products with ragged M / N: bias + GELU (kept pre-act) +
+    """The 128x128 ring tiles (1: 2-deep, 7: 4-deep, one WG per CU), the 64x128 tile (8: two
+    waves) and the 64x64 four-wave tile (9: gemm_s64_kernel, no split-K), forced in turn on K-major products with ragged M / N: bias + GELU (kept pre-act) +
     residual epilogue, and a plain product whose K split takes the slab reduce, vs the fp32
     product of the same bf16 values."""
     from capk._lib import ACT_GELU_ERF
