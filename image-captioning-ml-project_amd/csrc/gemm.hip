@@ -159,21 +159,24 @@ __global__ __launch_bounds__(BMX / 32 * 64) void gemm_bf16_kernel(
 template <int NST, typename OutT>
 __global__ __launch_bounds__(256) void gemm_s64_kernel(const bf16* __restrict__ A, int64_t lda,
                                                        const bf16* __restrict__ B, int64_t ldb, int M, int N, int K,
-                                                       Epi e) {
+                                                       int splits, Epi e, float* __restrict__ ws) {
   constexpr int T = 64, BKX = 64, TB = T * BKX * 2, STAGE = 2 * TB, EPI_LD = T + 4;
   constexpr int SMEM = (NST * STAGE > T * EPI_LD * 4) ? NST * STAGE : T * EPI_LD * 4;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int ntn = (N + T - 1) / T;
+  const int ntn = (N + T - 1) / T, ntiles = ((M + T - 1) / T) * ntn;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = (wg / ntn) * T, n0 = (wg % ntn) * T;
-  const int nk = K / BKX;
+  const int split = wg / ntiles, tile = wg % ntiles;
+  const int m0 = (tile / ntn) * T, n0 = (tile % ntn) * T;
+  // split-K (ws != nullptr: fp32 slabs [splits][M][N], no epilogue -- the LayerNorm sums them)
+  const int nk_all = K / BKX, kt_per = (nk_all + splits - 1) / splits, kt0 = split * kt_per;
+  const int nk = max(0, min(nk_all, kt0 + kt_per) - kt0);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0, 0x00020000);  // unused (K-major)
   auto stage = [&](int kt, int slot) {
     char* base = smem + slot * STAGE;
-    stage_tile<true, T, BKX, 2>(A, lda, M, m0, kt * BKX, base, wave * 2, lane, rs);
-    stage_tile<true, T, BKX, 2>(B, ldb, N, n0, kt * BKX, base + TB, wave * 2, lane, rs);
+    stage_tile<true, T, BKX, 2>(A, lda, M, m0, (kt0 + kt) * BKX, base, wave * 2, lane, rs);
+    stage_tile<true, T, BKX, 2>(B, ldb, N, n0, (kt0 + kt) * BKX, base + TB, wave * 2, lane, rs);
   };
   f32x4 acc[2][2];
 #pragma unroll
@@ -208,7 +211,7 @@ __global__ __launch_bounds__(256) void gemm_s64_kernel(const bf16* __restrict__ 
   const int ecol = (tid & 7) * 8, egn = n0 + ecol;
   float bias8[8];
   Raw8<OutT> side[1][ITS];
-  const bool has_side = prefetch_side<OutT, 1, ITS, 256, 8>(e, m0, egn, tid, bias8, side);
+  const bool has_side = !ws && prefetch_side<OutT, 1, ITS, 256, 8>(e, m0, egn, tid, bias8, side);
   lds_barrier();
   float* stg = (float*)smem;
 #pragma unroll
@@ -226,7 +229,8 @@ __global__ __launch_bounds__(256) void gemm_s64_kernel(const bf16* __restrict__ 
     if (gm < M && egn < N) {
       float v[8];
       Vec8<float>::load(stg + row * EPI_LD + ecol, v);
-      epilogue8<OutT>(e, gm, egn, v, e.bias ? bias8 : nullptr, has_side ? &side[0][it] : nullptr);
+      if (ws) Vec8<float>::store(ws + ((int64_t)split * M + gm) * N + egn, v);
+      else epilogue8<OutT>(e, gm, egn, v, e.bias ? bias8 : nullptr, has_side ? &side[0][it] : nullptr);
     }
   }
 }
@@ -698,10 +702,10 @@ extern "C" int capk_gemm(int in_dtype, int out_dtype, int M, int N, int K, const
   do {                                                                                                        \
     if (out_dtype == CAPK_BF16)                                                                               \
       hipLaunchKernelGGL((gemm_s64_kernel<NS, bf16>), dim3(grid), dim3(256), 0, st, (const bf16*)A, lda,      \
-                         (const bf16*)B, ldb, M, N, K, e);                                                    \
+                         (const bf16*)B, ldb, M, N, K, 1, e, nullptr);                                        \
     else                                                                                                      \
       hipLaunchKernelGGL((gemm_s64_kernel<NS, float>), dim3(grid), dim3(256), 0, st, (const bf16*)A, lda,     \
-                         (const bf16*)B, ldb, M, N, K, e);                                                    \
+                         (const bf16*)B, ldb, M, N, K, 1, e, nullptr);                                        \
   } while (0)
     if (nst2_on && grid > slots_of(9)) S64(2);
     else S64(3);
@@ -785,6 +789,27 @@ static int pair_splits(int M, int N, int K, bool seam) {
   return cdiv(nk, cdiv(nk, s));  // effective count: every split owns >= 1 K-tile
 }
 
+// The no-seam slab products with a K-major weight (the decode steps' out-projection / FFN2 ->
+// LayerNorm pairs) run on the 64x64 four-wave tile (cfg 9): splits so that about one round of
+// 3 WGs per CU runs, every split >= CAPK_PAIR_MINKT K-tiles (CAPK_SLAB_S64=0: the 128x128 ring
+// with pair_splits' count, for A/B).
+static bool slab_s64_on() {
+  static const bool on = [] {
+    const char* v = getenv("CAPK_SLAB_S64");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+static int s64_slab_splits(int M, int N, int K) {
+  static const int min_kt = [] {
+    const char* v = getenv("CAPK_PAIR_MINKT");
+    return v ? std::max(1, atoi(v)) : 4;
+  }();
+  const int tiles = cdiv(M, 64) * cdiv(N, 64), nk = cdiv(K, 64);
+  const int s = std::max(1, std::min(slots_of(9) / tiles, nk / min_kt));
+  return cdiv(nk, cdiv(nk, s));
+}
+
 extern "C" size_t capk_gemm_pair_workspace(int M, int N, int K, int* splits) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   const int s = pair_splits(M, N, K, true);
@@ -794,7 +819,9 @@ extern "C" size_t capk_gemm_pair_workspace(int M, int N, int K, int* splits) {
 
 extern "C" size_t capk_gemm_slabs_workspace(int M, int N, int K, int* splits) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
-  const int s = pair_splits(M, N, K, false);
+  // an upper bound over both weight layouts (capk_gemm_pair_slabs returns the count it ran)
+  int s = pair_splits(M, N, K, false);
+  if (slab_s64_on() && K % 64 == 0) s = std::max(s, s64_slab_splits(M, N, K));
   if (splits) *splits = s;
   return (size_t)s * M * N * sizeof(float);
 }
@@ -817,9 +844,23 @@ extern "C" int capk_gemm_pair_slabs(int M, int N, int K, const void* A, int64_t 
                      (!A2 || (uintptr_t)A2 % 16 == 0) && lda % 8 == 0 && ldb % 8 == 0 && lda2 % 8 == 0 &&
                      ldb2 % 8 == 0,
                  "capk_gemm_pair_slabs: operands must be 16-B aligned with leading dimensions %% 8 == 0");
-  const int splits = pair_splits(M, N, K, k1 > 0 || n1 > 0);
+  const bool s64 = slab_s64_on() && k1 == 0 && n1 == 0 && b_kmajor;
+  const int splits = s64 ? s64_slab_splits(M, N, K) : pair_splits(M, N, K, k1 > 0 || n1 > 0);
   CAPK_CHECK_ARG(ws_bytes >= (size_t)splits * M * N * sizeof(float), "capk_gemm_pair_slabs: workspace too small");
   Epi e{nullptr, N, 1.f, 0.f, nullptr, nullptr, 0, 0, nullptr, nullptr, 0, M, N, make_drop(0.f, 0)};
+  if (s64) {
+    const int grid = cdiv(M, 64) * cdiv(N, 64) * splits;
+    g_last_cfg = 9;
+    if (grid > slots_of(9))
+      hipLaunchKernelGGL((gemm_s64_kernel<2, bf16>), dim3(grid), dim3(256), 0, S(stream), (const bf16*)A, lda,
+                         (const bf16*)B, ldb, M, N, K, splits, e, ws);
+    else
+      hipLaunchKernelGGL((gemm_s64_kernel<3, bf16>), dim3(grid), dim3(256), 0, S(stream), (const bf16*)A, lda,
+                         (const bf16*)B, ldb, M, N, K, splits, e, ws);
+    CAPK_LAUNCH_CHECK("gemm_s64_kernel(slabs)");
+    if (splits_out) *splits_out = splits;
+    return CAPK_OK;
+  }
   const Seg2 g2{(const bf16*)A2, lda2, (const bf16*)B2, ldb2, k1, n1};
   const int grid = cdiv(M, 128) * cdiv(N, BN) * splits;
   const bool deep = deep_ring(grid);
