@@ -40,7 +40,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
-    ap.add_argument("--match", default="gemm_bf16_kernel,gemm8p_kernel,gemm8q_kernel,act_pass_kernel,splitk_reduce_kernel,colsum_finish_kernel")
+    ap.add_argument("--match", default="gemm_bf16_kernel,gemm_s64_kernel,gemm8p_kernel,gemm8q_kernel,act_pass_kernel,splitk_reduce_kernel,colsum_finish_kernel")
     ap.add_argument("--out")
     ap.add_argument("--cmd", default="")
     a = ap.parse_args()
@@ -51,7 +51,7 @@ def main():
     # per GEMM launch: all matched dispatches' bytes (the GEMM kernel and its companions -- the
     # split-K reduce, the column-sum finish, the activation pass) over the number of GEMM-kernel
     # dispatches, i.e. one capk_gemm call's HBM traffic
-    primary = ("gemm_bf16_kernel", "gemm8p_kernel", "gemm8q_kernel")
+    primary = ("gemm_bf16_kernel", "gemm_s64_kernel", "gemm8p_kernel", "gemm8q_kernel")
     npf = sum(1 for k in fv if any(m in fn[k] for m in primary)) or nf
     _, wn = per_dispatch(a.write_dir, "WRITE_SIZE", match)
     npw = sum(1 for k in wv if any(m in wn[k] for m in primary)) or nw
