@@ -63,6 +63,7 @@ SIGNATURES = {
     "capk_attention_bwd_bias_workspace": (_sz, [_i, _i, _i, _i, _i]),
     "capk_attention_set_bwd_slice": (_i, [_i]),
     "capk_attention_set_fused_bwd": (_i, [_i]),
+    "capk_debug_fill_lds": (_i, [ctypes.c_uint32, _c_p]),
     "capk_attention_bwd_bias": (_i, [_i, _i, _i, _i, _i, _i, _f, _i,
                                      _c_p, _i64, _i64, _c_p, _i64, _i64, _c_p, _i64, _i64,
                                      _c_p,

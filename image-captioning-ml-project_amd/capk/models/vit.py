@@ -26,10 +26,12 @@ from .._lib import ACT_DERIV, ACT_GELU_ERF, ACT_TANH
 from ..params import Fused, notify_final, store_of
 from .common import G, CapkModule, W, heads, join_dw, linear_bwd, mark
 
-# CAPK_ATTN_BIAS=1: the QKV bias gradient fused into the attention backward
-# (capk_attention_bwd_bias).  Default off: the separate column-sum pass runs on the
-# weight-gradient stream under the dX chain, and the fused kernels' extra registers cost more
-# (config-3 train 5240 -> 5122 img/s same box, profiles/round4/README.md)
+# CAPK_ATTN_BIAS=1: the QKV bias gradient from the attention backward (capk_attention_bwd_bias;
+# on the ViT shape the fused single-pass kernel sums the dQ / dK / dV it stores per (image, head),
+# round 6).  Default off: measured as a loss twice -- round 4 on the split kernels (5240 -> 5122
+# img/s, their dQ kernel spilled), round 6 on the fused kernel (5599 -> 5546 img/s same box ABAB,
+# profiles/round6/attn_bias_ab.txt: the per-workgroup reduction tail runs at one workgroup per
+# CU, 12 rounds a layer, and costs more than the 232 MB column-sum pass it replaces).
 _ATTN_BIAS = os.environ.get("CAPK_ATTN_BIAS", "0") == "1"
 
 VIT_ARCHS = {

@@ -310,7 +310,7 @@ def ce_lse_fwd(logits2d, targets, B, T, V, ignore_index, part):
     M = B * T
     loss = torch.empty(2, dtype=torch.float32, device=logits2d.device)
     lse = torch.empty(M, dtype=torch.float32, device=logits2d.device)
-    wsb = L.capk_ce_lse_workspace(B, T, logits2d.stride(0))
+    wsb = (4 + M) * 4  # the forward's share of capk_ce_lse_workspace: the count and the row losses
     ws = _ws(wsb, logits2d.device)
     nparts = part.numel() // (2 * M)
     check(L.capk_ce_lse_fwd(B, T, V, logits2d.stride(0), _p(logits2d), _p(targets), int(ignore_index), _p(part),

@@ -751,7 +751,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
 //    the chunk.
 // Same expressions as the split pair (P, dS, delta, masks, dropout index).  Requires hd == 64,
 // NKP = Nk rounded to 16 <= 256, LDS (2 NQP + NKP) x 128 B + the dS^T images <= 160 KiB.
-template <int MODE>
+// BIAS (round 6): also the per-(image, head) column sums of the dQ, dK and dV it stores (the
+// bf16 values, summed in fp32 in a fixed order) into AttnArgs::dbias_part [B][3 H 64]: the QKV
+// bias gradient of the fused projection without a column-sum pass over the 232 MB dQKV.
+template <int MODE, bool BIAS = false>
 __global__ __launch_bounds__(1024) void attn_bwd_fused64(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int HDP = 64, DSST = 48;  // dS^T image row stride: 32 queries + 16 (conflict-free transposed reads)
@@ -800,16 +803,21 @@ __global__ __launch_bounds__(1024) void attn_bwd_fused64(AttnArgs a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x < NQP) lse_s[threadIdx.x] = lse_r;  // log2 domain
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {  // delta = rowsum(dO * O), the attn_bwd_kv_bf16 order
+  // lse and delta for EVERY padded query row q < NQP (rows past Nq: 0), whatever blockDim is:
+  // the key waves read lse_s / del_s of the padded rows too (ds = 0 * (dp - del_s[q]) there,
+  // so a stale LDS word would turn into NaN)
+  for (int q = threadIdx.x; q < NQP; q += blockDim.x)
+    lse_s[q] = q == (int)threadIdx.x ? lse_r : (q < a.Nq ? a.lse_in[((int64_t)b * a.H + h) * a.Nq + q] * kLog2e : 0.f);
+  for (int it = 0; it * (int)blockDim.x < NQP * 8; ++it) {  // delta = rowsum(dO * O), the attn_bwd_kv_bf16 order
     const int idx = threadIdx.x + it * (int)blockDim.x, q = idx >> 3, c = idx & 7;
-    if (it * (int)blockDim.x >= NQP * 8) break;  // uniform over the block
+    // (uniform loop bound over the block: every wave runs whole iterations for the shuffles)
+    const bf16x8 o8 = it == 0 ? ov[0] : it == 1 ? ov[1]
+                    : (q < a.Nq ? ld8((const bf16*)a.o + (int64_t)b * a.o_bs + (int64_t)q * a.o_rs + hoff + c * 8) : zero8());
     float sum = 0.f;
     if (q < NQP) {
       const bf16x8 dv = *(const bf16x8*)(dOs + swz_off(q, c * 8));
 #pragma unroll
-      for (int i = 0; i < 8; ++i) sum += (float)ov[it][i] * (float)dv[i];
+      for (int i = 0; i < 8; ++i) sum += (float)o8[i] * (float)dv[i];
     }
     sum += __shfl_xor(sum, 1, 64);
     sum += __shfl_xor(sum, 2, 64);
@@ -821,6 +829,7 @@ __global__ __launch_bounds__(1024) void attn_bwd_fused64(AttnArgs a) {
   f32x4 dvt[4], dkt[4];
 #pragma unroll
   for (int db = 0; db < 4; ++db) dvt[db] = dkt[db] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  f32x4 qsum = {0.f, 0.f, 0.f, 0.f};  // BIAS: this lane's query column of the stored dQ, over the chunks
   for (int t = 0; t < NQP / 32; ++t) {
     bf16* dsi = dST + (t & 1) * DSB;
     if (kw) {
@@ -875,6 +884,65 @@ __global__ __launch_bounds__(1024) void attn_bwd_fused64(AttnArgs a) {
       }
       const int q = t * 32 + qb * 16 + i16;
       if (q < a.Nq) store4((bf16*)a.dq + (int64_t)b * a.dq_bs + (int64_t)q * a.dq_rs + hoff + db * 16 + 4 * g, acc, a.scale);
+      if constexpr (BIAS) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) qsum[r] += q < a.Nq ? (float)(bf16)(acc[r] * a.scale) : 0.f;
+      }
+    }
+  }
+  if constexpr (BIAS) {
+    // per wave: the sums over its 16 lanes of a row group (keys of a key wave, queries of a dQ
+    // wave) by xor shuffles, then per dimension over the waves in wave order through LDS.  The
+    // partials overwrite the Q image, which no wave reads once it has passed the last chunk's
+    // barrier (the dQ phase reads K and dS^T only); the barrier below waits for LDS only, not
+    // for the dQ stores in flight, and the dK / dV stores are issued after it.
+    float* kpart = (float*)smem;      // [16 waves][64] dK sums
+    float* vpart = kpart + 16 * 64;   // [16][64] dV sums
+    float* qpart = vpart + 16 * 64;   // [2 query blocks][64] dQ sums
+    auto lanesum = [](float v) {
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      return v;
+    };
+    if (kw) {
+      const bool in = keyl < a.Nk;
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float ks = lanesum(in ? (float)(bf16)(dkt[db][r] * a.scale) : 0.f);
+          const float vs = lanesum(in ? (float)(bf16)dvt[db][r] : 0.f);
+          if (i16 == 0) {
+            kpart[wave * 64 + db * 16 + 4 * g + r] = ks;
+            vpart[wave * 64 + db * 16 + 4 * g + r] = vs;
+          }
+        }
+    }
+    if (wave < 8) {
+      const int qb = wave >> 2, db = wave & 3;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float qs = lanesum(qsum[r]);
+        if (i16 == 0) qpart[qb * 64 + db * 16 + 4 * g + r] = qs;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (threadIdx.x < 64) {
+      const int d = threadIdx.x;
+      float ks = 0.f, vs = 0.f;
+      for (int w = 0; w < NKB; ++w) {
+        ks += kpart[w * 64 + d];
+        vs += vpart[w * 64 + d];
+      }
+      float* out = a.dbias_part + (int64_t)b * a.dbias_ld + hoff + d;
+      const int64_t D = (int64_t)a.H * 64;
+      out[0] = qpart[d] + qpart[64 + d];
+      out[D] = ks;
+      out[2 * D] = vs;
     }
   }
   if (kw && keyl < a.Nk) {
@@ -2328,12 +2396,25 @@ static int attention_bwd_impl(int dtype, int B, int H, int Nq, int Nk, int hd, f
     return CAPK_OK;
   }
   // 64-wide heads without the bias sums: the fused single-pass kernel (attn_bwd_fused64)
-  static const bool fused_env = [] { const char* e = getenv("CAPK_ATTN_FUSED_BWD"); return !(e && e[0] == '0'); }();
-  if ((g_fused_bwd >= 0 ? g_fused_bwd == 1 : fused_env) && hd == 64 && !bias_part && Nq > 32 && Nk <= 256) {
+  // CAPK_ATTN_FUSED_BWD: 0 the split pair, 1 (default) attn_bwd_fused64
+  static const int fused_env = [] { const char* e = getenv("CAPK_ATTN_FUSED_BWD"); return !(e && e[0] == '0'); }();
+  const int fmode = g_fused_bwd >= 0 ? g_fused_bwd : fused_env;
+  if (fmode >= 1 && hd == 64 && Nq > 32 && Nk <= 256) {
     const int nqp = (Nq + 31) & ~31, nkp = (Nk + 15) & ~15, nkc = (nkp + 31) / 32;
     const size_t shm = (size_t)(2 * nqp + nkp) * 128 + (size_t)2 * nkc * 32 * 48 * 2 + (size_t)2 * nqp * 4;
-    if (shm <= 160 * 1024) {
+    if (shm <= 160 * 1024) {  // (>= 8.5 KiB: the BIAS partials reuse the images)
       const dim3 fg(B * H), fb(64 * std::max(8, nkp / 16));
+      if (bias_part) {  // the QKV bias gradient's per-(image, head) column sums, [B][3 H 64]
+        a.dbias_part = bias_part;
+        a.dbias_ld = (int64_t)3 * H * hd;
+        *bias_fused = true;
+        switch (mode) {
+          case 0: return launch_dyn(attn_bwd_fused64<0, true>, fg, fb, shm, st, a, "attn_bwd_fused64");
+          case 1: return launch_dyn(attn_bwd_fused64<1, true>, fg, fb, shm, st, a, "attn_bwd_fused64");
+          case 2: return launch_dyn(attn_bwd_fused64<2, true>, fg, fb, shm, st, a, "attn_bwd_fused64");
+          default: return launch_dyn(attn_bwd_fused64<3, true>, fg, fb, shm, st, a, "attn_bwd_fused64");
+        }
+      }
       switch (mode) {
         case 0: return launch_dyn(attn_bwd_fused64<0>, fg, fb, shm, st, a, "attn_bwd_fused64");
         case 1: return launch_dyn(attn_bwd_fused64<1>, fg, fb, shm, st, a, "attn_bwd_fused64");
@@ -2450,6 +2531,24 @@ extern "C" int capk_attention_bwd(int dtype, int B, int H, int Nq, int Nk, int h
 extern "C" int capk_attention_set_fused_bwd(int mode) {
   CAPK_CHECK_ARG(mode >= -1 && mode <= 1, "capk_attention_set_fused_bwd: mode must be -1, 0 or 1");
   g_fused_bwd = mode;
+  return CAPK_OK;
+}
+
+// Test support: every CU's LDS filled with one 32-bit pattern (e.g. a NaN or -inf), so that
+// a following kernel that reads LDS words it never wrote shows it (LDS is not cleared between
+// workgroups).  4 x 256 workgroups of 40 KiB each (four per CU), plain vector LDS stores.
+__global__ __launch_bounds__(256) void debug_fill_lds_kernel(uint32_t pattern) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint32_t* w = (uint32_t*)smem;
+  for (int i = threadIdx.x; i < 40 * 1024 / 4; i += blockDim.x) w[i] = pattern;
+  __syncthreads();
+  const uint32_t back = w[(threadIdx.x * 37) % (40 * 1024 / 4)];
+  asm volatile("" ::"v"(back));  // a live read keeps the stores
+}
+
+extern "C" int capk_debug_fill_lds(uint32_t pattern, void* stream) {
+  hipLaunchKernelGGL(debug_fill_lds_kernel, dim3(4 * 256), dim3(256), 40 * 1024, S(stream), pattern);
+  CAPK_LAUNCH_CHECK("debug_fill_lds_kernel");
   return CAPK_OK;
 }
 

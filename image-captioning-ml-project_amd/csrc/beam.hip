@@ -258,8 +258,12 @@ __global__ __launch_bounds__(ROWS_THREADS) void beam_rows_kernel(const T* __rest
   };
   // the chunk count is rounded up to a multiple of RPD: chunks past the row are all-invalid
   // (their loads hit the row's first line), which keeps every load unconditional
+  // (a row shorter than one chunk, V8 == 0, issues nothing: a 16-B load at the row start would
+  // read past a short last row)
+  if (V8 > 0) {
 #pragma unroll
-  for (int sl = 0; sl < RPD; ++sl) issue(sl, buf[sl]);
+    for (int sl = 0; sl < RPD; ++sl) issue(sl, buf[sl]);
+  }
   for (int q0 = 0; q0 < nq; q0 += RPD) {
 #pragma unroll
     for (int sl = 0; sl < RPD; ++sl) {

@@ -214,43 +214,43 @@ __global__ void ce_finish_kernel(int rows, const float* __restrict__ row_loss, c
 
 // ------------------------------------- shifted CE from the LM head's partials --------
 // capk_linear_lse leaves per row P = 4 cdiv(Vp, 256) pairs (max, sum 2^(t - max)) of
-// t = log2(e) * logit over disjoint column ranges.  Forward: four waves per 64 rows, each wave
-// merging a quarter of the partials (lane = row: coalesced 8-B reads), combined through LDS
-// into lse (natural log) and the row loss lse - logit[target].  Backward: one streaming pass,
-// dlogits = (2^(t - lse log2 e) - [col == target]) * grad_scale / count with the column sums of
-// the stored gradient (the LM-head bias gradient) as per-row-group partials.
+// t = log2(e) * logit over disjoint column ranges.  Forward: CEM_ROWS rows per workgroup and
+// 32 partial streams per row (lane = (stream, row): each wave-load reads 8 rows x 8 B of 8
+// partials), stream s merging partials s, s + 32, ..., combined in stream order through LDS into
+// lse (natural log) and the row loss lse - logit[target]; M / 8 workgroups (640 at config 3) fill
+// the chip where the round-5 form (64 rows per workgroup, 197 dependent loads per lane) ran 80.
+// Backward: one streaming pass, dlogits = (2^(t - lse log2 e) - [col == target]) * grad_scale /
+// count with the column sums of the stored gradient (the LM-head bias gradient) as per-row-group
+// partials.
+constexpr int CEM_ROWS = 8, CEM_STREAMS = 32;
+__device__ __forceinline__ void lse2_merge(float& m, float& s, float m2, float s2) {
+  if (m2 == -INFINITY) return;  // an empty state (a wave whose columns were all padding)
+  const float mn = fmaxf(m, m2);
+  s = s * __builtin_amdgcn_exp2f(m - mn) + s2 * __builtin_amdgcn_exp2f(m2 - mn);
+  m = mn;
+}
 __global__ __launch_bounds__(256) void ce_lse_merge_kernel(int B, int T_, int M, int P, const float2* __restrict__ part,
                                                            const bf16* __restrict__ logits, int64_t ld,
                                                            const int64_t* __restrict__ targets, int ignore_index,
                                                            float* __restrict__ lse_out, float* __restrict__ row_loss) {
-  __shared__ float red[2][4][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int row = blockIdx.x * 64 + lane;
-  const int p0 = w * P / 4, p1 = (w + 1) * P / 4;
+  __shared__ float red[2][CEM_STREAMS][CEM_ROWS];
+  const int r = threadIdx.x & (CEM_ROWS - 1), st = threadIdx.x / CEM_ROWS;
+  const int row = blockIdx.x * CEM_ROWS + r;
   float m = -INFINITY, sum = 0.f;
   if (row < M) {
 #pragma unroll 4
-    for (int p = p0; p < p1; ++p) {
+    for (int p = st; p < P; p += CEM_STREAMS) {
       const float2 q = part[(int64_t)p * M + row];
-      if (q.x == -INFINITY) continue;  // a wave whose columns were all padding
-      const float mn = fmaxf(m, q.x);
-      sum = sum * __builtin_amdgcn_exp2f(m - mn) + q.y * __builtin_amdgcn_exp2f(q.x - mn);
-      m = mn;
+      lse2_merge(m, sum, q.x, q.y);
     }
   }
-  red[0][w][lane] = m;
-  red[1][w][lane] = sum;
+  red[0][st][r] = m;
+  red[1][st][r] = sum;
   __syncthreads();
-  if (w == 0 && row < M) {
+  if (threadIdx.x < CEM_ROWS && row < M) {
     float mm = -INFINITY, ss = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float mi = red[0][i][lane], si = red[1][i][lane];
-      if (mi == -INFINITY) continue;
-      const float mn = fmaxf(mm, mi);
-      ss = ss * __builtin_amdgcn_exp2f(mm - mn) + si * __builtin_amdgcn_exp2f(mi - mn);
-      mm = mn;
-    }
+#pragma unroll 8
+    for (int i = 0; i < CEM_STREAMS; ++i) lse2_merge(mm, ss, red[0][i][r], red[1][i][r]);
     const float lse = (mm + __log2f(ss)) * 0.6931471805599453f;
     lse_out[row] = lse;
     const int b = row / T_, t = row % T_;
@@ -754,14 +754,14 @@ extern "C" int capk_ce_lse_fwd(int B, int T, int V, int64_t ld, const void* logi
                                void* ws, size_t ws_bytes, void* stream) {
   CAPK_CHECK_ARG(B > 0 && T > 1 && V > 0 && ld >= V && logits && targets && part && nparts > 0 && lse_out && loss_out,
                  "capk_ce_lse_fwd: bad arguments");
-  CAPK_CHECK_ARG(ws && ws_bytes >= capk_ce_lse_workspace(B, T, ld), "capk_ce_lse_fwd: workspace too small");
-  const int M = B * T;
+  const int M = B * T;  // (the forward uses only the count and the row losses: 4 + M floats)
+  CAPK_CHECK_ARG(ws && ws_bytes >= (size_t)(4 + M) * sizeof(float), "capk_ce_lse_fwd: workspace too small");
   float* cnt = (float*)ws;
   float* row_loss = cnt + 4;
   hipStream_t st = S(stream);
   hipLaunchKernelGGL(ce_count_kernel, dim3(1), dim3(1024), 0, st, B, T, targets, ignore_index, cnt);
   CAPK_LAUNCH_CHECK("ce_count_kernel");
-  hipLaunchKernelGGL(ce_lse_merge_kernel, dim3(cdiv(M, 64)), dim3(256), 0, st, B, T, M, nparts, (const float2*)part,
+  hipLaunchKernelGGL(ce_lse_merge_kernel, dim3(cdiv(M, CEM_ROWS)), dim3(CEM_ROWS * CEM_STREAMS), 0, st, B, T, M, nparts, (const float2*)part,
                      (const bf16*)logits, ld, targets, ignore_index, lse_out, row_loss);
   CAPK_LAUNCH_CHECK("ce_lse_merge_kernel");
   hipLaunchKernelGGL(ce_finish_kernel, dim3(1), dim3(1024), 0, st, M, row_loss, cnt, loss_out);

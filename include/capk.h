@@ -228,6 +228,9 @@ int capk_attention_set_bwd_slice(int images);
  * single-pass backward: one workgroup per (image, head) forms P and dS once and writes dQ, dK
  * and dV.  mode 1: on, 0: the split pair above, -1: back to CAPK_ATTN_FUSED_BWD (default on). */
 int capk_attention_set_fused_bwd(int mode);
+/* Test support (no reference counterpart): fills every CU's LDS with a 32-bit pattern, so that a
+ * following kernel reading LDS words it never wrote sees that pattern (e.g. a NaN). */
+int capk_debug_fill_lds(uint32_t pattern, void* stream);
 /* capk_attention_bwd plus the bias gradient of the fused QKV projection that produced q, k, v
  * (in_proj / c_attn / ViT query,key,value biases: autograd's sum of dQ, dK, dV over the tokens,
  * modeling_vit.py:205-216 through F.linear): dbias[3*H*hd] fp32 (+)= [colsum dQ | colsum dK |
@@ -304,7 +307,8 @@ int capk_shifted_ce_weighted(int dtype, int B, int T, int V, int64_t ld, const v
  * loss_out = (mean, count) as capk_shifted_ce.  capk_ce_lse_bwd writes d(loss)/d(logits) *
  * (*grad_scale) from the logits and lse in one pass (count: DEVICE pointer, loss_out + 1), and,
  * if dbias != NULL, the column sums of that gradient over its ld columns (the LM-head bias
- * gradient, written, not accumulated). */
+ * gradient, written, not accumulated).  capk_ce_lse_workspace bounds both calls; the forward
+ * needs only (4 + B*T) floats of it. */
 size_t capk_linear_lse_part_bytes(int M, int N);
 int capk_linear_lse(int M, int N, int K, const void* x, int64_t ldx, const void* w, int64_t ldw,
                     const float* bias, void* C, int64_t ldc, int V, float* part, size_t part_bytes,

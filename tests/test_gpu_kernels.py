@@ -588,18 +588,23 @@ def test_short_attention_train(ops, case):
 
 
 @cuda
-@pytest.mark.parametrize("case", ["vit", "mask_drop", "hd128", "short", "fp32"])
+@pytest.mark.parametrize("case", ["vit", "vit_split", "mask_drop", "mask_drop_split", "hd128", "short", "fp32"])
 def test_attention_bwd_qkv_bias(ops, case):
     """capk_attention_bwd_bias: the backward plus the fused QKV bias gradient dbias = [colsum dQ |
     colsum dK | colsum dV] over the B*N tokens (the ViT query / key / value bias gradients,
-    modeling_vit.py:205-216).  ViT self-attention (N = 197, hd 64) rides on the split kernels
-    (dQ sums from sum_q dS x K in the dK/dV kernel, dK / dV sums from per-query dS / P~ sums x Q /
-    dO in the dQ kernel); key padding + dropout, hd 128, and the short / fp32 routes (separate
-    column sums) are checked against the fp32 autograd reference and against the column sums of
-    the kernel's own gradients; accumulate adds."""
+    modeling_vit.py:205-216).  ViT self-attention (N = 197, hd 64) rides on the fused single-pass
+    kernel (round 6: column sums of the bf16 values it stores, equal to the column sums of its own
+    gradients to fp32 rounding, gradients bit-identical to the plain backward) or, *_split, on
+    the split kernels (dQ sums from sum_q dS x K in the dK/dV kernel, dK / dV sums from per-query
+    dS / P~ sums x Q / dO in the dQ kernel); key padding + dropout, hd 128, and the short / fp32
+    routes (separate column sums) are checked against the fp32 autograd reference and against
+    the column sums of the kernel's own gradients; accumulate adds."""
     from capk.ops import HeadView
+    L = ops.lib()
     g = torch.Generator(device="cuda").manual_seed(31)
     p, seed, key_pad, dt = 0.0, 0, None, torch.bfloat16
+    split = case.endswith("_split")
+    case = case.replace("_split", "")
     if case == "vit":
         B, H, N, hd = 8, 12, 197, 64
     elif case == "mask_drop":
@@ -634,18 +639,29 @@ def test_attention_bwd_qkv_bias(ops, case):
     ref = torch.cat([t.grad.sum((0, 2)).reshape(-1) for t in (qr, kr, vr)])  # [h, d] order = column h*hd + d
     dqkv = torch.empty_like(qkv)
     dbias = torch.full((3 * D,), 5.0, device="cuda")
-    ops.attention_bwd_bias(Q, K_, V_, O, hv(do, 0, D), lse, hv(dqkv, 0, 3 * D), hv(dqkv, D, 3 * D),
-                           hv(dqkv, 2 * D, 3 * D), B, H, N, N, hd, sc, dbias, key_pad_u8=kp, drop=(p, seed))
+    fused = hd == 64 and N > 32 and not split and dt == torch.bfloat16  # the attn_bwd_fused64 route
+    try:
+        if split:
+            ops.check(L.capk_attention_set_fused_bwd(0), "set_fused_bwd")
+        ops.attention_bwd_bias(Q, K_, V_, O, hv(do, 0, D), lse, hv(dqkv, 0, 3 * D), hv(dqkv, D, 3 * D),
+                               hv(dqkv, 2 * D, 3 * D), B, H, N, N, hd, sc, dbias, key_pad_u8=kp, drop=(p, seed))
+        plain = torch.empty_like(qkv)  # the same route without the bias sums
+        ops.attention_bwd(Q, K_, V_, O, hv(do, 0, D), lse, hv(plain, 0, 3 * D), hv(plain, D, 3 * D),
+                          hv(plain, 2 * D, 3 * D), B, H, N, N, hd, sc, key_pad_u8=kp, drop=(p, seed))
+        acc = torch.full((3 * D,), 5.0, device="cuda")
+        ops.attention_bwd_bias(Q, K_, V_, O, hv(do, 0, D), lse, hv(dqkv, 0, 3 * D), hv(dqkv, D, 3 * D),
+                               hv(dqkv, 2 * D, 3 * D), B, H, N, N, hd, sc, acc, key_pad_u8=kp, drop=(p, seed),
+                               accumulate=True)
+    finally:
+        L.capk_attention_set_fused_bwd(-1)
     tol = 1e-4 if dt == torch.float32 else 2e-2
     scale_ref = ref.abs().max()
     assert _rel(dbias, ref) < tol, _rel(dbias, ref)
     assert float((dbias[D:2 * D] - ref[D:2 * D]).abs().max()) < tol * float(scale_ref)  # analytically ~0
     own = dqkv.float().sum(0)  # column sums of the kernel's own (rounded) gradients
-    assert _rel(dbias, own) < (1e-5 if dt == torch.float32 else 1e-2), _rel(dbias, own)
-    acc = torch.full((3 * D,), 5.0, device="cuda")
-    ops.attention_bwd_bias(Q, K_, V_, O, hv(do, 0, D), lse, hv(dqkv, 0, 3 * D), hv(dqkv, D, 3 * D),
-                           hv(dqkv, 2 * D, 3 * D), B, H, N, N, hd, sc, acc, key_pad_u8=kp, drop=(p, seed),
-                           accumulate=True)
+    assert _rel(dbias, own) < (1e-5 if dt == torch.float32 or fused else 1e-2), _rel(dbias, own)
+    if fused or split:
+        assert torch.equal(dqkv, plain)
     torch.testing.assert_close(acc, dbias + 5.0, rtol=0, atol=1e-4 * float(scale_ref) + 1e-5)
 
 
@@ -747,6 +763,51 @@ def test_attention_fused_bwd_matches_split(ops, case):
         assert _rel(got(0), qr.grad) < 3e-2
         assert _rel(got(D), kr.grad) < 3e-2
         assert _rel(got(2 * D), vr.grad) < 3e-2
+
+
+@cuda
+@pytest.mark.parametrize("nq,nk", [(200, 64), (40, 197), (256, 16), (250, 100), (197, 197), (64, 256)])
+def test_attention_fused_bwd_ragged_after_poisoned_lds(ops, nq, nk):
+    """The fused backward with Nq != Nk, at query counts past the workgroup's delta / lse passes
+    of round 5 (Nq = 200 with 64 keys: 512 threads covered 128 queries), run right after every
+    CU's LDS was filled with NaN (capk_debug_fill_lds) so a padded-row delta or lse the kernel did not write shows up as NaN.
+    dK / dV equal the split pair's, dQ within 5e-3, all three vs fp32 autograd within 3e-2."""
+    from capk.ops import HeadView
+    L = ops.lib()
+    g = torch.Generator(device="cuda").manual_seed(53)
+    B, H, hd = 6, 4, 64
+    D = H * hd
+    q = torch.randn(B * nq, D, device="cuda", generator=g).bfloat16()
+    kv = torch.randn(B * nk, 2 * D, device="cuda", generator=g).bfloat16()
+    do = torch.randn(B * nq, D, device="cuda", generator=g).bfloat16()
+    o = torch.empty(B * nq, D, device="cuda", dtype=torch.bfloat16)
+    Q, K_, V_ = HeadView(q, 0, nq * D, D), HeadView(kv, 0, nk * 2 * D, 2 * D), HeadView(kv, D, nk * 2 * D, 2 * D)
+    O, dO = HeadView(o, 0, nq * D, D), HeadView(do, 0, nq * D, D)
+    sc = 1.0 / math.sqrt(hd)
+    lse, _ = ops.attention_fwd(Q, K_, V_, O, B, H, nq, nk, hd, sc)
+    outs = []
+    try:
+        for mode in (0, 1):
+            ops.check(L.capk_attention_set_fused_bwd(mode), "set_fused_bwd")
+            dq, dkv = torch.zeros_like(q), torch.zeros_like(kv)
+            ops.check(L.capk_debug_fill_lds(0x7FC00000, ops._stream()), "debug_fill_lds")  # quiet NaN
+            ops.attention_bwd(Q, K_, V_, O, dO, lse, HeadView(dq, 0, nq * D, D), HeadView(dkv, 0, nk * 2 * D, 2 * D),
+                              HeadView(dkv, D, nk * 2 * D, 2 * D), B, H, nq, nk, hd, sc)
+            outs.append((dq, dkv))
+    finally:
+        L.capk_attention_set_fused_bwd(-1)
+    (dq_s, dkv_s), (dq_f, dkv_f) = outs
+    assert bool(torch.isfinite(dq_f.float()).all()) and bool(torch.isfinite(dkv_f.float()).all())
+    assert torch.equal(dkv_f, dkv_s)
+    assert _rel(dq_f, dq_s) < 5e-3
+    qr = q.float().view(B, nq, H, hd).transpose(1, 2).requires_grad_(True)
+    kr = kv[:, :D].float().reshape(B, nk, H, hd).transpose(1, 2).detach().requires_grad_(True)
+    vr = kv[:, D:].float().reshape(B, nk, H, hd).transpose(1, 2).detach().requires_grad_(True)
+    _attn_ref(qr, kr, vr, sc, False, None).backward(do.float().view(B, nq, H, hd).transpose(1, 2))
+    heads = lambda t, n: t.float().reshape(B, n, H, hd).transpose(1, 2)
+    assert _rel(heads(dq_f, nq), qr.grad) < 3e-2
+    assert _rel(heads(dkv_f[:, :D], nk), kr.grad) < 3e-2
+    assert _rel(heads(dkv_f[:, D:], nk), vr.grad) < 3e-2
 
 
 @cuda
