@@ -31,6 +31,7 @@ from .transformer import _history_reorder, _history_tables
 from .._lib import ACT_DERIV, ACT_GELU_TANH
 from ..ops import HeadView
 from .common import G, CapkModule, W, heads, next_seed
+from ..params import notify_final, store_of
 from .transformer import _padded_grad, _pad64
 
 PREFIX_LEN = 10  # decoders.py:540
@@ -150,6 +151,12 @@ class GPT2DecoderCore(CapkModule):
         # unused by the reference forward: no gradient, AdamW skips them (torch: grad None)
         return [self.visual_projection.weight, self.visual_projection.bias, self.image_prefix]
 
+    def _capk_store_first(self):
+        # finished last by the backward (the prefix projection, after the embeddings): in front,
+        # so ln_f and the blocks are a growing suffix for dp.GradBucketer (the tied wte -- LM
+        # head and embedding -- is registered first already)
+        return [self.image_to_prefix.weight, self.image_to_prefix.bias]
+
     def forward_logits(self, pooled, captions, use_pad_mask=True):
         """pooled [B, D], captions [B, T] int64 -> logits [B, T, V] (view of a padded buffer)."""
         return _GPT2Fn.apply(pooled, captions, self.model.transformer.wte.weight, self, use_pad_mask)
@@ -254,6 +261,8 @@ class _GPT2Fn(torch.autograd.Function):
             dxf = ops.linear_dx(dl, wout)
         ctx.logits_pad = None
         dx = ops.layernorm_bwd(dxf, xL, tr.ln_f.weight.detach(), muf, rsf, G(tr.ln_f.weight), G(tr.ln_f.bias))
+        store = store_of(m)
+        notify_final(store, [tr.ln_f.weight, tr.ln_f.bias])
         dprefix = torch.empty(B, P * D, dtype=torch.float32, device=dev)
         for li in range(len(saved) - 1, -1, -1):
             blk = tr.h[li]
@@ -291,6 +300,7 @@ class _GPT2Fn(torch.autograd.Function):
             ops.colsum(dqkv, G(at.c_attn.bias))
             dx = ops.layernorm_bwd(dh1, x_in, blk.ln_1.weight.detach(), mu1, rs1, G(blk.ln_1.weight),
                                    G(blk.ln_1.bias), dres=dx1)
+            notify_final(store, blk.parameters())  # this block's gradients are complete
         # embeddings: wte already holds the LM-head gradient; wpe rows 10..10+T-1
         ops.zero_(G(tr.wpe.weight))
         ops.embedding_bwd(captions, dx, None, G(wte), G(tr.wpe.weight), P, drop=ctx.d_emb)
@@ -301,6 +311,7 @@ class _GPT2Fn(torch.autograd.Function):
             ops.cast(dprefix, dP)
         ops.linear_dw(dP, pooled, G(itp.weight))
         ops.colsum(dP, G(itp.bias))
+        notify_final(store, [wte, tr.wpe.weight, itp.weight, itp.bias])
         dpooled = ops.linear_dx(dP, W(itp.weight, dt))
         return dpooled, None, None, None, None
 

@@ -30,6 +30,7 @@ from .. import ops
 from .._lib import ACT_DERIV, ACT_GELU_ERF
 from .common import G, CapkModule, W, heads, linear_bwd, next_seed
 from ..ops import HeadView
+from ..params import notify_final, store_of
 
 
 def _pad64(v):
@@ -80,6 +81,12 @@ class TransformerDecoderCore(CapkModule):
         self.visual_projection = nn.Linear(hidden_dim, hidden_dim)
         self.output_layer.weight._capk_pad_rows = self.vocab_pad
         self.output_layer.bias._capk_pad_rows = self.vocab_pad
+
+    def _capk_store_first(self):
+        # the backward finishes the visual projection last (after the embeddings): in front of
+        # the embeddings in the flat buffers, so the LM head and every layer are a growing
+        # suffix that dp.GradBucketer exchanges while the rest of the backward runs
+        return [self.visual_projection.weight, self.visual_projection.bias]
 
     # -------------------------------------------------------------- forward
     def forward_logits(self, features, captions, use_pad_mask=True):
@@ -204,6 +211,8 @@ class _DecoderFn(torch.autograd.Function):
         if dhidden is not None:
             dx = dx + dhidden.reshape(BT, D)
         ctx.logits_pad = None
+        store = store_of(m)
+        notify_final(store, [ol.weight, ol.bias])  # (its bias gradient: here or by the CE backward)
         dmem = torch.empty(M_ext, D, dtype=dt, device=dev)
         first = True
         for li in range(len(saved_layers) - 1, -1, -1):
@@ -263,16 +272,19 @@ class _DecoderFn(torch.autograd.Function):
             ops.colsum(dqkv, G(sa.in_proj_bias))
             ops.linear_dx(dqkv, W(sa.in_proj_weight, dt), out=ds1, beta=1.0)  # dx = ds1 + dqkv Win
             dx = ds1
+            notify_final(store, L.parameters())  # this layer's gradients are complete
         # embeddings (scatter-add into zeroed grads; padding_idx rows skipped)
         ops.zero_(G(m.embedding.weight))
         ops.zero_(G(m.position_encoding.weight))
         ops.embedding_bwd(captions, dx, m.pad_token_id, G(m.embedding.weight), G(m.position_encoding.weight), 0,
                           drop=ctx.d_emb)
+        notify_final(store, [m.embedding.weight, m.position_encoding.weight])
         # visual projection
         vp = m.visual_projection
         # gap rows of dmem are exactly zero: every dkv gap row is zero (see above)
         ops.linear_dw(dmem, feat_mem, G(vp.weight))
         ops.colsum(dmem, G(vp.bias))
+        notify_final(store, [vp.weight, vp.bias])
         dfeat_mem = ops.linear_dx(dmem, W(vp.weight, dt))
         shape, stride = ctx.features_meta
         dfeatures = dfeat_mem.as_strided(shape, stride, 0)

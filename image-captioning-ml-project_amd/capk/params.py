@@ -93,6 +93,20 @@ class ParamStore:
                 if id(q) not in seen:
                     seen.add(id(q))
                     order.append(q)
+        # a module whose backward finishes some of its parameters LAST (the decoder's visual
+        # projection, after every layer) lists them in _capk_store_first(): they move to the
+        # front of the module's run, so its layers' gradients still grow as a suffix
+        for m in model.modules():
+            fn = getattr(m, "_capk_store_first", None)
+            if fn is None:
+                continue
+            first = [q for q in fn() if q is not None]
+            ids = {id(q) for q in first}
+            own = {id(q) for q in m.parameters()}
+            at = min(i for i, q in enumerate(order) if id(q) in own)
+            rest = [q for q in order if id(q) not in ids]
+            at = sum(1 for q in order[:at] if id(q) not in ids)
+            order = rest[:at] + first + rest[at:]
         for p in order:
             g = "no_decay" if no_decay(names[id(p)]) else "decay"
             self.groups[g].append(p)

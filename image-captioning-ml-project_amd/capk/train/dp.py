@@ -7,7 +7,8 @@ the flat fp32 gradient buffers of the ParamStore are averaged with bucketed
 of the flat buffers (no packing copies).
 
 ``GradBucketer`` overlaps that exchange with the backward.  Model code reports
-when gradients are final (``params.notify_final``: each encoder layer at the end
+when gradients are final (``params.notify_final``: the Transformer / GPT-2 decoder's LM
+head and each of its layers as the backward leaves them, each encoder layer at the end
 of its backward, the encoder head once the decoder and the head are done).  The
 flat buffers are laid out in registration order (params.py) and the backward
 finishes the modules in reverse order, so in every buffer the final gradients
@@ -78,8 +79,23 @@ class GradBucketer:
                       if exchange == "bf16" and self.active else None)
         # per group: [start, end) of every parameter, in buffer order
         self.spans = {}
+        # the buffer tail the store keeps for optional-gradient parameters (e.g. the ViT pooler
+        # when the decoder ignores pooled_features) and frozen ones: not part of the growing
+        # suffix -- an optional parameter is written (if at all) by the encoder head, late in the
+        # backward, and would hold back every decoder bucket in front of it -- but exchanged by
+        # finish() once the whole backward is done ([tail0, opt_end): the optional ones)
+        self.tail0, self.opt_end, self.ntail = {}, {}, {}
+        late = set(store.frozen) | set(store.optional)
         for g, plist in store.groups.items():
             self.spans[g] = sorted((p._capk_offset, p._capk_offset + _round(_alloc_numel(p)), id(p)) for p in plist)
+            tail = [sp for sp in self.spans[g] if sp[2] in late]
+            self.ntail[g] = len(tail)
+            n = store.grad[g].numel()
+            self.tail0[g] = tail[0][0] if tail else n
+            frozen = [sp for sp in self.spans[g] if sp[2] in store.frozen]
+            self.opt_end[g] = frozen[0][0] if frozen else n
+            assert all(sp[2] in late for sp in self.spans[g][len(self.spans[g]) - len(tail):]), \
+                "GradBucketer: optional / frozen parameters must sit at the buffer tail"
         if self.active:
             self.op, self.need_scale = _avg_op()
             self.world = dist.get_world_size()
@@ -87,11 +103,12 @@ class GradBucketer:
         self.reset()
 
     def reset(self):
-        self.final = set(self.store.frozen)  # frozen parameters never receive a gradient
+        # frozen parameters never receive a gradient; optional ones are exchanged by finish()
+        self.final = set(self.store.frozen) | set(self.store.optional)
         self.works = []
-        self.k = {g: 0 for g in self.spans}                       # spans known final, counted from the end
-        self.lo = {g: self.store.grad[g].numel() for g in self.spans}  # start of the final suffix
-        self.hi = dict(self.lo)                                    # [hi, end) already launched
+        self.k = dict(self.ntail)                                  # spans known final, counted from the end
+        self.lo = dict(self.tail0)                                 # start of the final suffix
+        self.hi = dict(self.lo)                                    # [hi, tail0) already launched
 
     def mark_final(self, ids):
         self.final.update(ids)
@@ -121,6 +138,8 @@ class GradBucketer:
             for g in self.spans:
                 if self.hi[g] > 0:
                     self._launch(g, 0, self.hi[g])
+                if self.opt_end[g] > self.tail0[g]:  # the optional tail, final now
+                    self._launch(g, self.tail0[g], self.opt_end[g])
             for work, chunk, wire in self.works:
                 work.wait()
                 if wire is not chunk:

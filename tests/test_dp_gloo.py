@@ -146,6 +146,88 @@ def test_dp_overlapped_buckets_equal_full_batch(tmp_path, golden_dir, exchange, 
     assert res["early"] > 0, res  # collectives were in flight before the last gradient was written
 
 
+def _backward_groups(m):
+    """The notify_final points of the real backward, in its order (capk/models/transformer.py
+    _DecoderFn.backward, vit.py _ViTLayerFn / _ViTHeadFn / _ViTEmbedFn): the decoder's LM head,
+    its layers last to first, its embeddings, its visual projection; then the encoder head
+    (every parameter but the encoder's embeddings and layers), the encoder layers last to first."""
+    dec, enc = m.decoder, m.encoder.model
+    groups = [("dec_head", [dec.output_layer.weight, dec.output_layer.bias])]
+    for i in reversed(range(len(dec.transformer_decoder.layers))):
+        groups.append((f"dec_layer{i}", list(dec.transformer_decoder.layers[i].parameters())))
+    groups.append(("dec_emb", [dec.embedding.weight, dec.position_encoding.weight]))
+    groups.append(("dec_vproj", [dec.visual_projection.weight, dec.visual_projection.bias]))
+    groups.append(("enc_head", None))  # all_except: the encoder's embeddings and layers
+    for i in reversed(range(len(enc.layers))):
+        groups.append((f"enc_layer{i}", list(enc.layers[i].parameters())))
+    groups.append(("enc_emb", list(enc.embeddings.parameters())))
+    return groups
+
+
+def _worker_decoder_buckets(rank, world, port, golden, out):
+    """GradBucketer with the model's own notification points: the decoder's buckets (LM head,
+    each layer) launch while the decoder backward still runs -- the visual projection, finished
+    last, sits in front of the decoder's run (params._capk_store_first) and the optional ViT
+    pooler at the buffer tail is exchanged by finish() -- and the result is the full-batch
+    gradient (NaN-poisoned buffers catch any premature launch)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    m, sd, dims = _tiny(golden)
+    from capk.params import attach, notify_final
+    from capk.train.dp import GradBucketer
+    store = attach(m, "cpu")
+    bucketer = GradBucketer(store, bucket_elems=1000)
+    D, Le, He, Ld, Hd, V, pad, patch, img = dims
+    g = torch.Generator().manual_seed(321)
+    images = torch.randn(4, 3, img, img, generator=g)
+    caps = torch.randint(0, V - 1, (4, 7), generator=g)
+    shard = slice(rank * 2, rank * 2 + 2)
+    named = dict(m.named_parameters())
+    name_of = {id(p): n for n, p in named.items()}
+    full = _oracle_grads(sd, dims, images, caps)
+    grads = _oracle_grads(sd, dims, images[shard], caps[shard])
+    for buf in store.grad.values():
+        buf.fill_(float("nan"))
+    launched = {}
+    enc_skip = list(m.encoder.model.embeddings.parameters()) + list(m.encoder.model.layers.parameters())
+    done = set()
+    for tag, params in _backward_groups(m):
+        if params is None:  # the encoder head: everything not written yet but the encoder body
+            skip = {id(p) for p in enc_skip}
+            params = [p for p in named.values() if id(p) not in skip and id(p) not in done]
+        with torch.no_grad():
+            for p in params:
+                p._capk_grad.copy_(grads[name_of[id(p)]])
+                done.add(id(p))
+        if tag == "enc_head":
+            notify_final(store, all_except=enc_skip)
+        else:
+            notify_final(store, params)
+        launched[tag] = len(bucketer.works)
+    bucketer.finish()
+    err = max(float((named[n]._capk_grad - full[n]).abs().max()) for n in full)
+    gmax = max(float(full[n].abs().max()) for n in full)
+    if rank == 0:
+        torch.save({"err": err, "gmax": gmax, "launched": launched}, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_decoder_layer_buckets_launch_early(tmp_path, golden_dir):
+    out = str(tmp_path / "dpd.pt")
+    golden = os.path.join(golden_dir, "vit_transformer_step.npz")
+    mp.spawn(_worker_decoder_buckets, args=(2, _free_port(), golden, out), nprocs=2, join=True)
+    res = torch.load(out, weights_only=True)
+    assert res["err"] < 1e-5 * max(1.0, res["gmax"]), res
+    L = res["launched"]
+    # decoder buckets in flight before the decoder backward is over (its embeddings and visual
+    # projection), and more launched while the encoder layers still run
+    assert L["dec_layer0"] > 0, L
+    assert L["dec_head"] <= L["dec_layer0"] <= L["enc_head"] <= L["enc_layer0"], L
+
+
 def test_dp_allreduce_equals_full_batch(tmp_path, golden_dir):
     out = str(tmp_path / "dp.pt")
     golden = os.path.join(golden_dir, "vit_transformer_step.npz")
