@@ -84,27 +84,18 @@ template <> struct SideSeg<float> {
   }
 };
 
-// 8 results of one row segment -> one (bf16) or two (fp32) 16-byte buffer stores; AUX = the
-// cache-policy bits (2: nt)
-template <int AUX = 0>
+// 8 results of one row segment -> one (bf16) or two (fp32) 16-byte buffer stores
 __device__ __forceinline__ void store8(__amdgpu_buffer_rsrc_t rs, uint32_t off, const float (&v)[8], bf16*) {
   bf16x8 o;
 #pragma unroll
   for (int i = 0; i < 8; ++i) o[i] = (bf16)v[i];
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, o), rs, off, 0, AUX);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, o), rs, off, 0, 0);
 }
-template <int AUX = 0>
 __device__ __forceinline__ void store8(__amdgpu_buffer_rsrc_t rs, uint32_t off, const float (&v)[8], float*) {
   const i32x4 a = {__float_as_int(v[0]), __float_as_int(v[1]), __float_as_int(v[2]), __float_as_int(v[3])};
   const i32x4 b = {__float_as_int(v[4]), __float_as_int(v[5]), __float_as_int(v[6]), __float_as_int(v[7])};
-  __builtin_amdgcn_raw_buffer_store_b128(a, rs, off, 0, AUX);
-  __builtin_amdgcn_raw_buffer_store_b128(b, rs, off + 16, 0, AUX);
-}
-// the output stores: nontemporal when the launch asks for it (Epi8q::nt, wave-uniform)
-template <typename T>
-__device__ __forceinline__ void store8o(__amdgpu_buffer_rsrc_t rs, uint32_t off, const float (&v)[8], T* tag, int nt) {
-  if (nt) store8<2>(rs, off, v, tag);
-  else store8<0>(rs, off, v, tag);
+  __builtin_amdgcn_raw_buffer_store_b128(a, rs, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(b, rs, off + 16, 0, 0);
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, int64_t bytes) {
@@ -137,7 +128,6 @@ struct Epi8q {
   int group;  // grouped raster: tiles of the whole-item rows in groups of `group` row blocks, column-major
               // inside a group (0: row-major); host: gemm8q_group()
   unsigned long long* trace;  // CAPK_DIAG_TRACE builds only: per-item timestamps
-  int nt;  // C / pre-activation stores nontemporal (CAPK_GEMM_NT_STORE=1, an A/B switch)
 };
 
 
@@ -449,11 +439,11 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
 #if defined(CAPK_DIAG_NOSTORE)  // diagnostic build: the stores issue but are dropped (range check)
       store8(rsC, OOR, v, (OutT*)nullptr);
 #else
-      store8o(rsC, (qn ? o1 : o0) + seg_add(e.ldc, ESZ, qm, i), v, (OutT*)nullptr, e.nt);
+      store8(rsC, (qn ? o1 : o0) + seg_add(e.ldc, ESZ, qm, i), v, (OutT*)nullptr);
 #endif
       if constexpr (ACT != 0) {
         const __amdgpu_buffer_rsrc_t rsPre = rsrc_of(e.pre, (int64_t)M * e.ldp * ESZ);
-        store8o(rsPre, (qn ? p1 : p0) + seg_add(e.ldp, ESZ, qm, i), pre, (OutT*)nullptr, e.nt);
+        store8(rsPre, (qn ? p1 : p0) + seg_add(e.ldp, ESZ, qm, i), pre, (OutT*)nullptr);
       }
     };
 #define CAPK_SEG(QN, I) \
@@ -843,8 +833,6 @@ int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int
   CAPK_CHECK_ARG(!fwd_act || (a_kmajor && b_kmajor), "capk_gemm(gemm8q): forward activations need K-major operands");
   // grouped raster over the whole-item rows (all rows, or [0, r0) with a tail round)
   p.group = gemm8q_group(p.tail_ws ? p.tail_r0 : cdiv(M, 256), cdiv(N, 256));
-  static const int nt_env = [] { const char* v = getenv("CAPK_GEMM_NT_STORE"); return v ? atoi(v) : 0; }();
-  p.nt = nt_env;
 #if defined(CAPK_DIAG_TRACE)
   p.trace = (unsigned long long*)diag_trace_buf();
   CAPK_CHECK_ARG(p.trace != nullptr, "capk_gemm(gemm8q, trace build): no trace buffer");
