@@ -93,6 +93,31 @@ def test_ring_configs_bf16(ops, cfg, M, N, K):
 
 
 @cuda
+@pytest.mark.parametrize("M,N,K", [(1280, 768, 768), (1280, 1536, 1536), (1280, 2304, 768), (1280, 3072, 768)])
+def test_s64_ring_depths(ops, M, N, K):
+    """The 64x64 decode tile (cfg 9) on one-round and multi-round grids (240 / 480 / 720 WGs: the
+    3-deep ring; 960: the 2-deep ring) with the bias + GELU + residual epilogue, vs the fp32 product
+    of the same bf16 values (the split-K slab route: test_product_ln_slabs_bit_identical)."""
+    from capk._lib import ACT_GELU_ERF
+    L = ops.lib()
+    g = torch.Generator(device="cuda").manual_seed(19)
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device="cuda", generator=g)
+    r = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    try:
+        ops.check(L.capk_gemm_force_config(9), "force_config")
+        y = ops.linear(x, w, b, residual=r, act=ACT_GELU_ERF, preact=pre)
+        assert L.capk_gemm_last_config() == 9
+    finally:
+        L.capk_gemm_force_config(-1)
+    ref_pre = x.float() @ w.float().t() + b
+    assert _rel(pre, ref_pre) < 1e-2
+    assert _rel(y, F.gelu(ref_pre) + r.float()) < 1e-2
+
+
+@cuda
 def test_gemm_bf16_splitk_and_beta(ops):
     """dW-shaped GEMM with a long reduction (split-K slabs + reduce) and accumulate."""
     g = torch.Generator(device="cuda").manual_seed(2)
