@@ -292,7 +292,7 @@ def test_transformer_beam5_config3_fp32_vs_oracle():
 
 
 def _config3_peaked(precision, seed=42, n_hot=64, gain=40.0, eos_hot=False, round_bf16=False, bias_step=0.0,
-                    cold_bias=0.0, bias_spread=0.0):
+                    cold_bias=0.0, bias_spread=0.0, bias_offset=0.0):
     """The config-3 model (test_gpu_model._full_model) with a peaked LM head: the output rows of
     n_hot tokens (fixed, seed-drawn; with eos_hot the EOS token is one of them) scaled by `gain`,
     so that, like a trained captioner's, the next-token distribution concentrates on a few tokens
@@ -307,7 +307,9 @@ def _config3_peaked(precision, seed=42, n_hot=64, gain=40.0, eos_hot=False, roun
     small, so the bf16 logits' rounding -- an ulp of 2^-8 |logit| -- stays small too).  bias_spread:
     the hot tokens' biases drawn uniformly from [0, bias_spread) (seeded; generic values, so sums
     along different hypotheses do not tie): a confident head whose candidate gaps are set mostly
-    by exact fp32 biases, the image-dependent logits (gain) deciding between close ones."""
+    by exact fp32 biases, the image-dependent logits (gain) deciding between close ones.
+    bias_offset: added to the hot tokens' biases (centring the hot logits near 0 keeps their bf16
+    rounding small: the logits are stored in bf16, an ulp of 2^-8 |logit|)."""
     import capk
     from capk import config as C
     from capk.models import captioning_model as cm
@@ -325,8 +327,9 @@ def _config3_peaked(precision, seed=42, n_hot=64, gain=40.0, eos_hot=False, roun
         model.decoder.output_layer.weight[hot] *= gain
         if bias_step:
             model.decoder.output_layer.bias[hot] += bias_step * torch.arange(n_hot, dtype=torch.float32)
-        if bias_spread:
-            model.decoder.output_layer.bias[hot] = torch.rand(n_hot, generator=torch.Generator().manual_seed(seed + 1)) * bias_spread
+        if bias_spread or bias_offset:
+            model.decoder.output_layer.bias[hot] = (torch.rand(n_hot, generator=torch.Generator().manual_seed(seed + 1))
+                                                    * bias_spread + bias_offset)
         if cold_bias:
             cold = torch.ones(cfg.model.vocab_size, dtype=torch.bool)
             cold[hot] = False
@@ -370,13 +373,16 @@ def _bf16_vs_fp32_margins(m32, m16, cfg, images, k=5, L=20):
         init[:, 0] = 0.0
         st = {"S32": init.clone(), "S16": init.clone(), "err": torch.zeros(B, device="cuda"),
               "stable": torch.ones(B, dtype=torch.bool, device="cuda"), "lp32": None, "lp16": None,
-              "steps": 0, "steps_ok": 0}
+              "steps": 0, "steps_ok": 0, "first_bad": torch.full((B,), 1 << 30, dtype=torch.long, device="cuda"),
+              "h": torch.full((B * k,), cfg.model.bos_token_id, dtype=torch.long, device="cuda"), "sets": []}
 
         def step(cur_len, ids, reorder):
             if reorder is not None:  # running scores of the new rows: parent's score + chosen token's log-prob
                 par = reorder.long()
                 for p in ("32", "16"):
                     st["S" + p] = (st["S" + p].view(-1)[par] + st["lp" + p][par, ids]).view(B, k)
+                st["h"] = _hyp_hash(st["h"], par, ids)
+            st["sets"].append(st["h"].view(B, k).sort(1).values)
             lg32 = r32.step(cur_len, ids, reorder)
             lg16 = r16.step(cur_len, ids, reorder)
             st["lp32"] = torch.log_softmax(lg32[:, :V].float(), -1)
@@ -409,6 +415,7 @@ def _bf16_vs_fp32_margins(m32, m16, cfg, images, k=5, L=20):
             last = cur_len + 1 >= L
             step_ok = (ok | ~need).all(2).all(1) | last
             st["stable"] &= step_ok
+            st["first_bad"] = torch.where(~step_ok & (st["first_bad"] > st["steps"]), st["steps"], st["first_bad"])
             st["steps"] += 1
             st["steps_ok"] += int(step_ok.sum())
             return lg32
@@ -424,22 +431,43 @@ def _bf16_vs_fp32_margins(m32, m16, cfg, images, k=5, L=20):
     stable = st["stable"] & ((sc[:, 0] - sc[:, 1]) > 2 * st["err"] / min_len)
     same = (_padded(out["sequences"], L, pad) == _padded(ids16, L, pad)).all(1)
     _bf16_vs_fp32_margins.step_cov = st["steps_ok"] / max(1, st["steps"] * B)
+    # the fp32 search's running set at every step (sorted hypothesis hashes, [B, k] per step) and, per
+    # image, the first step not decided by margins: every running set up to and including the one
+    # after that step's predecessor is the bf16 search's too (same induction, one image at a time)
+    _bf16_vs_fp32_margins.sets = st["sets"]
+    _bf16_vs_fp32_margins.first_bad = st["first_bad"].clamp_max(st["steps"])
     return same, stable, ids16, st["err"]
+
+
+def _hyp_hash(h, par, ids):
+    """Running-set bookkeeping of a beam search: each row's hypothesis (token sequence) as a 64-bit
+    polynomial hash, extended by the row's parent (global row index) and chosen token."""
+    return h[par] * 1000003 + ids.long()
 
 
 # peaked-head settings of the bf16-vs-fp32 beam test and the stable coverage each must reach
 # (tools/beam_margin_probe.py measured them on the GPU: profiles/round5/beam_margin_probe_7.txt).
 # A narrow head decides most images by wide margins but every image then takes the same caption;
 # a wider one gives 13 distinct captions over the batch with fewer images decided by margins.
+# A diverse head (16 hot tokens, biases centred on 0; profiles/round6/beam_margin_probe_r6.txt)
+# gives 76 distinct captions over the 256 images: no image is decided by margins at all of its 19
+# steps, but every image is checked step by step up to its first near-tie (the running sets must
+# be the fp32 search's until then: 0.254 of the 256 x 19 running sets verified), and at least
+# `min_same` of the images must still return the fp32 caption (measured 0.867).  min_verified:
+# the fraction of (image, step) running sets so verified (measured 0.694 / 0.494 / 0.254).
 BEAM_PEAKS = [
-    (dict(n_hot=6, gain=2.0, eos_hot=False, round_bf16=True, cold_bias=-20.0, bias_spread=8.0), 0.40),
-    (dict(n_hot=8, gain=2.5, eos_hot=False, round_bf16=True, cold_bias=-20.0, bias_spread=8.0), 0.04),
+    (dict(n_hot=6, gain=2.0, eos_hot=False, round_bf16=True, cold_bias=-20.0, bias_spread=8.0),
+     dict(min_stable=0.40, min_verified=0.60)),
+    (dict(n_hot=8, gain=2.5, eos_hot=False, round_bf16=True, cold_bias=-20.0, bias_spread=8.0),
+     dict(min_stable=0.04, min_verified=0.40)),
+    (dict(n_hot=16, gain=4.0, eos_hot=False, round_bf16=True, cold_bias=-20.0, bias_spread=4.0, bias_offset=-2.0),
+     dict(min_stable=0.0, min_verified=0.20, min_same=0.75, min_distinct=50)),
 ]
 
 
 @cuda
-@pytest.mark.parametrize("peak,min_stable", BEAM_PEAKS, ids=["narrow", "wide"])
-def test_transformer_beam5_config3_bf16_vs_fp32(peak, min_stable):
+@pytest.mark.parametrize("peak,expect", BEAM_PEAKS, ids=["narrow", "wide", "diverse"])
+def test_transformer_beam5_config3_bf16_vs_fp32(peak, expect):
     """The benchmarked path end to end: config-3 model (ViT-B/16 + 6L/8H decoder, V = 50 257),
     256 images, bf16 beam-5 through ``generate`` (graph-replayed KV-cached decode).
 
@@ -453,7 +481,10 @@ def test_transformer_beam5_config3_bf16_vs_fp32(peak, min_stable):
        bit-exactly to the CPU reference by test_transformer_beam5_config3_fp32_vs_oracle), every
        image whose search is decided by margins larger than the bf16 error at every step
        (_bf16_vs_fp32_margins) must return the identical best sequence, and such images must be
-       at least ``min_stable`` of the batch.  Weights: random init with a peaked LM head
+       at least ``min_stable`` of the batch.  Step by step: every image's bf16 running set (the k
+       kept hypotheses) equals the fp32 one at every step up to the first one not decided by
+       margins (and at every step for a stable image).  With ``min_same``/``min_distinct``: at
+       least that fraction of identical best sequences, and that many distinct captions.  Weights: random init with a peaked LM head
        (_config3_peaked with ``peak``: the next-token distribution concentrates on a few
        well-separated tokens, like a trained captioner's)."""
     from capk.beam import beam_search
@@ -469,7 +500,8 @@ def test_transformer_beam5_config3_bf16_vs_fp32(peak, min_stable):
         ids16, info16 = m16.generate(images=images, max_length=L, num_beams=k)
         # 1. an eager device search over the same bf16 decode steps, every selection checked
         r16 = KVDecodeRunner(m16.decoder, f16, k, L)
-        st1 = {"S": None, "c": None, "ok": torch.ones(B, dtype=torch.bool, device="cuda"), "n": 0}
+        st1 = {"S": None, "c": None, "ok": torch.ones(B, dtype=torch.bool, device="cuda"), "n": 0,
+               "h": torch.full((B * k,), cfg.model.bos_token_id, dtype=torch.long, device="cuda"), "sets": []}
         slot_img = torch.arange(B * k, device="cuda") // k
 
         def step16(cur_len, ids, reorder):
@@ -477,6 +509,7 @@ def test_transformer_beam5_config3_bf16_vs_fp32(peak, min_stable):
                 S = torch.full((B, k), -1e9, device="cuda")
                 S[:, 0] = 0.0
             else:  # the rows the device kept: their scores must be the k best non-EOS candidates
+                st1["h"] = _hyp_hash(st1["h"], reorder.long(), ids)
                 par = reorder.long() - slot_img * k
                 S = st1["c"][slot_img, par * V + ids].view(B, k)
                 masked = st1["c"].view(B, k, V).clone()
@@ -484,6 +517,7 @@ def test_transformer_beam5_config3_bf16_vs_fp32(peak, min_stable):
                 best = masked.view(B, k * V).topk(k, -1).values
                 st1["ok"] &= (S.sort(1, descending=True).values - best).abs().amax(1) <= 1e-4
                 st1["n"] += 1
+            st1["sets"].append(st1["h"].view(B, k).sort(1).values)
             lg = r16.step(cur_len, ids, reorder)
             lp = torch.log_softmax(lg[:, :V].float(), -1)
             st1["c"] = (S[:, :, None] + lp.view(B, k, V)).view(B, k * V)
@@ -495,9 +529,24 @@ def test_transformer_beam5_config3_bf16_vs_fp32(peak, min_stable):
     # 2. bf16 vs fp32 along the fp32 path
     same, stable, _, err = _bf16_vs_fp32_margins(m32, m16, cfg, images, k, L)
     cov = float(stable.float().mean())
+    # running sets step by step: the first step where the bf16 search's set differs from the fp32
+    # one must come after the first step not decided by margins
+    sets32, first_bad = _bf16_vs_fp32_margins.sets, _bf16_vs_fp32_margins.first_bad
+    n = min(len(sets32), len(st1["sets"]))
+    differ = torch.stack([(a != b).any(1) for a, b in zip(sets32[:n], st1["sets"][:n])], 1)  # [B, n]
+    first_diff = torch.where(differ.any(1), differ.int().argmax(1), torch.full_like(first_bad, n))
+    verified = torch.minimum(first_bad + 1, torch.full_like(first_bad, n))
+    distinct = len(set(map(tuple, ids16.tolist())))
     print(f"bf16 beam-5 at config-3 size: {st1['n']} selections x {B} images checked; vs fp32: identical best "
           f"sequence {float(same.float().mean()):.3f}, stable {int(stable.sum())}/{B} = {cov:.3f} "
-          f"(identical {int((same & stable).sum())}), median max candidate error {float(err.median()):.4f}, "
-          f"distinct captions {len(set(map(tuple, ids16.tolist())))} (stable {len(set(map(tuple, ids16[stable].tolist())))})")
+          f"(identical {int((same & stable).sum())}), running sets verified by margins "
+          f"{float(verified.sum()) / (B * n):.3f} of {B} x {n} (identical {float((~differ).float().mean()):.3f}), "
+          f"median max candidate error {float(err.median()):.4f}, "
+          f"distinct captions {distinct} (stable {len(set(map(tuple, ids16[stable].tolist())))})")
     assert bool(same[stable].all()), torch.nonzero(stable & ~same).flatten().tolist()
-    assert cov >= min_stable, cov
+    bad = differ.any(1) & (first_diff <= first_bad)
+    assert not bool(bad.any()), [(i, int(first_diff[i]), int(first_bad[i])) for i in torch.nonzero(bad).flatten().tolist()]
+    assert cov >= expect["min_stable"], cov
+    assert float(verified.sum()) / (B * n) >= expect["min_verified"]
+    assert float(same.float().mean()) >= expect.get("min_same", 0.0)
+    assert distinct >= expect.get("min_distinct", 1), distinct

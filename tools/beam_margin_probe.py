@@ -1,6 +1,7 @@
 """Stable coverage of the bf16-vs-fp32 beam-5 precision check (tests/test_gpu_beam.py
 _bf16_vs_fp32_margins) for several peaked-LM-head settings of the config-3 model, 256 images.
-PROBE_SETTINGS="n_hot:gain:eos_hot:round_bf16:bias_step:cold_bias:bias_spread;..." overrides the list."""
+PROBE_SETTINGS="n_hot:gain:eos_hot:round_bf16:bias_step:cold_bias:bias_spread[:bias_offset];..." overrides
+the list."""
 import os
 import sys
 
@@ -18,9 +19,11 @@ def main():
     B = int(os.environ.get("PROBE_B", "256"))
     images = torch.randn(B, 3, 224, 224, generator=torch.Generator().manual_seed(3)).cuda()
     for item in os.environ.get("PROBE_SETTINGS", DEFAULT).split(";"):
-        n_hot, gain, eos_hot, rb, bstep, cold, spread = item.split(":")
+        f = item.split(":")
+        n_hot, gain, eos_hot, rb, bstep, cold, spread = f[:7]
         kw = dict(n_hot=int(n_hot), gain=float(gain), eos_hot=eos_hot == "1", round_bf16=rb == "1",
-                  bias_step=float(bstep), cold_bias=float(cold), bias_spread=float(spread))
+                  bias_step=float(bstep), cold_bias=float(cold), bias_spread=float(spread),
+                  bias_offset=float(f[7]) if len(f) > 7 else 0.0)
         m32, cfg = tb._config3_peaked("fp32", **kw)
         m16, _ = tb._config3_peaked("bf16", **kw)
         same, stable, ids16, err = tb._bf16_vs_fp32_margins(m32, m16, cfg, images)
