@@ -34,10 +34,15 @@
 //    row blocks [0, r0) run as whole items (r0 * ntn <= 256 * rounds), and the remaining
 //    row blocks run as S K-splits per tile in one extra round (T * S <= 256 parts), each
 //    part writing its fp32 accumulators to its own slab; the host then launches the split-K
-//    reduce + epilogue over those rows (gemm.hip: splitk_reduce_kernel).  No cross-WG
-//    hand-off: the kernel boundary orders the slabs (the round-4 alternative that handed
-//    accumulators between WGs through an sc1 workspace paid more for the payload round trip
-//    than it saved, profiles/round4/ab_round4.md).  Contiguous-range stream-K was measured
+//    reduce + epilogue over those rows (tail mode 1, default; gemm.hip: splitk_reduce_kernel).
+//    Tail mode 2 (round 6, opt-in) combines inside the launch instead: each part draws an
+//    arrival ticket for its tile (slab stores drained, one agent-scope release); the part
+//    drawing the last one takes one agent-scope acquire, sums the tile's slabs in split order
+//    and runs the item's register epilogue -- bit-identical to mode 1, but measured 30-33 us
+//    SLOWER per ViT product (profiles/round6/gemm_tail_combine_ab.txt): one WG per tail tile
+//    reads its 3 x 256 KiB of slabs at ~30 GB/s, where the reduce launch spreads the same
+//    bytes over the whole chip (round 4's pairwise hand-off through an sc1 workspace lost
+//    the same way, profiles/round4/ab_round4.md).  Contiguous-range stream-K was measured
 //    slower (profiles/round4/streamk_contiguous_ab.txt: concurrent WGs no longer shared A
 //    row blocks in L2).
 //
@@ -47,6 +52,8 @@
 // result.  alpha != 1, dropout and split-K run on gemm8p.
 #include <atomic>
 #include <ctime>
+#include <map>
+#include <mutex>
 #include <type_traits>
 
 #include "gemm_common.h"
@@ -57,6 +64,7 @@ namespace {
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) unsigned long long gu64;  // hand-off flag words: global, never flat
+typedef __attribute__((address_space(1))) unsigned gu32;
 
 // One segment of the side operand (8 elements of one row) loaded by an asm buffer load that
 // hipcc does not count; the epilogue waits for all of them with one vmcnt(0) statement that
@@ -123,6 +131,8 @@ struct Epi8q {
   float* dsum;  // DSUM kernels: column-sum partials [2 * tile rows][N]
   float* tail_ws;  // TAIL kernels: fp32 slabs [splits][M - 256 tail_r0][N] of the tail row blocks
   int tail_r0, tail_splits;
+  int* tail_cnt;   // TAIL kernels, in-launch combine: one arrival ticket per tail tile (zero on entry,
+                   // zeroed again by the tile's last arriver); nullptr: the host launches the reduce
   float* lse_part;  // LSEP kernels: softmax partials [ntn * 4][M] of (max, sum exp) pairs (float2)
   int lse_v;        // LSEP: columns >= lse_v are padding (excluded from the partials)
   int group;  // grouped raster: tiles of the whole-item rows in groups of `group` row blocks, column-major
@@ -149,7 +159,7 @@ __device__ __forceinline__ void wait_le(int n) {
 // output gradient this dX is): per (tile row, wm) partial rows [2 ntm][N] into e.dsum,
 // summed in a fixed order by colsum_finish (capk_gemm_dx_act_colsum).
 template <bool AK, bool BK, typename OutT, int ACT, bool DV, int SK, bool DSUM = false, bool TAIL = false,
-          bool LSEP = false>
+          bool LSEP = false, bool TCOMB = false>
 __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A, int64_t lda,
                                                      const void* __restrict__ B, int64_t ldb, int M, int N, int K,
                                                      int splits, Epi8q e) {
@@ -691,6 +701,84 @@ __global__ __launch_bounds__(512) void gemm8q_kernel(const void* __restrict__ A,
     }
   }
   if (!lag) bar();  // realign the two groups (every barrier is matched)
+  if constexpr (TAIL && TCOMB) {
+    // ---- in-launch split-K combine of the tail tile (e.tail_cnt): every part has stored its
+    // slab (tail_store); the part drawing the tile's last ticket sums the slabs in split order
+    // (0 + s0 + s1 + ..., splitk_reduce_kernel's order: the same bits) and runs the item's
+    // register epilogue.  Publish: every wave drains its slab stores, the barrier, then ONE
+    // agent-scope release before the ticket; the reducer takes ONE agent-scope acquire before
+    // its plain slab loads (correct for any placement of a tile's parts over the XCDs).
+    if (hasTail && e.tail_cnt != nullptr) {
+      int* const last_flag = (int*)(smem + BIAS0 + 2 * 8 * 256);  // the 16 spare bytes of smem
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        gu32* const cnt = (gu32*)(e.tail_cnt + ttile);  // a global (never flat) agent-scope word
+        const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == (unsigned)(TS - 1);
+        if (last) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        *last_flag = last;
+      }
+      __syncthreads();
+      if (*last_flag == 0) return;
+      // the slabs, summed segment by segment in tail_store's (swapped) layout into acc, then
+      // swapped back (the swap is an involution) for the epilogue
+      const int64_t Mt = (int64_t)M - (int64_t)e.tail_r0 * 256;
+      zero_acc();
+      // one quadrant row at a time (16 segments of 2 loads in flight, no spills)
+      auto combine = [&](auto qmc) {
+        constexpr int qm = decltype(qmc)::value;
+        uint32_t off[2][4];
+#pragma unroll
+        for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int64_t row = (int64_t)cur.m0 - (int64_t)e.tail_r0 * 256 + qm * 128 + i * 16 + lrow;
+            const int n = cur.n0 + qn * 128 + lcol;
+            off[qn][i] = row < Mt && n < N ? (uint32_t)((row * N + n) * 4) : OOR;
+          }
+        for (int s = 0; s < TS; ++s) {
+          const __amdgpu_buffer_rsrc_t rsW = rsrc_of(e.tail_ws + (size_t)s * Mt * N, Mt * N * 4);
+#pragma unroll
+          for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const i32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rsW, off[qn][i], 0, 0);
+              const i32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rsW, off[qn][i] + 16, 0, 0);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                acc[qm][qn][i][0][r] += __int_as_float(a[r]);
+                acc[qm][qn][i][1][r] += __int_as_float(b[r]);
+              }
+            }
+        }
+      };
+      combine(std::integral_constant<int, 0>{});
+      combine(std::integral_constant<int, 1>{});
+#pragma unroll
+      for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+        for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[qm][qn][i][0][r]),
+                                                               __float_as_uint(acc[qm][qn][i][1][r]), false, false);
+              acc[qm][qn][i][0][r] = __uint_as_float(sw[0]);
+              acc[qm][qn][i][1][r] = __uint_as_float(sw[1]);
+            }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      fence();
+      epilogue(cur, nseg - 1);
+    }
+  }
 #if defined(CAPK_DIAG_TRACE)
   if ((wave & 3) == 0 && e.trace) {  // this wave's stamps -> e.trace [blockIdx][group][item][4]
     unsigned long long* dst = e.trace + ((size_t)blockIdx.x * 2 + (wave >> 2)) * TR_ITEMS * 4;
@@ -731,12 +819,15 @@ static void* diag_trace_buf() {
 // 1536 (24 K-tiles), S >= 2, each split >= 8 K-tiles.  capk_gemm_set_tail / CAPK_GEMM_TAIL=0
 // turn it off (A/B).
 static int g_tail_mode = -1;
-bool gemm8q_tail_plan(int M, int N, int K, int* r0, int* splits) {
+static int tail_mode() {
   static const int env_mode = [] {
     const char* v = getenv("CAPK_GEMM_TAIL");
     return v ? atoi(v) : 1;
   }();
-  const int mode = g_tail_mode >= 0 ? g_tail_mode : env_mode;
+  return g_tail_mode >= 0 ? g_tail_mode : env_mode;
+}
+bool gemm8q_tail_plan(int M, int N, int K, int* r0, int* splits) {
+  const int mode = tail_mode();
   const int ntm = cdiv(M, 256), ntn = cdiv(N, 256), items = ntm * ntn, nk = cdiv(K, 64);
   const int rounds = items >> 8;
   if (mode == 0 || rounds < 1 || (items & 255) == 0 || nk < 24) return false;
@@ -748,6 +839,44 @@ bool gemm8q_tail_plan(int M, int N, int K, int* r0, int* splits) {
   *splits = S;
   return true;
 }
+// Arrival tickets of the in-launch tail combine: a pool of zeroed 256-int blocks per device,
+// allocated on the first tail launch outside a stream capture; each (device, stream) takes its
+// own block on first use (no allocation then, so a stream being captured can take one too).
+// Every launch leaves its tickets at zero (the last arriver of each tile resets its own), so
+// launches on one stream -- graph replays included -- reuse the block, and concurrent streams
+// never share one.  No block (first use inside a capture, pool exhausted): the launch reduces
+// with the separate kernel instead.
+static int* tail_tickets(hipStream_t st) {
+  constexpr int kBlocks = 64, kInts = 256;
+  static std::mutex mu;
+  static std::map<int, int*> pools;
+  static std::map<std::pair<int, hipStream_t>, int*> taken;
+  static std::map<int, int> used;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  const auto key = std::make_pair(dev, st);
+  auto it = taken.find(key);
+  if (it != taken.end()) return it->second;
+  auto pit = pools.find(dev);
+  if (pit == pools.end()) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    int* p = nullptr;
+    if (hipMalloc(&p, (size_t)kBlocks * kInts * sizeof(int)) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, (size_t)kBlocks * kInts * sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+      (void)hipFree(p);
+      return nullptr;
+    }
+    pit = pools.emplace(dev, p).first;
+  }
+  int& n = used[dev];
+  if (n >= kBlocks) return nullptr;
+  int* b = pit->second + (size_t)(n++) * kInts;
+  taken[key] = b;
+  return b;
+}
+
 size_t gemm8q_tail_workspace(int M, int N, int K) {
   int r0, S;
   if (!gemm8q_tail_plan(M, N, K, &r0, &S)) return 0;
@@ -826,7 +955,9 @@ int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int
       p.tail_ws = (float*)ws;
       p.tail_r0 = r0;
       p.tail_splits = S;
-      *tail_r0 = r0;
+      // mode 2: the parts combine in the launch (tickets), else the caller's reduce launch
+      p.tail_cnt = tail_mode() == 2 ? tail_tickets(st) : nullptr;
+      *tail_r0 = p.tail_cnt ? -1 : r0;
       *tail_splits = S;
     }
   }
@@ -842,7 +973,10 @@ int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int
 #define L8(AK, BKM, OT, ACTK, DVK, SKK, DS)                                                                        \
   do {                                                                                                          \
     constexpr bool TAILV = !DS;                                                                                 \
-    if (TAILV && p.tail_ws)                                                                                     \
+    if (TAILV && p.tail_ws && p.tail_cnt)                                                                       \
+      hipLaunchKernelGGL((gemm8q_kernel<AK, BKM, OT, ACTK, DVK, SKK, DS, TAILV, false, true>), grid, block, 0, st, \
+                         A, lda, B, ldb, M, N, K, 1, p);                                                        \
+    else if (TAILV && p.tail_ws)                                                                                \
       hipLaunchKernelGGL((gemm8q_kernel<AK, BKM, OT, ACTK, DVK, SKK, DS, TAILV>), grid, block, 0, st, A, lda, B, \
                          ldb, M, N, K, 1, p);                                                                   \
     else                                                                                                        \
@@ -918,7 +1052,7 @@ extern "C" int capk_gemm_set_group(int rows) {
 }
 
 extern "C" int capk_gemm_set_tail(int mode) {
-  CAPK_CHECK_ARG(mode >= -1 && mode <= 1, "capk_gemm_set_tail: mode must be -1 (environment), 0 or 1");
+  CAPK_CHECK_ARG(mode >= -1 && mode <= 2, "capk_gemm_set_tail: mode must be -1 (environment), 0, 1 or 2");
   capk::g_tail_mode = mode;
   return CAPK_OK;
 }

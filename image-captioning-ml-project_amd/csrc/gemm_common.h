@@ -346,9 +346,10 @@ int launch_colsum_finish(int parts, int N, const float* part, float* out, int ac
 // the stored C over columns < lse_v, [cdiv(N, 256) * 4][M] (max, sum exp) pairs in the log2
 // domain (capk_linear_lse)
 // tail_r0 != nullptr and ws of gemm8q_tail_workspace() bytes: the split-K tail round when
-// gemm8q_tail_plan() picks one -- then *tail_r0 >= 0 and the caller must reduce the fp32
-// slabs ws[*tail_splits][M - 256 *tail_r0][N] into rows [256 *tail_r0, M) with the epilogue
-// (splitk_reduce_kernel); otherwise *tail_r0 = -1 and the launch wrote every row
+// gemm8q_tail_plan() picks one -- then, unless the launch combines the slabs itself (tail mode
+// 2), *tail_r0 >= 0 and the caller must reduce the fp32 slabs ws[*tail_splits][M - 256
+// *tail_r0][N] into rows [256 *tail_r0, M) with the epilogue (splitk_reduce_kernel);
+// otherwise *tail_r0 = -1 and the launch wrote every row
 int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int64_t lda, const void* B, int64_t ldb,
                   int M, int N, int K, int splits, const Epi& e, float* slab, hipStream_t st, float* dsum = nullptr,
                   void* ws = nullptr, size_t ws_bytes = 0, int* tail_r0 = nullptr, int* tail_splits = nullptr,

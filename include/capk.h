@@ -84,8 +84,10 @@ int capk_gemm_last_config(void);
 int capk_gemm_force_config(int cfg);
 /* Split-K tail round of the persistent 256x256 kernel (grids of more than 256 items with a
  * partial last round and K >= 1536: the row blocks past the whole rounds run as 2+ K-splits
- * per tile into fp32 slabs in capk_gemm's workspace, then one reduce + epilogue launch):
- * 1 on (default), 0 off, -1 back to CAPK_GEMM_TAIL. */
+ * per tile into fp32 slabs in capk_gemm's workspace): 1 (default) one reduce + epilogue
+ * launch after the GEMM, 2 the split arriving last at a tail tile sums the slabs in split
+ * order and runs the epilogue inside the launch (arrival tickets per stream; bit-identical
+ * to 1, measured slower), 0 off, -1 back to CAPK_GEMM_TAIL. */
 int capk_gemm_set_tail(int mode);
 /* Tile raster of the persistent 256x256 kernel: tiles in groups of `rows` row blocks,
  * column-major inside a group, so the 32 tiles an XCD runs at a time share fewer operand

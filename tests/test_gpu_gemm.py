@@ -184,12 +184,13 @@ def test_dx_act_colsum_fused(M):
 
 
 @cuda
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
 def test_tail_round_exact(mode, ak, bk):
     """The persistent kernel's split-K tail round (capk_gemm_set_tail(1): after the whole
     round, the remaining row blocks run as K-splits into fp32 slabs, reduced with the epilogue by
-    one more launch) vs whole items (0): a 273-item grid (21 x 13 tiles: 19 row blocks of whole
+    one more launch; 2: the split that arrives last at a tile sums the slabs and runs the
+    epilogue inside the launch) vs whole items (0): a 273-item grid (21 x 13 tiles: 19 row blocks of whole
     items, 26 tail tiles x 3 splits) with K = 1536 (24 K-tiles, splits of 8), exact
     small-integer operands (every partial sum exact in fp32, so the slabs must reproduce the
     product bit for bit), plain / bias + residual / beta * C / GELU + act' / backward * aux
@@ -245,7 +246,56 @@ def test_tail_round_exact(mode, ak, bk):
 
 
 @cuda
-@pytest.mark.parametrize("tail", [0, 1])
+@pytest.mark.parametrize("out_f32", [False, True])
+def test_tail_combine_matches_reduce(out_f32):
+    """The in-launch tail combine (capk_gemm_set_tail(2): arrival tickets, the last split of a
+    tail tile sums the slabs in split order and runs the register epilogue) against the reduce
+    launch (1) on random operands: the same fp32 additions in the same order, so the outputs are
+    bit-identical -- plain, bias + residual (bf16) / plain, bias (fp32 outputs), all four operand
+    layouts, a 50 432 x 768 x 3072 ViT product (27 tail row blocks x 3 splits) and a 21 x 13-tile
+    grid; repeated launches and a second stream (its own ticket block) included."""
+    from capk import _lib, ops
+    L = _lib.load()
+    L.capk_gemm_force_config(6)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(5)
+        side = torch.cuda.Stream()
+        for (M, N, K) in [(50432, 768, 3072), (20 * 256 + 72, 13 * 256, 1536)]:
+            a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+            w = (torch.randn(N, K, device="cuda", generator=g) * 0.05).bfloat16()
+            bias = torch.randn(N, device="cuda", generator=g)
+            res = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+            layouts = [(True, True), (True, False), (False, True), (False, False)] if M < 50000 else [(True, True), (True, False)]
+            for ak, bk in layouts:
+                A = a if ak else a.t().contiguous()
+                B = w if bk else w.t().contiguous()
+                dt = torch.float32 if out_f32 else torch.bfloat16
+                kw = dict(lda=A.stride(0), ldb=B.stride(0), ldc=N)
+                epis = [dict(), dict(bias=bias)] if out_f32 else [dict(), dict(bias=bias, residual=res, ldr=N)]
+                for epi in epis:
+                    outs = {}
+                    for mode in (1, 2, 2):
+                        L.capk_gemm_set_tail(mode)
+                        C = torch.full((M, N), float("nan"), device="cuda", dtype=dt)
+                        ops.gemm(A, ak, B, bk, M, N, K, C, **kw, **epi)
+                        assert L.capk_gemm_last_config() == 6
+                        outs.setdefault(mode, []).append(C)
+                    side.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(side):
+                        C = torch.full((M, N), float("nan"), device="cuda", dtype=dt)
+                        ops.gemm(A, ak, B, bk, M, N, K, C, **kw, **epi)
+                    torch.cuda.current_stream().wait_stream(side)
+                    outs[2].append(C)
+                    for C in outs[2]:
+                        assert torch.equal(C, outs[1][0]), (M, ak, bk, sorted(epi))
+        torch.cuda.synchronize()
+    finally:
+        L.capk_gemm_set_tail(-1)
+        L.capk_gemm_force_config(-1)
+
+
+@cuda
+@pytest.mark.parametrize("tail", [0, 1, 2])
 @pytest.mark.parametrize("group", [0, 2, 8, -1])
 def test_grouped_raster_exact(group, tail):
     """The persistent kernel's grouped raster (capk_gemm_set_group: tiles of the whole-item rows
