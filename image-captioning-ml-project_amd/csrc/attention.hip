@@ -830,35 +830,71 @@ __global__ __launch_bounds__(1024) void attn_bwd_fused64(AttnArgs a) {
 #pragma unroll
   for (int db = 0; db < 4; ++db) dvt[db] = dkt[db] = (f32x4){0.f, 0.f, 0.f, 0.f};
   f32x4 qsum = {0.f, 0.f, 0.f, 0.f};  // BIAS: this lane's query column of the stored dQ, over the chunks
+  // the key waves' LDS element offsets at chunk 0: the swizzle reads row bits 1-2 only, which a
+  // chunk's 32 rows and a 16-row half leave alone, so chunk t is + t * 2048 and the upper half
+  // + 1024 (swz_off / tr_read8_sw values, without their per-read address arithmetic)
+  int fo[2], tro[4];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) fo[s] = swz_off(i16, s * 32 + 8 * g);
+#pragma unroll
+  for (int db = 0; db < 4; ++db) tro[db] = swz_off(4 * g + (i16 >> 2), db * 16 + 4 * (i16 & 3));
+  auto tr8 = [](const bf16* p) -> bf16x8 {  // tr_read8_sw at a precomputed offset (both halves)
+    const bf16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, p));
+    const bf16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, p + 1024));
+    bf16x8 r;
+    r[0] = x0[0]; r[1] = x0[1]; r[2] = x0[2]; r[3] = x0[3];
+    r[4] = x1[0]; r[5] = x1[1]; r[6] = x1[2]; r[7] = x1[3];
+    return r;
+  };
   for (int t = 0; t < NQP / 32; ++t) {
     bf16* dsi = dST + (t & 1) * DSB;
     if (kw) {
-      f32x4 p[2], ds[2];
+      const bf16* Qt = Qs + t * 2048;
+      const bf16* dOt = dOs + t * 2048;
+      f32x4 p[2], ds[2], s_acc[2], dp_acc[2], l4[2], d4[2];
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        const int qa = t * 32 + c * 16 + i16;
-        f32x4 s_acc = {0.f, 0.f, 0.f, 0.f}, dp_acc = {0.f, 0.f, 0.f, 0.f};
+        s_acc[c] = dp_acc[c] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          const int qo = swz_off(qa, s * 32 + 8 * g);
-          s_acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(Qs + qo), kf[s], s_acc, 0, 0, 0);
-          dp_acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(dOs + qo), vf[s], dp_acc, 0, 0, 0);
+          s_acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(Qt + c * 1024 + fo[s]), kf[s], s_acc[c], 0, 0, 0);
+          dp_acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(dOt + c * 1024 + fo[s]), vf[s], dp_acc[c], 0, 0, 0);
         }
+        // lse / delta of the lane's 4 queries (one 16-B read each)
+        l4[c] = *(const f32x4*)(lse_s + t * 32 + c * 16 + 4 * g);
+        d4[c] = *(const f32x4*)(del_s + t * 32 + c * 16 + 4 * g);
+      }
+      // P and dS without branches: exp2 of every entry, masked entries selected to 0 afterwards
+      // (the same values); a chunk of 32 real queries against a full key block (no dropout)
+      // takes the form without any mask
+      if (!dropm<MODE>() && t * 32 + 32 <= a.Nq && fullk<MODE>(a, kb)) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int q = t * 32 + c * 16 + g * 4 + r;
-          const bool ok = q < a.Nq && (fullk<MODE>(a, kb) || kok<MODE>(a, b, keyl, q));
-          const float pv = ok ? fexp2(s_acc[r] * sl2 - lse_s[q]) : 0.f;
-          const float mk = dropm<MODE>() && q < a.Nq ? pdrop(a, b, h, q, keyl) : 1.f;
-          p[c][r] = pv * mk;
-          ds[c][r] = pv * (dp_acc[r] * mk - del_s[q]);
-        }
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float e = fexp2(s_acc[c][r] * sl2 - l4[c][r]);
+            p[c][r] = e;
+            ds[c][r] = e * (dp_acc[c][r] - d4[c][r]);
+          }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int q = t * 32 + c * 16 + g * 4 + r;
+            const bool ok = q < a.Nq && (fullk<MODE>(a, kb) || kok<MODE>(a, b, keyl, q));
+            const float e = fexp2(s_acc[c][r] * sl2 - l4[c][r]);
+            const float pv = ok ? e : 0.f;
+            const float mk = dropm<MODE>() && q < a.Nq ? pdrop(a, b, h, q, keyl) : 1.f;
+            p[c][r] = pv * mk;
+            ds[c][r] = pv * (dp_acc[c][r] * mk - d4[c][r]);
+          }
       }
       const bf16x8 pb = pack8(p[0], p[1]), dsb = pack8(ds[0], ds[1]);
 #pragma unroll
       for (int db = 0; db < 4; ++db) {
-        const bf16x8 dot = tr_read8_sw(dOs, t * 32, db * 16, lane, true);
-        const bf16x8 qt = tr_read8_sw(Qs, t * 32, db * 16, lane, true);
+        const bf16x8 dot = tr8(dOt + tro[db]);
+        const bf16x8 qt = tr8(Qt + tro[db]);
         dvt[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, pb, dvt[db], 0, 0, 0);
         dkt[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, dsb, dkt[db], 0, 0, 0);
       }
@@ -876,11 +912,28 @@ __global__ __launch_bounds__(1024) void attn_bwd_fused64(AttnArgs a) {
     if (wave < 8) {  // dQ^T block (dims db * 16.., queries qb * 16..) of the chunk, over every key
       const int qb = wave >> 2, db = wave & 3;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      for (int kc = 0; kc < NKC; ++kc) {
-        const bool hi = kc * 32 + 16 < NKP;
-        const bf16x8 kt = tr_read8_sw(Ks, kc * 32, db * 16, lane, hi);
-        const bf16x8 dst = tr_read8(dsi, DSST, kc * 32, qb * 16, lane);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt, dst, acc, 0, 0, 0);
+      if (NKC == 7) {  // the ViT shape (N = 197): transposed reads four key chunks ahead of the MFMA chain
+        bf16x8 kt[4], dst[4];
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) {
+          kt[kc] = tr_read8_sw(Ks, kc * 32, db * 16, lane, true);
+          dst[kc] = tr_read8(dsi, DSST, kc * 32, qb * 16, lane);
+        }
+#pragma unroll
+        for (int kc = 0; kc < 7; ++kc) {
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt[kc & 3], dst[kc & 3], acc, 0, 0, 0);
+          if (kc + 4 < 7) {
+            kt[kc & 3] = tr_read8_sw(Ks, (kc + 4) * 32, db * 16, lane, (kc + 4) * 32 + 16 < NKP);
+            dst[kc & 3] = tr_read8(dsi, DSST, (kc + 4) * 32, qb * 16, lane);
+          }
+        }
+      } else {
+        for (int kc = 0; kc < NKC; ++kc) {
+          const bool hi = kc * 32 + 16 < NKP;
+          const bf16x8 kt = tr_read8_sw(Ks, kc * 32, db * 16, lane, hi);
+          const bf16x8 dst = tr_read8(dsi, DSST, kc * 32, qb * 16, lane);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt, dst, acc, 0, 0, 0);
+        }
       }
       const int q = t * 32 + qb * 16 + i16;
       if (q < a.Nq) store4((bf16*)a.dq + (int64_t)b * a.dq_bs + (int64_t)q * a.dq_rs + hoff + db * 16 + 4 * g, acc, a.scale);
