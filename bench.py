@@ -56,7 +56,7 @@ def beam_bench(model, batch, reps, device, rank):
     return dt, gem, int(ids.shape[1])
 
 
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "round5", "gemm_traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "round6", "gemm_traffic.json")
 KERNEL_SOURCES = ["gemm.hip", "gemm8p.hip", "gemm8q.hip", "gemm_common.h", "common.h"]
 
 
