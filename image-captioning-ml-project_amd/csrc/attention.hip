@@ -69,9 +69,27 @@ __device__ __forceinline__ int xcd_bh(const AttnArgs& a) {
 __device__ __forceinline__ int64_t kv_row(const AttnArgs& a, int b, int j) {
   return (a.kv_rows && j < a.Nk - 1) ? (int64_t)a.kv_rows[(int64_t)b * a.kv_rows_ld + j] : (int64_t)b;
 }
-__device__ __forceinline__ float pdrop(const AttnArgs& a, int b, int h, int q, int key) {
-  return a.drop.mul((((uint64_t)(b + a.b_base) * a.H + h) * a.Nq + q) * a.Nk + key);
+__device__ __forceinline__ uint64_t drop_idx(const AttnArgs& a, int b, int h, int q, int key) {
+  return (((uint64_t)(b + a.b_base) * a.H + h) * a.Nq + q) * a.Nk + key;
 }
+__device__ __forceinline__ float pdrop(const AttnArgs& a, int b, int h, int q, int key) {
+  return a.drop.mul(drop_idx(a, b, h, q, key));
+}
+// Drop::mul(idx0 + off) for a run of a lane's scores from one base index (the same values as
+// pdrop: drop_hash's low-word product is (lo + off) C1 = lo C1 + off C1 mod 2^32, and a carry
+// out of the low word adds C2 to the high word's): per score two adds, a compare and the
+// finaliser, instead of the 64-bit index product and two more 32-bit multiplies.
+struct DropRun {
+  uint32_t lo, lo_c1, hi_c2;
+  __device__ __forceinline__ explicit DropRun(uint64_t idx0)
+      : lo((uint32_t)idx0), lo_c1((uint32_t)idx0 * 0x9E3779B9u), hi_c2((uint32_t)(idx0 >> 32) * 0x7FEB352Du) {}
+  __device__ __forceinline__ float mul(const Drop& d, uint32_t off) const {
+    const uint32_t l = lo + off;
+    uint32_t x = d.seed ^ (lo_c1 + off * 0x9E3779B9u) ^ (hi_c2 + (l < off ? 0x7FEB352Du : 0u));
+    x ^= x >> 16; x *= 0x85EBCA6Bu; x ^= x >> 13; x *= 0xC2B2AE35u; x ^= x >> 16;
+    return x >= d.thr ? d.scale : 0.f;
+  }
+};
 
 __device__ __forceinline__ bool key_ok(const AttnArgs& a, int b, int key, int q) {
   if (key >= a.Nk) return false;
@@ -1512,14 +1530,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HDP == 96 ?
     m[qt] = fmaxf(m[qt], __shfl_xor(m[qt], 16, 64));
     m[qt] = fmaxf(m[qt], __shfl_xor(m[qt], 32, 64));
     l[qt] = 0.f;
+    const DropRun dr(dropm<MODE>() ? drop_idx(a, b, h, 16 * qt + c16, k0 + 4 * g) : 0);  // + 16 kb + r
 #pragma unroll
     for (int kb = 0; kb < KPW / 16; ++kb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float p = m[qt] == -INFINITY ? 0.f : fexp2(sc[qt][kb][r] - m[qt]);
         l[qt] += p;  // the normaliser excludes dropout
-        sc[qt][kb][r] = dropm<MODE>() && 16 * qt + c16 < a.Nq ? p * pdrop(a, b, h, 16 * qt + c16, k0 + kb * 16 + 4 * g + r)
-                                                              : p;
+        sc[qt][kb][r] = dropm<MODE>() && 16 * qt + c16 < a.Nq ? p * dr.mul(a.drop, kb * 16 + r) : p;
       }
     l[qt] += __shfl_xor(l[qt], 16, 64);
     l[qt] += __shfl_xor(l[qt], 32, 64);
@@ -1689,12 +1707,13 @@ __global__ __launch_bounds__(256) void attn_xbwd_bf16(AttnArgs a) {
           sa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[qt][s], kf[kb][s], sa, 0, 0, 0);
           dpa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dof[qt][s], vf[kb][s], dpa, 0, 0, 0);
         }
+        const DropRun dr(dropm<MODE>() ? drop_idx(a, b, h, 16 * qt + 4 * g, key) : 0);  // + r Nk
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int q = 16 * qt + 4 * g + r;
           const bool ok = (MODE & AM_MASK) ? key_ok(a, b, key, q) : key < a.Nk;
           const float pv = ok ? fexp2(sa[r] * sl2 - lq[qt][r]) : 0.f;
-          const float mk = dropm<MODE>() && q < a.Nq ? pdrop(a, b, h, q, key) : 1.f;
+          const float mk = dropm<MODE>() && q < a.Nq ? dr.mul(a.drop, (uint32_t)(r * a.Nk)) : 1.f;
           p[qt][r] = pv * mk;
           ds[qt][r] = pv * (dpa[r] * mk - dq_[qt][r]);
         }
@@ -1824,13 +1843,14 @@ __global__ __launch_bounds__(64 * SW_WAVES) void attn_short_fwd_bf16(AttnArgs a)
     m = fmaxf(m, __shfl_xor(m, 16, 64));
     m = fmaxf(m, __shfl_xor(m, 32, 64));
     float l = 0.f;
+    const DropRun dr(dropm<MODE>() ? drop_idx(a, b, h, q, 4 * g) : 0);  // + 16 kb + r
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float p = m == -INFINITY ? 0.f : fexp2(sc[qt][kb][r] - m);
         l += p;  // the normaliser excludes dropout
-        sc[qt][kb][r] = dropm<MODE>() && q < a.Nq ? p * pdrop(a, b, h, q, 16 * kb + 4 * g + r) : p;
+        sc[qt][kb][r] = dropm<MODE>() && q < a.Nq ? p * dr.mul(a.drop, 16 * kb + r) : p;
       }
     l += __shfl_xor(l, 16, 64);
     l += __shfl_xor(l, 32, 64);
@@ -1939,12 +1959,13 @@ __global__ __launch_bounds__(64 * SB_WAVES) void attn_short_bwd_bf16(AttnArgs a)
         sa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[qt][s], kf[kb][s], sa, 0, 0, 0);
         dpa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dof[qt][s], vf[kb][s], dpa, 0, 0, 0);
       }
+      const DropRun dr(dropm<MODE>() ? drop_idx(a, b, h, 16 * qt + 4 * g, key) : 0);  // + r Nk
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int q = 16 * qt + 4 * g + r;
         const bool ok = (MODE & AM_MASK) ? key_ok(a, b, key, q) : key < a.Nk;
         const float pv = ok ? fexp2(sa[r] * sl2 - lq[qt][r]) : 0.f;
-        const float mk = dropm<MODE>() && q < a.Nq ? pdrop(a, b, h, q, key) : 1.f;
+        const float mk = dropm<MODE>() && q < a.Nq ? dr.mul(a.drop, (uint32_t)(r * a.Nk)) : 1.f;
         p[qt][r] = pv * mk;
         ds[qt][r] = pv * (dpa[r] * mk - dd[qt][r]);
       }
