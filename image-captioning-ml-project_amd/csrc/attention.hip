@@ -502,12 +502,13 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16(AttnArgs a) {
           dp_acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(dOs + qa * ST + d),
                                                            *(const bf16x8*)(Vs + keyl * ST + d), dp_acc, 0, 0, 0);
         }
+        const DropRun dr(dropm<MODE>() ? drop_idx(a, b, h, t * 32 + c * 16 + (lane >> 4) * 4, keyl) : 0);  // + r Nk
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int q = t * 32 + c * 16 + (lane >> 4) * 4 + r;
           const bool ok = q < a.Nq && (fullk<MODE>(a, kb) || kok<MODE>(a, b, keyl, q));
           const float pv = ok ? fexp2(s_acc[r] * sl2 - lse_s[q]) : 0.f;
-          const float mk = dropm<MODE>() && q < a.Nq ? pdrop(a, b, h, q, keyl) : 1.f;
+          const float mk = dropm<MODE>() && q < a.Nq ? dr.mul(a.drop, (uint32_t)(r * a.Nk)) : 1.f;
           p[c][r] = pv * mk;
           ds[c][r] = pv * (dp_acc[r] * mk - del_s[q]);
         }
@@ -554,12 +555,13 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16(AttnArgs a) {
           dp_acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(Vs + ka * ST + d),
                                                            *(const bf16x8*)(dOs + ql * ST + d), dp_acc, 0, 0, 0);
         }
+        const DropRun dr(dropm<MODE>() ? drop_idx(a, b, h, ql, t * 32 + c * 16 + (lane >> 4) * 4) : 0);  // + r
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = t * 32 + c * 16 + (lane >> 4) * 4 + r;
           const bool ok = ql < a.Nq && (fullk<MODE>(a, 2 * t + c) || kok<MODE>(a, b, key, ql));
           const float pv = ok ? fexp2(s_acc[r] * sl2 - lq) : 0.f;
-          const float mk = dropm<MODE>() && ok ? pdrop(a, b, h, ql, key) : 1.f;
+          const float mk = dropm<MODE>() && ok ? dr.mul(a.drop, r) : 1.f;
           ds[c][r] = pv * (dp_acc[r] * mk - dq_del);
         }
       }
@@ -692,12 +694,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
           s_acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(Qs + qo), kf[s], s_acc, 0, 0, 0);
           dp_acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)(dOs + qo), vf[s], dp_acc, 0, 0, 0);
         }
+        const DropRun dr(dropm<MODE>() ? drop_idx(a, b, h, t * 32 + c * 16 + (lane >> 4) * 4, keyl) : 0);  // + r Nk
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int q = t * 32 + c * 16 + (lane >> 4) * 4 + r;
           const bool ok = q < a.Nq && (fullk<MODE>(a, kb) || kok<MODE>(a, b, keyl, q));
           const float pv = ok ? fexp2(s_acc[r] * sl2 - lse_s[q]) : 0.f;
-          const float mk = dropm<MODE>() && q < a.Nq ? pdrop(a, b, h, q, keyl) : 1.f;
+          const float mk = dropm<MODE>() && q < a.Nq ? dr.mul(a.drop, (uint32_t)(r * a.Nk)) : 1.f;
           p[c][r] = pv * mk;
           ds[c][r] = pv * (dp_acc[r] * mk - del_s[q]);
           if constexpr (BIAS) dsum += ds[c][r];
@@ -896,17 +899,19 @@ __global__ __launch_bounds__(1024) void attn_bwd_fused64(AttnArgs a) {
           }
       } else {
 #pragma unroll
-        for (int c = 0; c < 2; ++c)
+        for (int c = 0; c < 2; ++c) {
+          const DropRun dr(dropm<MODE>() ? drop_idx(a, b, h, t * 32 + c * 16 + g * 4, keyl) : 0);  // + r Nk
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int q = t * 32 + c * 16 + g * 4 + r;
             const bool ok = q < a.Nq && (fullk<MODE>(a, kb) || kok<MODE>(a, b, keyl, q));
             const float e = fexp2(s_acc[c][r] * sl2 - l4[c][r]);
             const float pv = ok ? e : 0.f;
-            const float mk = dropm<MODE>() && q < a.Nq ? pdrop(a, b, h, q, keyl) : 1.f;
+            const float mk = dropm<MODE>() && q < a.Nq ? dr.mul(a.drop, (uint32_t)(r * a.Nk)) : 1.f;
             p[c][r] = pv * mk;
             ds[c][r] = pv * (dp_acc[c][r] * mk - d4[c][r]);
           }
+        }
       }
       const bf16x8 pb = pack8(p[0], p[1]), dsb = pack8(ds[0], ds[1]);
 #pragma unroll
