@@ -8,7 +8,10 @@ T = 256 * 197
 SHAPES = [("vit_qkv_fwd", T, 2304, 768), ("vit_fc1_fwd", T, 3072, 768), ("vit_fc2_fwd", T, 768, 3072),
           ("vit_o_fwd", T, 768, 768), ("lm_head_fwd", 5120, 50304, 768), ("vit_fc1_dx", T, 768, 3072),
           ("vit_fc1_dw", 3072, 768, T), ("bf16_8k", 8192, 8192, 8192), ("tdec1280_fc1", 1280, 3072, 768),
-          ("tdec1280_q", 1280, 768, 768)]
+          ("tdec1280_q", 1280, 768, 768),
+          # config-3 decoder train products (rows B*T = 5120)
+          ("dec_o_fwd", 5120, 768, 768), ("dec_fc2_fwd", 5120, 768, 3072), ("dec_qkv_fwd", 5120, 2304, 768),
+          ("dec_fc1_fwd", 5120, 3072, 768), ("dec_o_dw", 768, 768, 5120), ("dec_fc1_dw", 3072, 768, 5120)]
 
 
 def main(iters=20):
