@@ -1468,7 +1468,9 @@ template <int HDP, int MODE, int NQT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HDP == 96 ? 3 : 1, 8))) void attn_xdec_bf16(
     AttnArgs a) {
   constexpr int NW = 4, KPW = 64, ST = HDP + (HDP == 96 ? 8 : 16), NCH = HDP / 8, NS = HDP / 32, ND = HDP / 16, NQ = 16 * NQT;
-  static_assert(NQ * HDP * 4 <= KPW * ST * 2, "the fp32 partial O of a wave fits its V image");
+  constexpr int OPS = HDP + 1;  // fp32 partial-O row stride: an odd word count spreads the 16 query rows of a
+                                // store over the banks (HDP words put them on 2 bank groups: 8-way conflicts)
+  static_assert(NQ * OPS * 4 <= KPW * ST * 2, "the fp32 partial O of a wave fits its V image");
   __shared__ __attribute__((aligned(16))) bf16 vimg[NW][KPW * ST];
   __shared__ float mm[NW][NQ], ll[NW][NQ];
   const int bh = xcd_bh(a), b = bh / a.H, h = bh % a.H;
@@ -1565,13 +1567,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HDP == 96 ?
     }
   // merge the 4 waves: (m, l) per query, O^T partials into the (now free) V images as fp32
   __syncthreads();  // every wave is done reading its V image
-  float* op = (float*)vimg[w];  // [NQ queries][HDP] fp32 (fits in the wave's image)
+  float* op = (float*)vimg[w];  // [NQ queries][OPS] fp32 (fits in the wave's image)
 #pragma unroll
   for (int qt = 0; qt < NQT; ++qt)
 #pragma unroll
     for (int db = 0; db < ND; ++db)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) op[(16 * qt + c16) * HDP + db * 16 + 4 * g + r] = o[qt][db][r];
+      for (int r = 0; r < 4; ++r) op[(16 * qt + c16) * OPS + db * 16 + 4 * g + r] = o[qt][db][r];
   if (g == 0) {
 #pragma unroll
     for (int qt = 0; qt < NQT; ++qt) {
@@ -1590,7 +1592,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HDP == 96 ?
 #pragma unroll
       for (int ww = 0; ww < NW; ++ww) {
         const float f = mm[ww][q] == -INFINITY ? 0.f : fexp2(mm[ww][q] - mt);
-        num += f * ((const float*)vimg[ww])[q * HDP + d];
+        num += f * ((const float*)vimg[ww])[q * OPS + d];
         den += f * ll[ww][q];
       }
     }
@@ -1765,7 +1767,11 @@ __global__ __launch_bounds__(256) void attn_xbwd_bf16(AttnArgs a) {
   }
   // ---- dQ: the 4 waves' partials summed in a fixed order through two fp32 buffers over kimg
   __syncthreads();
-  float* red = (float*)&kimg[0][0];  // [2][NQ][HDP]
+  // row stride RS = HDP + 4 words: a store's 4 row groups (4g) land 16 banks apart (HDP words
+  // put them on the same 16 banks: 4-way conflicts)
+  constexpr int RS = HDP + 4;
+  static_assert(2 * NQ * RS * 4 <= (int)sizeof(kimg), "two padded fp32 dQ partials fit the K images");
+  float* red = (float*)&kimg[0][0];  // [2][NQ][RS]
   auto put = [&](float* buf, bool add) {
 #pragma unroll
     for (int qt = 0; qt < NQT; ++qt)
@@ -1773,18 +1779,18 @@ __global__ __launch_bounds__(256) void attn_xbwd_bf16(AttnArgs a) {
       for (int db = 0; db < ND; ++db)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float* x = buf + (16 * qt + 4 * g + r) * HDP + db * 16 + c16;
+          float* x = buf + (16 * qt + 4 * g + r) * RS + db * 16 + c16;
           *x = add ? *x + dqa[qt][db][r] : dqa[qt][db][r];
         }
   };
-  if (w < 2) put(red + w * NQ * HDP, false);
+  if (w < 2) put(red + w * NQ * RS, false);
   __syncthreads();
-  if (w >= 2) put(red + (w - 2) * NQ * HDP, true);
+  if (w >= 2) put(red + (w - 2) * NQ * RS, true);
   __syncthreads();
   for (int e = threadIdx.x; e < a.Nq * a.hd; e += blockDim.x) {
     const int q = e / a.hd, d = e % a.hd;
     ((bf16*)a.dq)[(int64_t)b * a.dq_bs + (int64_t)q * a.dq_rs + hoff + d] =
-        (bf16)((red[q * HDP + d] + red[NQ * HDP + q * HDP + d]) * a.scale);
+        (bf16)((red[q * RS + d] + red[NQ * RS + q * RS + d]) * a.scale);
   }
 }
 
