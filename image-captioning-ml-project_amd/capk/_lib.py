@@ -88,6 +88,9 @@ SIGNATURES = {
     "capk_ce_lse_bwd": (_i, [_i, _i, _i, _i, _i64, _c_p, _c_p, _i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _sz, _c_p]),
     "capk_zero": (_i, [_c_p, _sz, _c_p]),
     "capk_colsum_workspace": (_sz, [_i, _i]),
+    "capk_finish_defer": (_i, [_i]),
+    "capk_finish_flush": (_i, [_c_p]),
+    "capk_finish_flush_all": (_i, []),
     "capk_colsum": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i, _c_p, _sz, _c_p]),
     "capk_act_bwd_colsum": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _i, _c_p, _i, _c_p, _sz, _c_p]),
     "capk_gemm_dx_act_colsum_workspace": (_sz, [_i, _i, _i]),

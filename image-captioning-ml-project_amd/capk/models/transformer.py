@@ -217,61 +217,63 @@ class _DecoderFn(torch.autograd.Function):
         first = True
         for li in range(len(saved_layers) - 1, -1, -1):
             L = m.transformer_decoder.layers[li]
-            sa, ca = L.self_attn, L.multihead_attn
-            (x_in, qkv, a, lse1, kp, s1, mu1, rs1, x1, qc, kv, c, lse2, s2, mu2, rs2, x2, f_pre, f, s3, mu3,
-             rs3, drops) = saved_layers[li]
-            saved_layers[li] = None
-            on = drops[1][0] > 0
+            # the layer's LayerNorm / bias partial-sum finishes as one launch (ops.deferred_finishes)
+            with ops.deferred_finishes():
+                sa, ca = L.self_attn, L.multihead_attn
+                (x_in, qkv, a, lse1, kp, s1, mu1, rs1, x1, qc, kv, c, lse2, s2, mu2, rs2, x2, f_pre, f, s3, mu3,
+                 rs3, drops) = saved_layers[li]
+                saved_layers[li] = None
+                on = drops[1][0] > 0
 
-            def ln_bwd(dy, s, norm, mu, rs, drop):
-                """grad of s = x + dropout(branch) through norm: (ds, ds * mask)."""
-                if not on:
-                    g = ops.layernorm_bwd(dy, s, norm.weight.detach(), mu, rs, G(norm.weight), G(norm.bias))
-                    return g, g
-                gm = torch.empty_like(s)
-                g = ops.layernorm_bwd(dy, s, norm.weight.detach(), mu, rs, G(norm.weight), G(norm.bias), drop=drop,
-                                      out_drop=gm)
-                return g, gm
+                def ln_bwd(dy, s, norm, mu, rs, drop):
+                    """grad of s = x + dropout(branch) through norm: (ds, ds * mask)."""
+                    if not on:
+                        g = ops.layernorm_bwd(dy, s, norm.weight.detach(), mu, rs, G(norm.weight), G(norm.bias))
+                        return g, g
+                    gm = torch.empty_like(s)
+                    g = ops.layernorm_bwd(dy, s, norm.weight.detach(), mu, rs, G(norm.weight), G(norm.bias), drop=drop,
+                                          out_drop=gm)
+                    return g, gm
 
-            # norm3(x2 + dropout3(linear2(dropout(gelu(linear1(x2))))))
-            ds3, ds3m = ln_bwd(dx, s3, L.norm3, mu3, rs3, drops[5])
-            dfp = linear_bwd(ds3m, f, L.linear2.weight, L.linear2.bias, dt, act_bwd=ACT_GELU_ERF | ACT_DERIV, aux=f_pre,
-                             drop=drops[4])
-            ops.linear_dw(dfp, x2, G(L.linear1.weight))
-            ops.colsum(dfp, G(L.linear1.bias))
-            ops.linear_dx(dfp, W(L.linear1.weight, dt), out=ds3, beta=1.0)  # dx2 = ds3 + dfp W1
-            # norm2(x1 + dropout2(MHA(x1, mem)))
-            ds2, ds2m = ln_bwd(ds3, s2, L.norm2, mu2, rs2, drops[3])
-            dc = linear_bwd(ds2m, c, ca.out_proj.weight, ca.out_proj.bias, dt)
-            dqc = torch.empty(BT, D, dtype=dt, device=dev)
-            dkv = torch.empty(M_ext, 2 * D, dtype=dt, device=dev)
-            if rpb != S:
-                ops.zero_gap_rows(dkv, B, rpb, S)  # gap rows (e.g. ViT CLS rows) get no K/V gradient
-            ops.attention_bwd(heads(qc, 0, B, T), HeadView(kv, 0, rpb * 2 * D, 2 * D),
-                              HeadView(kv, D, rpb * 2 * D, 2 * D), heads(c, 0, B, T), heads(dc, 0, B, T), lse2,
-                              heads(dqc, 0, B, T), HeadView(dkv, 0, rpb * 2 * D, 2 * D),
-                              HeadView(dkv, D, rpb * 2 * D, 2 * D), B, H, T, S, hd, scale, drop=drops[2])
-            gW, gB = G(ca.in_proj_weight), G(ca.in_proj_bias)
-            wca = W(ca.in_proj_weight, dt)
-            ops.linear_dw(dkv, mem, gW[D:])
-            ops.colsum(dkv, gB[D:])
-            ops.linear_dx(dkv, wca[D:], out=dmem, beta=0.0 if first else 1.0)
-            first = False
-            ops.linear_dw(dqc, x1, gW[:D])
-            ops.colsum(dqc, gB[:D])
-            ops.linear_dx(dqc, wca[:D], out=ds2, beta=1.0)  # dx1 = ds2 + dqc Wq
-            # norm1(x + dropout1(SA(x)))
-            ds1, ds1m = ln_bwd(ds2, s1, L.norm1, mu1, rs1, drops[1])
-            da = linear_bwd(ds1m, a, sa.out_proj.weight, sa.out_proj.bias, dt)
-            dqkv = torch.empty_like(qkv)
-            ops.attention_bwd(heads(qkv, 0, B, T), heads(qkv, D, B, T), heads(qkv, 2 * D, B, T), heads(a, 0, B, T),
-                              heads(da, 0, B, T), lse1, heads(dqkv, 0, B, T), heads(dqkv, D, B, T),
-                              heads(dqkv, 2 * D, B, T), B, H, T, T, hd, scale, causal=True, key_pad_u8=kp,
-                              drop=drops[0])
-            ops.linear_dw(dqkv, x_in, G(sa.in_proj_weight))
-            ops.colsum(dqkv, G(sa.in_proj_bias))
-            ops.linear_dx(dqkv, W(sa.in_proj_weight, dt), out=ds1, beta=1.0)  # dx = ds1 + dqkv Win
-            dx = ds1
+                # norm3(x2 + dropout3(linear2(dropout(gelu(linear1(x2))))))
+                ds3, ds3m = ln_bwd(dx, s3, L.norm3, mu3, rs3, drops[5])
+                dfp = linear_bwd(ds3m, f, L.linear2.weight, L.linear2.bias, dt, act_bwd=ACT_GELU_ERF | ACT_DERIV, aux=f_pre,
+                                 drop=drops[4])
+                ops.linear_dw(dfp, x2, G(L.linear1.weight))
+                ops.colsum(dfp, G(L.linear1.bias))
+                ops.linear_dx(dfp, W(L.linear1.weight, dt), out=ds3, beta=1.0)  # dx2 = ds3 + dfp W1
+                # norm2(x1 + dropout2(MHA(x1, mem)))
+                ds2, ds2m = ln_bwd(ds3, s2, L.norm2, mu2, rs2, drops[3])
+                dc = linear_bwd(ds2m, c, ca.out_proj.weight, ca.out_proj.bias, dt)
+                dqc = torch.empty(BT, D, dtype=dt, device=dev)
+                dkv = torch.empty(M_ext, 2 * D, dtype=dt, device=dev)
+                if rpb != S:
+                    ops.zero_gap_rows(dkv, B, rpb, S)  # gap rows (e.g. ViT CLS rows) get no K/V gradient
+                ops.attention_bwd(heads(qc, 0, B, T), HeadView(kv, 0, rpb * 2 * D, 2 * D),
+                                  HeadView(kv, D, rpb * 2 * D, 2 * D), heads(c, 0, B, T), heads(dc, 0, B, T), lse2,
+                                  heads(dqc, 0, B, T), HeadView(dkv, 0, rpb * 2 * D, 2 * D),
+                                  HeadView(dkv, D, rpb * 2 * D, 2 * D), B, H, T, S, hd, scale, drop=drops[2])
+                gW, gB = G(ca.in_proj_weight), G(ca.in_proj_bias)
+                wca = W(ca.in_proj_weight, dt)
+                ops.linear_dw(dkv, mem, gW[D:])
+                ops.colsum(dkv, gB[D:])
+                ops.linear_dx(dkv, wca[D:], out=dmem, beta=0.0 if first else 1.0)
+                first = False
+                ops.linear_dw(dqc, x1, gW[:D])
+                ops.colsum(dqc, gB[:D])
+                ops.linear_dx(dqc, wca[:D], out=ds2, beta=1.0)  # dx1 = ds2 + dqc Wq
+                # norm1(x + dropout1(SA(x)))
+                ds1, ds1m = ln_bwd(ds2, s1, L.norm1, mu1, rs1, drops[1])
+                da = linear_bwd(ds1m, a, sa.out_proj.weight, sa.out_proj.bias, dt)
+                dqkv = torch.empty_like(qkv)
+                ops.attention_bwd(heads(qkv, 0, B, T), heads(qkv, D, B, T), heads(qkv, 2 * D, B, T), heads(a, 0, B, T),
+                                  heads(da, 0, B, T), lse1, heads(dqkv, 0, B, T), heads(dqkv, D, B, T),
+                                  heads(dqkv, 2 * D, B, T), B, H, T, T, hd, scale, causal=True, key_pad_u8=kp,
+                                  drop=drops[0])
+                ops.linear_dw(dqkv, x_in, G(sa.in_proj_weight))
+                ops.colsum(dqkv, G(sa.in_proj_bias))
+                ops.linear_dx(dqkv, W(sa.in_proj_weight, dt), out=ds1, beta=1.0)  # dx = ds1 + dqkv Win
+                dx = ds1
             notify_final(store, L.parameters())  # this layer's gradients are complete
         # embeddings (scatter-add into zeroed grads; padding_idx rows skipped)
         ops.zero_(G(m.embedding.weight))

@@ -253,40 +253,42 @@ class _ViTLayerFn(torch.autograd.Function):
         dt = L.cdtype
         x, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, f_pre, f = ctx.saved
         ctx.saved = None
-        dy = dy.contiguous()
-        D = x.shape[1]
-        H = L.num_heads
-        hd = D // H
-        at, fc1, fc2, act = L.attn, L.fc1, L.fc2, L.act
-        ln1, ln2 = L.ln1, L.ln2
-        # FC2's bias gradient = colsum(dy): already produced by the LN backward that made dy
-        # (next layer's LN1 / the head's final LN) when that one was linked to this layer
-        fused_b2 = getattr(L, "_capk_fc2_bias_done", False)
-        L._capk_fc2_bias_done = False
-        # FC1's bias gradient = colsum(dfp), fused into the GELU' pass that produces dfp
-        dfp = linear_bwd(dy, f, fc2.weight, None if fused_b2 else fc2.bias, dt, act_bwd=act | ACT_DERIV, aux=f_pre, side_dw=True,
-                         dsum=G(fc1.bias))
-        dh2 = linear_bwd(dfp, h2, fc1.weight, None, dt, side_dw=True)
-        # dx1 = the O projection's output gradient: its column sums (O bias grad) come out of the LN kernel
-        dx1 = ops.layernorm_bwd(dh2, x1, ln2.weight.detach(), mu2, rs2, G(ln2.weight), G(ln2.bias), dres=dy,
-                                dsum=G(at.o_proj.bias))
-        do = linear_bwd(dx1, o, at.o_proj.weight, None, dt, side_dw=True)
-        dqkv = torch.empty_like(qkv)
-        hv = (heads(qkv, 0, B, N), heads(qkv, D, B, N), heads(qkv, 2 * D, B, N), heads(o, 0, B, N),
-              heads(do, 0, B, N), lse, heads(dqkv, 0, B, N), heads(dqkv, D, B, N), heads(dqkv, 2 * D, B, N),
-              B, H, N, N, hd, 1.0 / math.sqrt(hd))
-        if _ATTN_BIAS:
-            # the QKV bias gradient (column sums of dQ | dK | dV) comes out of the attention backward kernels
-            ops.attention_bwd_bias(*hv, at.qkv_b.grad)
-            dh1 = linear_bwd(dqkv, h1, None, None, dt, fused=(at.qkv_w, None), side_dw=True)
-        else:
-            ops.attention_bwd(*hv)
-            dh1 = linear_bwd(dqkv, h1, None, None, dt, fused=(at.qkv_w, at.qkv_b), side_dw=True)
-        prev = getattr(L, "_capk_prev", None)
-        dx = ops.layernorm_bwd(dh1, x, ln1.weight.detach(), mu1, rs1, G(ln1.weight), G(ln1.bias), dres=dx1,
-                               dsum=G(prev.fc2.bias) if prev is not None else None)
-        if prev is not None:
-            prev._capk_fc2_bias_done = True
+        # the layer's LayerNorm / bias partial-sum finishes as one launch (ops.deferred_finishes)
+        with ops.deferred_finishes():
+            dy = dy.contiguous()
+            D = x.shape[1]
+            H = L.num_heads
+            hd = D // H
+            at, fc1, fc2, act = L.attn, L.fc1, L.fc2, L.act
+            ln1, ln2 = L.ln1, L.ln2
+            # FC2's bias gradient = colsum(dy): already produced by the LN backward that made dy
+            # (next layer's LN1 / the head's final LN) when that one was linked to this layer
+            fused_b2 = getattr(L, "_capk_fc2_bias_done", False)
+            L._capk_fc2_bias_done = False
+            # FC1's bias gradient = colsum(dfp), fused into the GELU' pass that produces dfp
+            dfp = linear_bwd(dy, f, fc2.weight, None if fused_b2 else fc2.bias, dt, act_bwd=act | ACT_DERIV, aux=f_pre, side_dw=True,
+                             dsum=G(fc1.bias))
+            dh2 = linear_bwd(dfp, h2, fc1.weight, None, dt, side_dw=True)
+            # dx1 = the O projection's output gradient: its column sums (O bias grad) come out of the LN kernel
+            dx1 = ops.layernorm_bwd(dh2, x1, ln2.weight.detach(), mu2, rs2, G(ln2.weight), G(ln2.bias), dres=dy,
+                                    dsum=G(at.o_proj.bias))
+            do = linear_bwd(dx1, o, at.o_proj.weight, None, dt, side_dw=True)
+            dqkv = torch.empty_like(qkv)
+            hv = (heads(qkv, 0, B, N), heads(qkv, D, B, N), heads(qkv, 2 * D, B, N), heads(o, 0, B, N),
+                  heads(do, 0, B, N), lse, heads(dqkv, 0, B, N), heads(dqkv, D, B, N), heads(dqkv, 2 * D, B, N),
+                  B, H, N, N, hd, 1.0 / math.sqrt(hd))
+            if _ATTN_BIAS:
+                # the QKV bias gradient (column sums of dQ | dK | dV) comes out of the attention backward kernels
+                ops.attention_bwd_bias(*hv, at.qkv_b.grad)
+                dh1 = linear_bwd(dqkv, h1, None, None, dt, fused=(at.qkv_w, None), side_dw=True)
+            else:
+                ops.attention_bwd(*hv)
+                dh1 = linear_bwd(dqkv, h1, None, None, dt, fused=(at.qkv_w, at.qkv_b), side_dw=True)
+            prev = getattr(L, "_capk_prev", None)
+            dx = ops.layernorm_bwd(dh1, x, ln1.weight.detach(), mu1, rs1, G(ln1.weight), G(ln1.bias), dres=dx1,
+                                   dsum=G(prev.fc2.bias) if prev is not None else None)
+            if prev is not None:
+                prev._capk_fc2_bias_done = True
         notify_final(store_of(L), L.parameters())  # this layer's gradients are complete
         return dx, None, None, None, None
 

@@ -7,7 +7,9 @@ eager-PyTorch fallback: a missing library or a non-GPU tensor raises.
 """
 
 import ctypes
+import contextlib
 import os
+import threading
 
 import torch
 
@@ -46,6 +48,42 @@ def _ws(nbytes, device):
 
 def lib():
     return _lib.load()
+
+
+# ------------------------------------------------------ deferred finishes ---
+# capk_finish_defer (include/capk.h): inside `deferred_finishes()` the column-sum / LayerNorm
+# partial-sum finishes are queued per stream and launched as one kernel per stream at exit
+# (the same sums, bit-identical); the workspaces they read are held here until then.
+# CAPK_FINISH_DEFER=0: every finish launches at once (A/B).
+_FIN = threading.local()
+_FIN_ON = os.environ.get("CAPK_FINISH_DEFER", "1") != "0"
+
+
+def _hold(ws):
+    """Keep a workspace whose finish may be queued alive until the context's flush."""
+    h = getattr(_FIN, "hold", None)
+    if h is not None and ws is not None:
+        h.append(ws)
+
+
+@contextlib.contextmanager
+def deferred_finishes():
+    """One launch for the partial-sum finishes issued inside (a layer's backward)."""
+    if not _FIN_ON or getattr(_FIN, "hold", None) is not None:  # off, or nested: the outer one flushes
+        yield
+        return
+    L = lib()
+    _FIN.hold = []
+    check(L.capk_finish_defer(1), "capk_finish_defer")
+    try:
+        yield
+    finally:
+        try:
+            check(L.capk_finish_flush_all(), "capk_finish_flush_all")
+        finally:
+            L.capk_finish_defer(0)
+            # the flushes are enqueued: a later kernel reusing these blocks runs after them
+            _FIN.hold = None
 
 
 # ------------------------------------------------------------------- GEMM ---
@@ -326,6 +364,7 @@ def ce_lse_bwd(logits2d, targets, B, T, V, ignore_index, lse, loss, grad_scale, 
     check(L.capk_ce_lse_bwd(dtype_code(logits2d), B, T, V, logits2d.stride(0), _p(logits2d), _p(targets),
                             int(ignore_index), _p(lse), loss[1:].data_ptr(), _p(grad_scale), _p(dlogits), _p(dbias),
                             _p(ws), wsb, _stream()), "capk_ce_lse_bwd")
+    _hold(ws)
     return dlogits
 
 
@@ -352,6 +391,7 @@ def linear_dx(dy, w, *, out=None, act_bwd=0, aux=None, beta=0.0, drop=NO_DROP, d
             check(L.capk_gemm_dx_act_colsum(M, K, N, _p(dy), dy.stride(0), _p(w), w.stride(0), _p(out), out.stride(0),
                                             int(act_bwd), _p(aux), aux.stride(0), _p(dsum), 0, _p(ws), wsb, _stream()),
                   "capk_gemm_dx_act_colsum")
+            _hold(ws)
             if timed:  # A, B, aux read once; C written once
                 ev1.record()
                 GEMM_TIMER.records.append((ev0, ev1, 2.0 * M * K * N, dtype_code(dy), 2 * (M * N + N * K + 2 * M * K), 0))
@@ -382,6 +422,7 @@ def colsum(dy, out, accumulate=False):
     ws = _ws(wsb, dy.device)
     check(L.capk_colsum(dtype_code(dy), M, N, _p(dy), dy.stride(0), _p(out), int(accumulate), _p(ws), wsb,
                         _stream()), "capk_colsum")
+    _hold(ws)
     return out
 
 
@@ -394,6 +435,7 @@ def act_bwd_colsum(c, aux, act, db, accumulate=False):
     ws = _ws(wsb, c.device)
     check(L.capk_act_bwd_colsum(dtype_code(c), M, N, _p(c), c.stride(0), _p(aux), aux.stride(0), int(act), _p(db),
                                 int(accumulate), _p(ws), wsb, _stream()), "capk_act_bwd_colsum")
+    _hold(ws)
     return c
 
 
@@ -426,6 +468,7 @@ def layernorm_bwd(dy, x, w, mean, rstd, dw, db, *, dres=None, out=None, accumula
                                float(drop[0]), int(drop[1]) & 0xFFFFFFFF, _p(out_drop),
                                out_drop.stride(0) if out_drop is not None else 0, _p(ws), wsb, _stream()),
           "capk_layernorm_bwd")
+    _hold(ws)
     return out
 
 
@@ -489,6 +532,7 @@ def attention_bwd_bias(q, k, v, o, do, lse, dq, dk, dv, B, H, Nq, Nk, hd, scale,
                                     dq.ptr(), dq.bs, dq.rs, dk.ptr(), dk.bs, dk.rs, dv.ptr(), dv.bs, dv.rs,
                                     float(drop[0]), int(drop[1]) & 0xFFFFFFFF, _p(dbias), int(accumulate), _p(ws), wsb,
                                     _stream()), "capk_attention_bwd_bias")
+    _hold(ws)
 
 
 # ------------------------------------------------------ embeddings / misc ---

@@ -73,6 +73,12 @@ template <> struct Vec8<bf16> {
   }
 };
 
+// Deferred finishes (capk_finish_defer, misc.hip): while on (this host thread), the partial-sum
+// finishes of the column-sum producers are queued per stream and launched together by
+// capk_finish_flush -- out[n] (+)= the sum over nparts rows of part[r * ld + n], n < ncols, the
+// same per-column sums as the single launches.  Returns false when deferral is off.
+bool finish_enqueue(const float* part, int64_t ld, int nparts, int ncols, float* out, int accumulate, hipStream_t st);
+
 // ------------------------------------------------------ partial-sum finish ---
 // Column i of part[nparts][ld] summed over the parts ph, ph+PH, ph+2PH, ... with four
 // independent accumulators (four loads in flight per thread).  The finish kernels run
@@ -92,10 +98,11 @@ __device__ __forceinline__ float sum_parts(const float* __restrict__ part, int64
   return (s0 + s1) + (s2 + s3);
 }
 // 1024-thread finish block: returns the column total in threads 0..15 (column blockIdx.x*16 + tid).
-__device__ __forceinline__ float finish_parts16(const float* __restrict__ part, int64_t ld, int nparts, int ncols) {
+__device__ __forceinline__ float finish_parts16(const float* __restrict__ part, int64_t ld, int nparts, int ncols,
+                                                int cb = -1) {  // cb: column block (default blockIdx.x)
   __shared__ float red[64][17];
   const int c = threadIdx.x & 15, ph = threadIdx.x >> 4;
-  const int i = blockIdx.x * 16 + c;
+  const int i = (cb < 0 ? (int)blockIdx.x : cb) * 16 + c;
   red[ph][c] = i < ncols ? sum_parts<64>(part, ld, nparts, i, ph) : 0.f;
   __syncthreads();
   if (threadIdx.x < 64) {  // 4 lanes per column, 16 phases each, then two shuffles

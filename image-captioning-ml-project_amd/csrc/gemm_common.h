@@ -340,6 +340,7 @@ int launch_gemm8p_f8(bool out_f32, int grid, const void* A, int64_t lda, const u
 bool gemm8q_supports(const Epi& e, bool out_f32);
 // misc.hip: out[n] (+)= sum over `parts` partial rows part[r][n] (fixed order)
 int launch_colsum_finish(int parts, int N, const float* part, float* out, int accumulate, hipStream_t st);
+
 // dsum != nullptr: the dX x act' product also writes per-(tile row, wave row) column-sum
 // partials [2 * cdiv(M, 256)][N] fp32 there (capk_gemm_dx_act_colsum)
 // lse_part != nullptr (plain K-major bf16 products; no tail round): also the softmax partials of

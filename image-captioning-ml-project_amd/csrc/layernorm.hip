@@ -488,6 +488,13 @@ extern "C" int capk_layernorm_bwd(int dtype, int rows, int cols, const void* dy,
 #undef L
 #undef L768
   CAPK_LAUNCH_CHECK("ln_bwd_kernel");
+  // deferred (capk_finish_defer): the weight / bias / fused-sum columns as three queued finishes
+  // over the same partial rows (the same per-column sums as ln_bwd_finish_kernel)
+  if (finish_enqueue((const float*)ws, (int64_t)np * cols, nb, cols, dw, accumulate, st)) {
+    finish_enqueue((const float*)ws + cols, (int64_t)np * cols, nb, cols, db, accumulate, st);
+    if (dsum) finish_enqueue((const float*)ws + 2 * cols, (int64_t)np * cols, nb, cols, dsum, accumulate, st);
+    return CAPK_OK;
+  }
   hipLaunchKernelGGL(ln_bwd_finish_kernel, dim3(cdiv(np * cols, 16)), dim3(1024), 0, st, nb, cols, np,
                      (const float*)ws, dw, db, dsum, accumulate);
   CAPK_LAUNCH_CHECK("ln_bwd_finish_kernel");

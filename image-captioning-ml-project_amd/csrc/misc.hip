@@ -2,6 +2,9 @@
 // position embeddings, shifted cross entropy (fwd+bwd fused), bias-gradient
 // column sums, casts/copies and the AdamW update.  All use 16-B vector
 // accesses per lane (cdna guide G13).
+#include <utility>
+#include <vector>
+
 #include "common.h"
 
 namespace capk {
@@ -584,7 +587,74 @@ static int grid_for(int64_t work, int per_block = 256) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(8192, (work + per_block - 1) / per_block));
 }
 
+// ---- deferred partial-sum finishes: one launch for the finishes a layer's backward issues
+// (its LayerNorm weight / bias / fused-bias sums and bias column sums: 4-9 launches of ~5 us,
+// each a handful of workgroups, the rest of the chip idle).  Every queued finish keeps its
+// own column blocks and the same summation order (finish_parts16), so the results are
+// bit-identical to the single launches.
+struct FinishDesc {
+  const float* part;
+  int64_t ld;
+  int nparts, ncols;
+  float* out;
+  int accumulate;
+};
+constexpr int FB_MAX = 16;
+struct FinishBatch {
+  FinishDesc d[FB_MAX];
+  int start[FB_MAX + 1];  // first column block of each finish; start[n] = the grid
+  int n;
+};
+__global__ __launch_bounds__(1024) void finish_batch_kernel(FinishBatch fb) {
+  int k = 0;
+  while (k + 1 < fb.n && (int)blockIdx.x >= fb.start[k + 1]) ++k;  // (block-uniform)
+  const FinishDesc d = fb.d[k];
+  const int cb = (int)blockIdx.x - fb.start[k];
+  const float s = finish_parts16(d.part, d.ld, d.nparts, d.ncols, cb);
+  const int n = cb * 16 + threadIdx.x;
+  if (threadIdx.x < 16 && n < d.ncols) d.out[n] = d.accumulate ? d.out[n] + s : s;
+}
+static thread_local bool t_defer = false;
+static thread_local std::vector<std::pair<hipStream_t, std::vector<FinishDesc>>> t_queues;
+static int flush_finishes(hipStream_t st) {
+  for (auto& qe : t_queues) {
+    if (qe.first != st || qe.second.empty()) continue;
+    std::vector<FinishDesc>& q = qe.second;
+    FinishBatch fb{};
+    fb.n = (int)q.size();
+    int blocks = 0;
+    for (int i = 0; i < fb.n; ++i) {
+      fb.d[i] = q[i];
+      fb.start[i] = blocks;
+      blocks += cdiv(q[i].ncols, 16);
+    }
+    fb.start[fb.n] = blocks;
+    q.clear();
+    hipLaunchKernelGGL(finish_batch_kernel, dim3(blocks), dim3(1024), 0, st, fb);
+    CAPK_LAUNCH_CHECK("finish_batch_kernel");
+  }
+  return CAPK_OK;
+}
+bool finish_enqueue(const float* part, int64_t ld, int nparts, int ncols, float* out, int accumulate, hipStream_t st) {
+  if (!t_defer) return false;
+  std::vector<FinishDesc>* q = nullptr;
+  for (auto& qe : t_queues)
+    if (qe.first == st) q = &qe.second;
+  if (!q) {
+    t_queues.emplace_back(st, std::vector<FinishDesc>());
+    q = &t_queues.back().second;
+  }
+  // a queued finish writing an overlapping output must land first (accumulation order), and
+  // a full batch goes out
+  bool clash = (int)q->size() >= FB_MAX;
+  for (const FinishDesc& d : *q) clash |= out < d.out + d.ncols && d.out < out + ncols;
+  if (clash) flush_finishes(st);
+  q->push_back(FinishDesc{part, ld, nparts, ncols, out, accumulate});
+  return true;
+}
+
 int launch_colsum_finish(int parts, int N, const float* part, float* out, int accumulate, hipStream_t st) {
+  if (finish_enqueue(part, N, parts, N, out, accumulate, st)) return CAPK_OK;
   hipLaunchKernelGGL(colsum_finish_kernel, dim3(cdiv(N, 16)), dim3(1024), 0, st, parts, N, part, out, accumulate);
   CAPK_LAUNCH_CHECK("colsum_finish_kernel");
   return CAPK_OK;
@@ -635,10 +705,7 @@ extern "C" int capk_colsum(int dtype, int M, int N, const void* dy, int64_t ldy,
   DT_DISPATCH(dtype, L, 0)
 #undef L
   CAPK_LAUNCH_CHECK("colsum_kernel");
-  hipLaunchKernelGGL(colsum_finish_kernel, dim3(cdiv(N, 16)), dim3(1024), 0, S(stream), splits, N, (const float*)ws, db,
-                     accumulate);
-  CAPK_LAUNCH_CHECK("colsum_finish_kernel");
-  return CAPK_OK;
+  return launch_colsum_finish(splits, N, (const float*)ws, db, accumulate, S(stream));
 }
 
 extern "C" int capk_act_bwd_colsum(int dtype, int M, int N, void* C, int64_t ldc, const void* aux, int64_t ldx,
@@ -655,10 +722,7 @@ extern "C" int capk_act_bwd_colsum(int dtype, int M, int N, void* C, int64_t ldc
   DT_DISPATCH(dtype, L, 0)
 #undef L
   CAPK_LAUNCH_CHECK("act_bwd_colsum_kernel");
-  hipLaunchKernelGGL(colsum_finish_kernel, dim3(cdiv(N, 16)), dim3(1024), 0, S(stream), splits, N, (const float*)ws, db,
-                     accumulate);
-  CAPK_LAUNCH_CHECK("colsum_finish_kernel");
-  return CAPK_OK;
+  return launch_colsum_finish(splits, N, (const float*)ws, db, accumulate, S(stream));
 }
 
 extern "C" size_t capk_vit_assemble_bwd_workspace(int B, int Np, int D) {
@@ -912,5 +976,20 @@ extern "C" int capk_dropout_mask(int64_t n, uint64_t offset, float p, uint32_t s
   if (n == 0) return CAPK_OK;
   hipLaunchKernelGGL(drop_mask_kernel, dim3(grid_for(n)), dim3(256), 0, S(stream), n, offset, make_drop(p, seed), out);
   CAPK_LAUNCH_CHECK("drop_mask_kernel");
+  return CAPK_OK;
+}
+
+extern "C" int capk_finish_defer(int on) {
+  capk::t_defer = on != 0;
+  return CAPK_OK;
+}
+
+extern "C" int capk_finish_flush(void* stream) { return capk::flush_finishes(S(stream)); }
+
+extern "C" int capk_finish_flush_all(void) {
+  for (auto& qe : capk::t_queues) {
+    const int rc = capk::flush_finishes(qe.first);
+    if (rc != CAPK_OK) return rc;
+  }
   return CAPK_OK;
 }

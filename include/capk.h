@@ -331,7 +331,19 @@ int capk_zero_gap_rows(void* base, int64_t ld_bytes, int64_t row_bytes, int B, i
 int capk_zero(void* ptr, size_t bytes, void* stream);
 
 /* --------------------------------------------------- Reductions ------------
- * db[n] (+)= sum_m dy[m, n]   (bias gradients; fp32 out). */
+ * Deferred finishes (round 6): with capk_finish_defer(1) on a host thread, the last step of
+ * the column-sum reductions below and of capk_layernorm_bwd (summing the per-workgroup
+ * partial rows into db / dw / dsum) is queued per stream instead of launched, and
+ * capk_finish_flush(stream) / capk_finish_flush_all() launch every queued finish of this thread
+ * in one kernel -- the same per-column sums, bit-identical outputs.  The workspaces passed to
+ * the queued calls must stay allocated until the flush is enqueued; a queued finish whose
+ * output overlaps an earlier one's flushes the queue first.  The backward of a model layer
+ * (src/models/encoders.py ViT layer, decoders.py:421-428 decoder layer) issues 4-9 such
+ * finishes: one launch instead of 4-9 launches of a few workgroups each.  Off by default. */
+int capk_finish_defer(int on);
+int capk_finish_flush(void* stream);
+int capk_finish_flush_all(void);
+/* db[n] (+)= sum_m dy[m, n]   (bias gradients; fp32 out). */
 size_t capk_colsum_workspace(int M, int N);
 int capk_colsum(int dtype, int M, int N, const void* dy, int64_t ldy, float* db, int accumulate,
                 void* ws, size_t ws_bytes, void* stream);

@@ -209,6 +209,45 @@ def test_bf16_train_steps_reduce_loss():
 
 
 @cuda
+@pytest.mark.parametrize("side", [False, True])
+def test_deferred_finishes_bit_identical(monkeypatch, side):
+    """ops.deferred_finishes -- a layer's LayerNorm weight / bias and bias column-sum finishes
+    queued and launched as one kernel per stream (capk_finish_defer / capk_finish_flush_all) --
+    vs every finish launched at once: a config-3 bf16 train-mode step (decoder dropout on, the
+    same dropout seeds; with and without the weight-gradient side stream, whose column sums
+    queue on their own stream) gives bit-identical gradients for every parameter."""
+    from capk import ops
+    from capk.models import common
+    from capk.train import CombinedLoss
+    monkeypatch.setattr(common, "DW_STREAM", side)
+    model, store, cfg, _ = _full_model("bf16")
+    B = 4
+    g = torch.Generator(device="cuda").manual_seed(0)
+    images = torch.randn(B, 3, 224, 224, device="cuda", generator=g)
+    caps = torch.randint(0, 50256, (B, 20), device="cuda", generator=g)
+    caps[1, 12:] = 50256
+    model.train()
+    loss_fn = CombinedLoss(50256)
+    seed0 = common._SEED[0]
+    grads = {}
+    for on in (False, True):
+        monkeypatch.setattr(ops, "_FIN_ON", on)
+        common._SEED[0] = seed0  # the same dropout masks
+        out = model(images=images, captions=caps)
+        loss_fn(out["logits"], caps)["total_loss"].backward()
+        torch.cuda.synchronize()
+        grads[on] = {n: p._capk_grad.clone() for n, p in model.named_parameters() if getattr(p, "_capk_grad", None) is not None}
+    assert grads[True].keys() == grads[False].keys() and len(grads[True]) > 200
+    # (the token / position embedding gradients are scatter-added with fp32 atomics: their
+    # summation order, hence their last bits, differ between any two runs)
+    atomic = {"decoder.embedding.weight", "decoder.position_encoding.weight"}
+    bad = [n for n in grads[True] if n not in atomic and not torch.equal(grads[True][n], grads[False][n])]
+    assert not bad, bad[:10]
+    for n in atomic & grads[True].keys():
+        torch.testing.assert_close(grads[True][n], grads[False][n], rtol=1e-5, atol=1e-7)
+
+
+@cuda
 def test_decoder_train_mode_dropout_matches_masked_reference(golden_dir):
     """Train-mode decoder (p=0.1 at 7 sites) vs a PyTorch reference applying the SAME masks
     (materialised with capk_dropout_mask from the intercepted per-site seeds): logits and
