@@ -314,8 +314,12 @@ __global__ __launch_bounds__(256) void ln_bwd768_kernel(int rows, const bf16* __
       if constexpr (SUM) ds[c][i] = 0.f;
     }
   }
-  struct Row { bf16x4 x[NC], d[NC], r[NC]; };
+  // the row's statistics travel with its operands: loaded at the head of step() they were the
+  // youngest loads, and the in-order vmcnt wait for them drained the next row's prefetch too
+  struct Row { bf16x4 x[NC], d[NC], r[NC]; float mu, rs; };
   auto fetch = [&](int row, Row& R) {
+    R.mu = mean[row];
+    R.rs = rstd[row];
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int col = (lane + 64 * c) * 4;
@@ -327,7 +331,7 @@ __global__ __launch_bounds__(256) void ln_bwd768_kernel(int rows, const bf16* __
   // one row: statistics from R, then R is refilled with row `nxt` (its loads overlap this
   // row's reductions and stores), then dx
   auto step = [&](Row& R, int row, int nxt) {
-    const float mu = mean[row], rs = rstd[row];
+    const float mu = R.mu, rs = R.rs;
     float xh[NC][4], g[NC][4], r[NC][4];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll

@@ -62,6 +62,14 @@ if [[ ,$S, == *,libbench,* ]]; then  # config-3 bench per library, alternated, 2
     done
   done
 fi
+if [[ ,$S, == *,lnab,* ]]; then  # tools/ln_bench.py per library, libraries alternated, 2 rounds
+  for r in 1 2; do
+    for L in libcapk.so ${LIBS}; do
+      CAPK_LIB_PATH=$PWD/image-captioning-ml-project_amd/capk/$L run lnab_${L}_$r 120 python -u tools/ln_bench.py
+    done
+  done
+  for L in libcapk.so ${LIBS}; do echo "== $L"; cat $OUT/lnab_${L}_*.log | grep us; done > $OUT/lnab_table.txt
+fi
 if [[ ,$S, == *,traffic,* ]]; then  # GEMM bytes per launch for bench.py's roofline.traffic (-> profiles/round6/gemm_traffic.json)
   TC="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --beam-batch 0"
   run fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/fetch -o run -- $TC
