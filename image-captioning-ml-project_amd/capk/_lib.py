@@ -96,8 +96,11 @@ SIGNATURES = {
     "capk_gemm_dx_act_colsum_workspace": (_sz, [_i, _i, _i]),
     "capk_gemm_dx_act_colsum": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p, _i64, _i, _c_p, _i64, _c_p, _i, _c_p,
                                      _sz, _c_p]),
+    "capk_gemm_dx_act_colsum_wt": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p, _i64, _i, _c_p, _i64, _c_p, _i,
+                                        _c_p, _sz, _c_p]),
     "capk_cast": (_i, [_i, _i, _i64, _c_p, _c_p, _c_p]),
     "capk_copy_rows": (_i, [_i, _i, _i, _c_p, _i64, _c_p, _i64, _c_p]),
+    "capk_transpose_bf16_batch": (_i, [_i, _c_p, _c_p]),
     "capk_act_bwd": (_i, [_i, _i64, _i, _c_p, _c_p, _c_p, _c_p]),
     "capk_adamw": (_i, [_i64, _c_p, _c_p, _c_p, _c_p, _c_p, _f, _f, _f, _f, _f, _f, _f, _c_p]),
     "capk_dropout_apply": (_i, [_i, _i, _i, _c_p, _i64, _f, _u32, _c_p, _i64, _c_p]),

@@ -10,6 +10,7 @@ import ctypes
 import contextlib
 import os
 import threading
+import weakref
 
 import torch
 
@@ -225,6 +226,104 @@ class Fp8State:
 FP8 = Fp8State()
 
 
+class _TransposeDesc(ctypes.Structure):
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("ld_src", ctypes.c_int64),
+                ("ld_dst", ctypes.c_int64), ("rows", ctypes.c_int32), ("cols", ctypes.c_int32)]
+
+
+class WeightT:
+    """K-major copies of the bf16 weights for the backward's dX products.
+
+    dX = dY W reads W [N_out][K_in] N-major; the same product with W^T [K_in][N_out] runs on the
+    K-major GEMM paths, 3-30 % faster on the config-3 shapes (profiles/round6/dx_kmajor.txt:
+    e.g. the ViT QKV dX 206 -> 182 us, the decoder FC1 dX 51 -> 36 us).  A copy is made the
+    first time a ParamStore weight reaches `linear_dx` and refreshed once per optimizer step
+    (`weights_changed`): the first dX product after a change re-transposes every known copy on
+    that device in one batched launch (capk_transpose_bf16_batch).  Views outside a live
+    ParamStore bf16 shadow, fp32 weights, products under graph capture and short products
+    (M < 2048 rows) keep the N-major operand.  CAPK_WT=0 turns the copies off (A/B)."""
+
+    MIN_ROWS = 2048
+    MAX_DIM = 8192  # (the LM-head dX, K = 50 304, stays on its split-K path)
+
+    def __init__(self):
+        self.enabled = os.environ.get("CAPK_WT", "1") != "0"
+        self.epoch = 0
+        self.buffers = []  # (weakref of a ParamStore bf16 shadow, start, end)
+        self.cache = {}    # (device, ptr, rows, cols, ld) -> [epoch, W^T]
+        self.lock = threading.Lock()
+
+    def register(self, buf):
+        """A new ParamStore shadow: its memory may be a freed store's, so every copy goes stale."""
+        with self.lock:
+            self._prune()
+            self.buffers.append((weakref.ref(buf), buf.data_ptr(), buf.data_ptr() + buf.numel() * buf.element_size()))
+            self.epoch += 1
+
+    def weights_changed(self):
+        self.epoch += 1
+
+    def _prune(self):
+        dead = [(a, b) for r, a, b in self.buffers if r() is None]
+        if dead:
+            self.buffers = [e for e in self.buffers if e[0]() is not None]
+            self.cache = {k: v for k, v in self.cache.items() if not any(a <= k[1] < b for a, b in dead)}
+
+    def _owned(self, w):
+        p = w.data_ptr()
+        end = p + ((w.shape[0] - 1) * w.stride(0) + w.shape[1]) * w.element_size()
+        return any(r() is not None and a <= p and end <= b for r, a, b in self.buffers)
+
+    def get(self, w, M):
+        """W^T for the dX product of M rows against `w`, or None (use `w` N-major)."""
+        if not self.enabled or M < self.MIN_ROWS or w.dtype != torch.bfloat16 or not w.is_cuda or w.dim() != 2:
+            return None
+        rows, cols = w.shape
+        if (w.stride(1) != 1 or rows % 8 or cols % 8 or w.stride(0) % 8 or w.data_ptr() % 16
+                or max(rows, cols) > self.MAX_DIM or torch.cuda.is_current_stream_capturing()):
+            return None
+        with self.lock:
+            if not self._owned(w):
+                return None
+            key = (w.device, w.data_ptr(), rows, cols, w.stride(0))
+            ent = self.cache.get(key)
+            if ent is None:
+                ent = self.cache[key] = [None, torch.empty(cols, rows, dtype=torch.bfloat16, device=w.device)]
+            if ent[0] != self.epoch:
+                self._refresh(w.device)
+            return ent[1]
+
+    def _refresh(self, dev):
+        stale = [(k, e) for k, e in self.cache.items() if k[0] == dev and e[0] != self.epoch]
+        _transpose_batch([(k[1], k[4], k[2], k[3], e[1]) for k, e in stale])
+        for _, e in stale:
+            e[0] = self.epoch
+
+
+def _transpose_batch(items):
+    """[(src pointer, src row stride, rows, cols, dst [cols, rows] bf16 tensor)] -> one
+    capk_transpose_bf16_batch call (one launch per 64 matrices)."""
+    descs = (_TransposeDesc * max(1, len(items)))()
+    for i, (src, ld, rows, cols, dst) in enumerate(items):
+        descs[i] = _TransposeDesc(src, dst.data_ptr(), ld, dst.stride(0), rows, cols)
+    check(lib().capk_transpose_bf16_batch(len(items), ctypes.cast(descs, ctypes.c_void_p), _stream()),
+          "capk_transpose_bf16_batch")
+
+
+def transpose_bf16_batch(pairs):
+    """dst <- src^T for every (src [R, C], dst [C, R]) bf16 pair (unit column strides), in one
+    batched launch per 64 pairs."""
+    for src, dst in pairs:
+        _need_gpu(src, dst)
+        if src.dtype != torch.bfloat16 or dst.dtype != torch.bfloat16 or src.dim() != 2 or \
+                src.stride(1) != 1 or dst.stride(1) != 1 or tuple(dst.shape) != (src.shape[1], src.shape[0]):
+            raise _lib.CapkError("transpose_bf16_batch: need bf16 src [R, C] and dst [C, R] with unit column strides")
+    _transpose_batch([(s.data_ptr(), s.stride(0), s.shape[0], s.shape[1], d) for s, d in pairs])
+
+
+WT = WeightT()
+
+
 def quant_fp8(x, *, transpose=False, q=None, scale=None):
     """e4m3fn rows with E8M0 per-row scales (capk_quant_fp8).  transpose: x [K, N] -> q [N, K]."""
     _need_gpu(x)
@@ -388,8 +487,10 @@ def linear_dx(dy, w, *, out=None, act_bwd=0, aux=None, beta=0.0, drop=NO_DROP, d
                 ev0 = torch.cuda.Event(enable_timing=True)
                 ev1 = torch.cuda.Event(enable_timing=True)
                 ev0.record()
-            check(L.capk_gemm_dx_act_colsum(M, K, N, _p(dy), dy.stride(0), _p(w), w.stride(0), _p(out), out.stride(0),
-                                            int(act_bwd), _p(aux), aux.stride(0), _p(dsum), 0, _p(ws), wsb, _stream()),
+            wt = WT.get(w, M)
+            fn, wop = (L.capk_gemm_dx_act_colsum_wt, wt) if wt is not None else (L.capk_gemm_dx_act_colsum, w)
+            check(fn(M, K, N, _p(dy), dy.stride(0), _p(wop), wop.stride(0), _p(out), out.stride(0),
+                     int(act_bwd), _p(aux), aux.stride(0), _p(dsum), 0, _p(ws), wsb, _stream()),
                   "capk_gemm_dx_act_colsum")
             _hold(ws)
             if timed:  # A, B, aux read once; C written once
@@ -398,7 +499,12 @@ def linear_dx(dy, w, *, out=None, act_bwd=0, aux=None, beta=0.0, drop=NO_DROP, d
             return out
         gemm(dy, True, w, False, M, K, N, out, lda=dy.stride(0), ldb=w.stride(0), ldc=out.stride(0))
         return act_bwd_colsum(out, aux, act_bwd, dsum)
-    gemm(dy, True, w, False, M, K, N, out, lda=dy.stride(0), ldb=w.stride(0), ldc=out.stride(0), beta=beta,
+    wt = WT.get(w, M)
+    if wt is not None:  # the K-major copy (WeightT)
+        w, bk = wt, True
+    else:
+        bk = False
+    gemm(dy, True, w, bk, M, K, N, out, lda=dy.stride(0), ldb=w.stride(0), ldc=out.stride(0), beta=beta,
          act=(ACT_BWD | act_bwd) if act_bwd else 0, aux=aux, ldx=aux.stride(0) if aux is not None else 0,
          drop=drop)
     return out
@@ -660,6 +766,8 @@ def adamw(param, grad, m, v, param_bf16, lr, wd, beta1, beta2, eps, step):
     bc2 = 1.0 - beta2 ** step
     check(lib().capk_adamw(param.numel(), _p(param), _p(grad), _p(m), _p(v), _p(param_bf16), float(lr), float(wd),
                            float(beta1), float(beta2), float(eps), float(bc1), float(bc2), _stream()), "capk_adamw")
+    if param_bf16 is not None:
+        WT.weights_changed()  # a bf16 shadow changed: the K-major dX copies are stale
 
 
 # ---------------------------------------------------------- Conv1D (GPT-2) ---

@@ -171,6 +171,9 @@ class ParamStore:
                     req = off
                 self.params.append(p)
             self.master[g], self.grad[g], self.bf16[g] = master, grad, shadow
+            if shadow is not None and shadow.is_cuda:
+                from . import ops
+                ops.WT.register(shadow)
             self.required_numel[g] = req
         for f in fused:
             self._bind_fused(f)
@@ -195,6 +198,7 @@ class ParamStore:
         """Re-derive the bf16 shadow after the master weights changed outside the optimizer."""
         from . import ops
         ops.FP8.weights_changed()
+        ops.WT.weights_changed()
         for g in self.groups:
             if self.bf16[g] is not None and self.master[g].is_cuda:
                 ops.cast(self.master[g], self.bf16[g])

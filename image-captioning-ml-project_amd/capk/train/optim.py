@@ -94,6 +94,7 @@ class CapkAdamW:
                           pg["weight_decay"], self.betas[0], self.betas[1], self.eps, n)
         st.written_optional.clear()
         ops.FP8.weights_changed()  # fp8 weight copies are re-quantised on their next use
+        ops.WT.weights_changed()   # and the K-major dX copies re-transposed (ops.WeightT)
 
     def zero_grad(self, set_to_none=False):
         # capk backward passes overwrite every gradient they produce (no accumulation

@@ -892,30 +892,43 @@ extern "C" size_t capk_gemm_dx_act_colsum_workspace(int M, int N, int K) {
   return std::max(g, std::max(c, d));
 }
 
-extern "C" int capk_gemm_dx_act_colsum(int M, int N, int K, const void* dY, int64_t ldy, const void* W, int64_t ldw,
-                                       void* C, int64_t ldc, int act, const void* aux, int64_t ldx, float* db,
-                                       int accumulate, void* ws, size_t ws_bytes, void* stream) {
+// w_kmajor: W given as its K-major copy W^T [N][K] (capk_gemm_dx_act_colsum_wt)
+static int dx_act_colsum(int M, int N, int K, const void* dY, int64_t ldy, const void* W, int64_t ldw, int w_kmajor,
+                         void* C, int64_t ldc, int act, const void* aux, int64_t ldx, float* db, int accumulate,
+                         void* ws, size_t ws_bytes, void* stream) {
   CAPK_CHECK_ARG(M > 0 && N > 0 && K > 0 && dY && W && C && aux && db && (act & 15),
                  "capk_gemm_dx_act_colsum: bad arguments");
   CAPK_CHECK_ARG(ws && ws_bytes >= capk_gemm_dx_act_colsum_workspace(M, N, K),
                  "capk_gemm_dx_act_colsum: workspace too small");
   const int act_bwd = CAPK_ACT_BWD | act;
   Epi e{C, ldc, 1.f, 0.f, nullptr, nullptr, 0, act_bwd, nullptr, aux, ldx, M, N, make_drop(0.f, 0)};
-  const int cfg = choose_cfg(M, N, K, 1, 0, act_bwd);
+  const int cfg = choose_cfg(M, N, K, 1, w_kmajor, act_bwd);
   const int splits = choose_splits(cfg, M, N, K);
   const bool fused = (cfg == 5 || cfg == 6) && splits == 1 && (act & CAPK_ACT_DERIV) && K % 32 == 0 &&
                      tiles_of(6, M, N) > 256 && gemm8q_supports(e, false) && K >= 128;
   if (fused) {
     g_last_cfg = 6;
-    const int rc = launch_gemm8q(true, false, false, dY, ldy, W, ldw, M, N, K, 1, e, nullptr, S(stream), (float*)ws,
-                                 nullptr, 0, nullptr, nullptr);
+    const int rc = launch_gemm8q(true, w_kmajor != 0, false, dY, ldy, W, ldw, M, N, K, 1, e, nullptr, S(stream),
+                                 (float*)ws, nullptr, 0, nullptr, nullptr);
     if (rc != CAPK_OK) return rc;
     return launch_colsum_finish(cdiv(M, 256) * 2, N, (const float*)ws, db, accumulate, S(stream));
   }
-  int rc = capk_gemm(CAPK_BF16, CAPK_BF16, M, N, K, dY, ldy, 1, W, ldw, 0, C, ldc, 1.f, 0.f, nullptr, nullptr, 0, 0,
-                     nullptr, nullptr, 0, 0.f, 0, ws, ws_bytes, stream);
+  int rc = capk_gemm(CAPK_BF16, CAPK_BF16, M, N, K, dY, ldy, 1, W, ldw, w_kmajor, C, ldc, 1.f, 0.f, nullptr, nullptr,
+                     0, 0, nullptr, nullptr, 0, 0.f, 0, ws, ws_bytes, stream);
   if (rc != CAPK_OK) return rc;
   return capk_act_bwd_colsum(CAPK_BF16, M, N, C, ldc, aux, ldx, act, db, accumulate, ws, ws_bytes, stream);
+}
+
+extern "C" int capk_gemm_dx_act_colsum(int M, int N, int K, const void* dY, int64_t ldy, const void* W, int64_t ldw,
+                                       void* C, int64_t ldc, int act, const void* aux, int64_t ldx, float* db,
+                                       int accumulate, void* ws, size_t ws_bytes, void* stream) {
+  return dx_act_colsum(M, N, K, dY, ldy, W, ldw, 0, C, ldc, act, aux, ldx, db, accumulate, ws, ws_bytes, stream);
+}
+
+extern "C" int capk_gemm_dx_act_colsum_wt(int M, int N, int K, const void* dY, int64_t ldy, const void* WT,
+                                          int64_t ldwt, void* C, int64_t ldc, int act, const void* aux, int64_t ldx,
+                                          float* db, int accumulate, void* ws, size_t ws_bytes, void* stream) {
+  return dx_act_colsum(M, N, K, dY, ldy, WT, ldwt, 1, C, ldc, act, aux, ldx, db, accumulate, ws, ws_bytes, stream);
 }
 
 // fp8 GEMM (config 5): C = epilogue((diag(2^sa) A8) (diag(2^sb) B8)^T), A8 [M][K], B8 [N][K]

@@ -1001,10 +1001,11 @@ int launch_gemm8q(bool a_kmajor, bool b_kmajor, bool out_f32, const void* A, int
     hipLaunchKernelGGL((gemm8q_kernel<true, true, bf16, 0, false, SIDE_NONE, false, false, true>), grid, block, 0, st,
                        A, lda, B, ldb, M, N, K, 1, p);
   } else if (dsum) {  // dX with the backward-activation multiply + column sums (capk_gemm_dx_act_colsum)
-    CAPK_CHECK_ARG(a_kmajor && !b_kmajor && !out_f32 && sk == SIDE_AUX,
+    CAPK_CHECK_ARG(a_kmajor && !out_f32 && sk == SIDE_AUX,
                    "capk_gemm(gemm8q): column sums only on the dX x act' product");
     p.dsum = dsum;
-    L8(true, false, bf16, 0, false, SIDE_AUX, true);
+    if (b_kmajor) L8(true, true, bf16, 0, false, SIDE_AUX, true);  // (the weight's K-major copy)
+    else L8(true, false, bf16, 0, false, SIDE_AUX, true);
   } else if (out_f32) {  // fp32 outputs: no activation, no side operand (gemm8q_supports)
     if (a_kmajor && b_kmajor) L8(true, true, float, 0, false, SIDE_NONE, false);
     else if (a_kmajor) L8(true, false, float, 0, false, SIDE_NONE, false);

@@ -986,6 +986,78 @@ extern "C" int capk_finish_defer(int on) {
 
 extern "C" int capk_finish_flush(void* stream) { return capk::flush_finishes(S(stream)); }
 
+namespace capk {
+// ------------------------------------------------------- batched transpose --
+// dst[c][r] = src[r][c] (bf16 bits) for up to TR_MAX matrices per launch: one workgroup per
+// 64 x 64 tile, 16-B row loads into an LDS tile, 16-B stores of its columns.  The weight
+// copies are a few MB each (HBM-bound, ~0.4 GB per training step in all).
+constexpr int TR_MAX = 64;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+struct TrDesc {
+  const uint16_t* src;
+  uint16_t* dst;
+  int64_t lds, ldd;
+  int rows, cols, tiles_c, tile0;
+};
+struct TrBatch {
+  TrDesc d[TR_MAX];
+  int n;
+};
+__global__ __launch_bounds__(256) void transpose_batch_kernel(TrBatch b) {
+  __shared__ __attribute__((aligned(16))) uint16_t t[64][64 + 8];
+  int k = 0;
+  while (k + 1 < b.n && (int)blockIdx.x >= b.d[k + 1].tile0) ++k;  // (block-uniform)
+  const TrDesc d = b.d[k];
+  const int tile = (int)blockIdx.x - d.tile0;
+  const int r0 = (tile / d.tiles_c) * 64, c0 = (tile % d.tiles_c) * 64;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int idx = threadIdx.x + h * 256, r = idx >> 3, ch = idx & 7;
+    if (r0 + r < d.rows && c0 + ch * 8 < d.cols) {
+      const u32x4 v = *(const u32x4*)(d.src + (int64_t)(r0 + r) * d.lds + c0 + ch * 8);
+      *(u32x4*)&t[r][ch * 8] = v;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int idx = threadIdx.x + h * 256, c = idx >> 3, rch = idx & 7;
+    if (c0 + c < d.cols && r0 + rch * 8 < d.rows) {
+      uint16_t o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = t[rch * 8 + i][c];
+      u32x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = ((uint32_t)o[2 * i] | ((uint32_t)o[2 * i + 1] << 16));
+      *(u32x4*)(d.dst + (int64_t)(c0 + c) * d.ldd + r0 + rch * 8) = v;
+    }
+  }
+}
+}  // namespace capk
+
+extern "C" int capk_transpose_bf16_batch(int n, const capk_transpose_desc* descs, void* stream) {
+  CAPK_CHECK_ARG(n >= 0 && (n == 0 || descs), "capk_transpose_bf16_batch: null descriptors");
+  for (int i0 = 0; i0 < n; i0 += capk::TR_MAX) {
+    capk::TrBatch b{};
+    int tiles = 0;
+    b.n = std::min(capk::TR_MAX, n - i0);
+    for (int k = 0; k < b.n; ++k) {
+      const capk_transpose_desc& s = descs[i0 + k];
+      CAPK_CHECK_ARG(s.src && s.dst && s.rows > 0 && s.cols > 0 && s.rows % 8 == 0 && s.cols % 8 == 0 &&
+                         s.ld_src % 8 == 0 && s.ld_dst % 8 == 0 && s.ld_src >= s.cols && s.ld_dst >= s.rows &&
+                         (uintptr_t)s.src % 16 == 0 && (uintptr_t)s.dst % 16 == 0,
+                     "capk_transpose_bf16_batch: descriptor %d (rows=%d cols=%d): sizes / strides must be "
+                     "multiples of 8, pointers 16-B aligned", i0 + k, s.rows, s.cols);
+      const int tc = cdiv(s.cols, 64);
+      b.d[k] = capk::TrDesc{(const uint16_t*)s.src, (uint16_t*)s.dst, s.ld_src, s.ld_dst, s.rows, s.cols, tc, tiles};
+      tiles += cdiv(s.rows, 64) * tc;
+    }
+    hipLaunchKernelGGL(capk::transpose_batch_kernel, dim3(tiles), dim3(256), 0, S(stream), b);
+    CAPK_LAUNCH_CHECK("transpose_batch_kernel");
+  }
+  return CAPK_OK;
+}
+
 extern "C" int capk_finish_flush_all(void) {
   for (auto& qe : capk::t_queues) {
     const int rc = capk::flush_finishes(qe.first);

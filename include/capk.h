@@ -363,9 +363,26 @@ size_t capk_gemm_dx_act_colsum_workspace(int M, int N, int K);
 int capk_gemm_dx_act_colsum(int M, int N, int K, const void* dY, int64_t ldy, const void* W, int64_t ldw, void* C,
                             int64_t ldc, int act, const void* aux, int64_t ldx, float* db, int accumulate, void* ws,
                             size_t ws_bytes, void* stream);
+/* The same with W given as its K-major copy WT = W^T [N][K] (ldwt): capk_transpose_bf16_batch. */
+int capk_gemm_dx_act_colsum_wt(int M, int N, int K, const void* dY, int64_t ldy, const void* WT, int64_t ldwt,
+                               void* C, int64_t ldc, int act, const void* aux, int64_t ldx, float* db, int accumulate,
+                               void* ws, size_t ws_bytes, void* stream);
 /* elementwise casts / copies */
 int capk_cast(int in_dtype, int out_dtype, int64_t n, const void* x, void* y, void* stream);
 int capk_copy_rows(int dtype, int rows, int cols, const void* x, int64_t ldx, void* y, int64_t ldy, void* stream);
+/* Batched bf16 transposes (round 6): dst[c][r] = src[r][c] for every descriptor, all in one
+ * launch per 64 descriptors.  The backward's dX products read the weight W [N_out][K_in]
+ * N-major; a K-major copy W^T [K_in][N_out], refreshed once per optimizer step for every
+ * weight the dX products use (capk/ops.py WeightT), runs them on the K-major GEMM paths
+ * (nn.Linear backward, torch autograd; the reference's decoders.py / ViT layers).  rows, cols,
+ * ld_src and ld_dst multiples of 8; src / dst 16-B aligned. */
+typedef struct capk_transpose_desc {
+  const void* src;
+  void* dst;
+  int64_t ld_src, ld_dst;
+  int32_t rows, cols;
+} capk_transpose_desc;
+int capk_transpose_bf16_batch(int n, const capk_transpose_desc* descs, void* stream);
 
 /* y = x * dropout-mask(p, seed, index r*cols + c) — the GEMM-epilogue mask of an
  * [rows, cols] output re-applied to its gradient (GPT-2 resid_dropout backward,

@@ -184,6 +184,40 @@ def test_dx_act_colsum_fused(M):
 
 
 @cuda
+@pytest.mark.parametrize("M", [6400 - 24, 1000])
+def test_dx_act_colsum_weight_copy(M):
+    """capk_gemm_dx_act_colsum_wt (W as its K-major copy, ops.WeightT): the same fused product
+    and column sums as capk_gemm_dx_act_colsum on the N-major weight, both routes (persistent
+    fused epilogue at M = 6376, product + act_bwd_colsum at M = 1000)."""
+    from capk import ops
+    from capk._lib import ACT_DERIV, ACT_GELU_ERF
+    g = torch.Generator(device="cuda").manual_seed(M + 1)
+    N, K = 3072, 768
+    shadow = torch.zeros(K * N, device="cuda", dtype=torch.bfloat16)
+    ops.WT.register(shadow)
+    w = shadow.view(K, N)
+    w.copy_((torch.randn(K, N, device="cuda", generator=g) / math.sqrt(K)).bfloat16())
+    dy = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    aux = torch.rand(M, N, device="cuda", generator=g).bfloat16()
+    res = {}
+    ops.WT.MIN_ROWS = 1  # (instance override: the short product takes the copy too)
+    for on in (True, False):
+        ops.WT.enabled = on
+        try:
+            assert (ops.WT.get(w, M) is not None) == on
+            db = torch.full((N,), 7.0, device="cuda")
+            res[on] = (ops.linear_dx(dy, w, act_bwd=ACT_GELU_ERF | ACT_DERIV, aux=aux, dsum=db), db)
+        finally:
+            ops.WT.enabled = True
+    del ops.WT.MIN_ROWS
+    ref = (dy.float() @ w.float()) * aux.float()
+    for on in (True, False):
+        assert _rel(res[on][0], ref) < 1e-2
+        assert _rel(res[on][1], ref.sum(0)) < 2e-3
+    assert _rel(res[True][0], res[False][0]) < 1e-2
+
+
+@cuda
 @pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
 def test_tail_round_exact(mode, ak, bk):

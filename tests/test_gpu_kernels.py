@@ -21,6 +21,62 @@ def _rel(a, b):
     return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-30))
 
 
+# ------------------------------------------------ weight transposes (round 6) ----
+@cuda
+def test_transpose_bf16_batch(ops):
+    """capk_transpose_bf16_batch: bit-exact transposes of ragged shapes (partial 64 x 64 edge
+    tiles), strided sources, and more than 64 matrices (two launches)."""
+    g = torch.Generator(device="cuda").manual_seed(0)
+    shapes = [(8, 8), (72, 136), (768, 2304), (2304, 768), (64, 64), (200, 520)] + [(16, 24)] * 70
+    pairs = []
+    for i, (r, c) in enumerate(shapes):
+        base = torch.randn(r, c + (8 if i % 3 == 1 else 0), device="cuda", generator=g).bfloat16()
+        src = base[:, :c]  # (every third one a strided view)
+        pairs.append((src, torch.full((c, r), float("nan"), device="cuda", dtype=torch.bfloat16)))
+    ops.transpose_bf16_batch(pairs)
+    for src, dst in pairs:
+        assert torch.equal(dst, src.t()), tuple(src.shape)
+
+
+@cuda
+@pytest.mark.parametrize("N,K", [(2304, 768), (768, 3072), (768, 768)])
+def test_linear_dx_weight_copy(ops, N, K):
+    """ops.WeightT: the dX product on the K-major weight copy matches the N-major operand
+    (fp32 reference of the bf16 inputs), follows an in-place weight change once
+    weights_changed() is signalled, and is refreshed by ops.adamw writing the bf16 shadow."""
+    g = torch.Generator(device="cuda").manual_seed(1)
+    M = 4096
+    shadow = torch.zeros(N * K + 4096, device="cuda", dtype=torch.bfloat16)
+    ops.WT.register(shadow)
+    w = shadow[:N * K].view(N, K)
+    w.copy_((torch.randn(N, K, device="cuda", generator=g) / math.sqrt(N)).bfloat16())
+    dy = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    wt = ops.WT.get(w, M)  # the copy path is taken, with an exact transpose
+    assert wt is not None and torch.equal(wt, w.t())
+    out = ops.linear_dx(dy, w)
+    ref = dy.float() @ w.float()
+    assert _rel(out, ref) < 1e-2
+    ops.WT.enabled = False
+    try:
+        out_n = ops.linear_dx(dy, w)
+    finally:
+        ops.WT.enabled = True
+    assert _rel(out, out_n) < 1e-2
+    w.neg_()
+    ops.WT.weights_changed()
+    assert torch.equal(ops.WT.get(w, M), w.t())
+    assert _rel(ops.linear_dx(dy, w), -ref) < 1e-2
+    # the optimizer path: AdamW rewriting the bf16 shadow invalidates the copies by itself
+    master = w.float().reshape(-1).contiguous()
+    grad = torch.randn(master.numel(), device="cuda", generator=g)
+    m, v = torch.zeros_like(master), torch.zeros_like(master)
+    ops.adamw(master, grad, m, v, shadow[:N * K], 1e-2, 0.0, 0.9, 0.999, 1e-8, 1)
+    assert torch.equal(ops.WT.get(w, M), w.t())
+    assert _rel(ops.linear_dx(dy, w), dy.float() @ w.float()) < 1e-2
+    # views outside a registered shadow keep the N-major operand
+    assert ops.WT.get(w.clone(), M) is None
+
+
 # ------------------------------------------------------------------ GEMM ----
 @cuda
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

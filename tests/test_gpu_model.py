@@ -248,6 +248,50 @@ def test_deferred_finishes_bit_identical(monkeypatch, side):
 
 
 @cuda
+def test_weight_copies_dx_step(monkeypatch):
+    """ops.WeightT on a config-3 bf16 train-mode step: every dX product on the K-major weight
+    copies (MIN_ROWS lowered so the decoder's short products take them too) vs the N-major
+    weights -- same gradients (per parameter within 1e-2 relative; the two operand layouts may
+    pick different tile / split-K routes), and a copy-path step after an optimizer update
+    matches the N-major path on the updated weights (the copies were refreshed)."""
+    from capk import ops
+    from capk.models import common
+    from capk.train import CombinedLoss
+    from capk.train.optim import CapkAdamW
+    model, store, cfg, _ = _full_model("bf16")
+    B = 12
+    g = torch.Generator(device="cuda").manual_seed(0)
+    images = torch.randn(B, 3, 224, 224, device="cuda", generator=g)
+    caps = torch.randint(0, 50256, (B, 20), device="cuda", generator=g)
+    model.train()
+    loss_fn = CombinedLoss(50256)
+    monkeypatch.setattr(ops.WeightT, "MIN_ROWS", 1)
+    opt = CapkAdamW(store, lr=1e-3)
+
+    def grads_for(on):
+        monkeypatch.setattr(ops.WT, "enabled", on)
+        common._SEED[0] = seed0
+        out = model(images=images, captions=caps)
+        loss_fn(out["logits"], caps)["total_loss"].backward()
+        torch.cuda.synchronize()
+        return {n: p._capk_grad.clone() for n, p in model.named_parameters() if getattr(p, "_capk_grad", None) is not None}
+
+    def compare(a, b):
+        bad = []
+        for n in a:
+            d = float((a[n] - b[n]).norm() / (b[n].norm() + 1e-20))
+            if d > 1e-2:
+                bad.append((n, d))
+        assert not bad, bad[:10]
+
+    seed0 = common._SEED[0]
+    compare(grads_for(True), grads_for(False))
+    assert len(ops.WT.cache) > 0
+    opt.step()
+    compare(grads_for(True), grads_for(False))
+
+
+@cuda
 def test_decoder_train_mode_dropout_matches_masked_reference(golden_dir):
     """Train-mode decoder (p=0.1 at 7 sites) vs a PyTorch reference applying the SAME masks
     (materialised with capk_dropout_mask from the intercepted per-site seeds): logits and
