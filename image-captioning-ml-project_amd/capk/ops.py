@@ -248,10 +248,47 @@ class WeightT:
 
     def __init__(self):
         self.enabled = os.environ.get("CAPK_WT", "1") != "0"
+        # (opt-in: measured 0.8 % slower on config 3 -- the transposes' 23 k workgroups take the
+        # CUs from the forward's first GEMMs; profiles/round6/weight_copies_ab.txt)
+        self.overlap = os.environ.get("CAPK_WT_OVERLAP", "0") == "1"
         self.epoch = 0
         self.buffers = []  # (weakref of a ParamStore bf16 shadow, start, end)
         self.cache = {}    # (device, ptr, rows, cols, ld) -> [epoch, W^T]
         self.lock = threading.Lock()
+        self.side = {}     # device -> side stream of refresh_async
+        self.pending = {}  # device -> event recorded after its refresh on the side stream
+
+    def refresh_async(self):
+        """Right after an optimizer step: re-transpose every known copy now, on a side stream
+        that waits for the update, so the transposes overlap the next forward; the first dX
+        product (get) and the next shadow write (join, from adamw / refresh_shadow) wait for
+        them.  Opt-in (CAPK_WT_OVERLAP=1); by default the copies are refreshed by that first dX
+        product."""
+        if not (self.enabled and self.overlap) or not torch.cuda.is_available() or \
+                torch.cuda.is_current_stream_capturing():
+            return
+        with self.lock:
+            for dev in {k[0] for k, e in self.cache.items() if e[0] != self.epoch}:
+                side = self.side.get(dev)
+                if side is None:
+                    side = self.side[dev] = torch.cuda.Stream(device=dev)
+                side.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(side):
+                    self._refresh(dev)
+                for k, e in self.cache.items():
+                    if k[0] == dev:
+                        e[1].record_stream(side)
+                ev = torch.cuda.Event()
+                ev.record(side)
+                self.pending[dev] = ev
+
+    def join(self, dev=None):
+        """Make the current stream wait for refreshes still running on the side stream."""
+        if not self.pending:
+            return
+        with self.lock:
+            for d in [d for d in self.pending if dev is None or d == dev]:
+                torch.cuda.current_stream(d).wait_event(self.pending.pop(d))
 
     def register(self, buf):
         """A new ParamStore shadow: its memory may be a freed store's, so every copy goes stale."""
@@ -291,6 +328,9 @@ class WeightT:
                 ent = self.cache[key] = [None, torch.empty(cols, rows, dtype=torch.bfloat16, device=w.device)]
             if ent[0] != self.epoch:
                 self._refresh(w.device)
+            ev = self.pending.pop(w.device, None)
+            if ev is not None:  # (refresh_async)
+                torch.cuda.current_stream(w.device).wait_event(ev)
             return ent[1]
 
     def _refresh(self, dev):
@@ -762,6 +802,8 @@ def act_bwd(dy, aux, act, out=None):
 
 
 def adamw(param, grad, m, v, param_bf16, lr, wd, beta1, beta2, eps, step):
+    if param_bf16 is not None:
+        WT.join(param_bf16.device)  # transposes of the previous weights may still read the shadow
     bc1 = 1.0 - beta1 ** step
     bc2 = 1.0 - beta2 ** step
     check(lib().capk_adamw(param.numel(), _p(param), _p(grad), _p(m), _p(v), _p(param_bf16), float(lr), float(wd),

@@ -198,6 +198,7 @@ class ParamStore:
         """Re-derive the bf16 shadow after the master weights changed outside the optimizer."""
         from . import ops
         ops.FP8.weights_changed()
+        ops.WT.join()
         ops.WT.weights_changed()
         for g in self.groups:
             if self.bf16[g] is not None and self.master[g].is_cuda:

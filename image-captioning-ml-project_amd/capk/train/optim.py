@@ -94,7 +94,8 @@ class CapkAdamW:
                           pg["weight_decay"], self.betas[0], self.betas[1], self.eps, n)
         st.written_optional.clear()
         ops.FP8.weights_changed()  # fp8 weight copies are re-quantised on their next use
-        ops.WT.weights_changed()   # and the K-major dX copies re-transposed (ops.WeightT)
+        ops.WT.weights_changed()   # and the K-major dX copies re-transposed (ops.WeightT),
+        ops.WT.refresh_async()     # now, on a side stream under the next forward
 
     def zero_grad(self, set_to_none=False):
         # capk backward passes overwrite every gradient they produce (no accumulation

@@ -1005,9 +1005,15 @@ struct TrBatch {
 };
 __global__ __launch_bounds__(256) void transpose_batch_kernel(TrBatch b) {
   __shared__ __attribute__((aligned(16))) uint16_t t[64][64 + 8];
-  int k = 0;
-  while (k + 1 < b.n && (int)blockIdx.x >= b.d[k + 1].tile0) ++k;  // (block-uniform)
-  const TrDesc d = b.d[k];
+  // the matrix of this tile: binary search over the tile offsets (a linear scan is a chain of
+  // up to 64 dependent argument loads per workgroup)
+  int lo = 0, hi = b.n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if ((int)blockIdx.x >= b.d[mid].tile0) lo = mid;
+    else hi = mid - 1;
+  }
+  const TrDesc d = b.d[lo];
   const int tile = (int)blockIdx.x - d.tile0;
   const int r0 = (tile / d.tiles_c) * 64, c0 = (tile % d.tiles_c) * 64;
 #pragma unroll

@@ -73,6 +73,17 @@ def test_linear_dx_weight_copy(ops, N, K):
     ops.adamw(master, grad, m, v, shadow[:N * K], 1e-2, 0.0, 0.9, 0.999, 1e-8, 1)
     assert torch.equal(ops.WT.get(w, M), w.t())
     assert _rel(ops.linear_dx(dy, w), dy.float() @ w.float()) < 1e-2
+    # the overlapped refresh (CapkAdamW.step): transposes on a side stream right after the
+    # update, awaited by the next dX product; a second update joins them before rewriting
+    ops.WT.overlap = True
+    try:
+        for _ in range(2):
+            ops.adamw(master, grad, m, v, shadow[:N * K], 1e-2, 0.0, 0.9, 0.999, 1e-8, 2)
+            ops.WT.refresh_async()
+        assert ops.WT.pending
+        assert torch.equal(ops.WT.get(w, M), w.t())
+    finally:
+        ops.WT.overlap = False
     # views outside a registered shadow keep the N-major operand
     assert ops.WT.get(w.clone(), M) is None
 
