@@ -124,7 +124,8 @@ class _DecoderFn(torch.autograd.Function):
         feat_mem, rpb, M_ext = _mem_geometry(features)
         vp = m.visual_projection
         mem = ops.linear(feat_mem, W(vp.weight, dt), vp.bias.detach())  # [M_ext, D]
-        tgt_pad = (captions == m.pad_token_id) if use_pad_mask else None  # bool [B,T] mask bookkeeping
+        # key padding mask, uint8 [B,T] (converted once here, not per layer by attention_fwd)
+        tgt_pad = (captions == m.pad_token_id).to(torch.uint8) if use_pad_mask else None
         # dropout (train mode, p = DecoderConfig.dropout): decoders.py:417 on the embeddings and,
         # per nn.TransformerDecoderLayer, MHA probabilities (self, cross), dropout1/2/3 on the
         # residual branches and the FFN inner dropout.  Masks are hashes of a per-site seed.
