@@ -85,6 +85,18 @@ __global__ __launch_bounds__(256) void ln_fwd_slabs_kernel(int rows, int cols, c
   for (int c = 0; c < MAXC; ++c)
 #pragma unroll
     for (int i = 0; i < 8; ++i) a[c][i] = 0.f;
+  // the bias and residual chunks are requested with the first slab group (loaded after the
+  // slab loop they were two more memory round trips per row); added after the slabs, in the
+  // same order as before
+  float bb[MAXC][8], rr[MAXC][8];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      if (bias) Vec8<float>::load(bias + ch * 8, bb[c]);
+      if (res) Vec8<bf16>::load(res + (int64_t)row * ldr + ch * 8, rr[c]);
+    }
+  }
   for (int k0 = 0; k0 < splits; k0 += 4) {
     float t[MAXC][4][8];
 #pragma unroll
@@ -110,16 +122,12 @@ __global__ __launch_bounds__(256) void ln_fwd_slabs_kernel(int rows, int cols, c
     const int ch = lane + c * 64;
     if (ch < nch) {
       if (bias) {
-        float bb[8];
-        Vec8<float>::load(bias + ch * 8, bb);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) a[c][i] += bb[i];
+        for (int i = 0; i < 8; ++i) a[c][i] += bb[c][i];
       }
       if (res) {
-        float r[8];
-        Vec8<bf16>::load(res + (int64_t)row * ldr + ch * 8, r);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) a[c][i] += r[i];
+        for (int i = 0; i < 8; ++i) a[c][i] += rr[c][i];
       }
       bf16x8 hx;
 #pragma unroll
