@@ -18,6 +18,17 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int cols, const T
   const T* xr = x + (int64_t)row * ldx;
   float v[MAXC][8];
   float s = 0.f;
+  // gamma / beta requested with the row (loaded after the statistics they were a second
+  // memory round trip per row)
+  float wv[MAXC][8], bv[MAXC][8];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      Vec8<float>::load(w + ch * 8, wv[c]);
+      Vec8<float>::load(b + ch * 8, bv[c]);
+    }
+  }
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     const int ch = lane + c * 64;
@@ -44,11 +55,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int cols, const T
   for (int c = 0; c < MAXC; ++c) {
     const int ch = lane + c * 64;
     if (ch < nch) {
-      float wv[8], bv[8], o[8];
-      Vec8<float>::load(w + ch * 8, wv);
-      Vec8<float>::load(b + ch * 8, bv);
+      float o[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) o[i] = (v[c][i] - mean) * rstd * wv[i] + bv[i];
+      for (int i = 0; i < 8; ++i) o[i] = (v[c][i] - mean) * rstd * wv[c][i] + bv[c][i];
       Vec8<T>::store(yr + ch * 8, o);
     }
   }
@@ -88,13 +97,15 @@ __global__ __launch_bounds__(256) void ln_fwd_slabs_kernel(int rows, int cols, c
   // the bias and residual chunks are requested with the first slab group (loaded after the
   // slab loop they were two more memory round trips per row); added after the slabs, in the
   // same order as before
-  float bb[MAXC][8], rr[MAXC][8];
+  float bb[MAXC][8], rr[MAXC][8], wv[MAXC][8], bv[MAXC][8];
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     const int ch = lane + c * 64;
     if (ch < nch) {
       if (bias) Vec8<float>::load(bias + ch * 8, bb[c]);
       if (res) Vec8<bf16>::load(res + (int64_t)row * ldr + ch * 8, rr[c]);
+      Vec8<float>::load(w + ch * 8, wv[c]);  // (gamma / beta likewise)
+      Vec8<float>::load(b + ch * 8, bv[c]);
     }
   }
   for (int k0 = 0; k0 < splits; k0 += 4) {
@@ -157,11 +168,9 @@ __global__ __launch_bounds__(256) void ln_fwd_slabs_kernel(int rows, int cols, c
   for (int c = 0; c < MAXC; ++c) {
     const int ch = lane + c * 64;
     if (ch < nch) {
-      float wv[8], bv[8], o[8];
-      Vec8<float>::load(w + ch * 8, wv);
-      Vec8<float>::load(b + ch * 8, bv);
+      float o[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) o[i] = (v[c][i] - mean) * rstd * wv[i] + bv[i];
+      for (int i = 0; i < 8; ++i) o[i] = (v[c][i] - mean) * rstd * wv[c][i] + bv[c][i];
       Vec8<bf16>::store(yr + ch * 8, o);
     }
   }
